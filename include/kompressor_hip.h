@@ -1,0 +1,191 @@
+/*
+ * kompressor_hip.h -- C-ABI of libkompressor_hip.so, the MI355X (gfx950) engine behind the
+ * drop-in ``kompressor_amd.{image,volume}`` API.
+ *
+ * Conventions
+ *   - Arrays are dense, C-contiguous, channels-last device buffers: volumes [B, D, H, W, C],
+ *     images [B, H, W, C].  ``C`` is the product of all trailing (channel) dims.
+ *   - Every entry point is stream-ordered on ``stream`` (a hipStream_t; NULL = legacy default
+ *     stream), returns 0 on success or a negative kmp_status, and never synchronises the
+ *     device, allocates, or frees memory (graph-capturable).  ``kmp_last_error()`` returns a
+ *     thread-local message for the last failure.
+ *   - Geometry follows the reference: an even spatial dim ``n`` is reflect-padded by one
+ *     (``dims`` = 1), the lowres grid has L = (n + dims + 1) / 2 nodes, L - 1 cells, and the
+ *     stored (trimmed) extent of node-lattice arrays is E = L - dims = ceil(n / 2).
+ *
+ * Each function names the reference interface it replaces (reference @ v1, file:line).  The
+ * reference is pure Python on JAX: "replaces" means the Python function whose semantics the
+ * kernel reproduces; the Python layer in kompressor_amd binds these through ctypes.
+ */
+#ifndef KOMPRESSOR_HIP_H
+#define KOMPRESSOR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* kmp_stream_t; /* ABI-identical to hipStream_t */
+
+typedef enum {
+  KMP_OK = 0,
+  KMP_ERR_ARG = -1,      /* bad pointer, shape, dtype or enum */
+  KMP_ERR_UNSUPPORTED = -2, /* valid request the engine does not implement */
+  KMP_ERR_LAUNCH = -3,   /* HIP launch / runtime error */
+} kmp_status;
+
+typedef enum { KMP_U8 = 0, KMP_U16 = 1, KMP_I32 = 2, KMP_F32 = 3, KMP_U32 = 4 } kmp_dtype;
+
+/* Residual coders, utils.py:28-55 (+ the build's mod-2^32 coder for bit-cast float32). */
+typedef enum { KMP_CODER_RAW = 0, KMP_CODER_U8 = 1, KMP_CODER_U16 = 2, KMP_CODER_U32 = 3 } kmp_coder;
+typedef enum { KMP_ENCODE = 0, KMP_DECODE = 1 } kmp_direction;
+
+typedef enum {
+  /* mean of the (2p+2)^d lowres neighbourhood, cast to the dtype, broadcast to all channels:
+     the reference test predictor, tests/volume/test_encode_decode.py:43-55 */
+  KMP_PRED_MEAN = 0,
+  /* pred[k] = sum_n feat[n] * W[n, k] + b[k] in float32 (MFMA), cast to the dtype
+     (build-defined; fills the reference's predictions_fn slot, volume/encode_decode.py:48) */
+  KMP_PRED_LINEAR = 1,
+} kmp_predictor_kind;
+
+typedef struct {
+  int32_t kind;         /* kmp_predictor_kind */
+  int32_t padding;      /* neighbourhood padding p >= 0 */
+  const float* weights; /* LINEAR: device [N, K] row-major, N = (2p+2)^d, K = 19 (3D) / 5 (2D) */
+  const float* bias;    /* LINEAR: device [K] */
+} kmp_predictor;
+
+/* Sub-box of the output frame [0, E) per spatial axis (z, y, x; 2D uses y, x).  NULL = all.
+   Used by the chunked drivers (encode_decode_chunk.py:77-117): a launch writes exactly the
+   outputs whose block coordinate lies in the box. */
+typedef struct {
+  int64_t begin[3];
+  int64_t end[3];
+} kmp_region;
+
+/* ---------------------------------------------------------------------------------------- */
+/* Library                                                                                   */
+/* ---------------------------------------------------------------------------------------- */
+const char* kmp_version(void);
+const char* kmp_last_error(void);
+/* 1 if the kernels were built for the device's ISA (gfx950) and a device is visible. */
+int kmp_device_ok(void);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Fused encode / decode (one pass over HBM each).                                           */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Replaces volume/encode_decode.py:30-56 ``encode`` for a built-in predictor and coder:
+   pad_highres -> lowres_from_highres -> maps_from_highres -> predictor ->
+   maps_from_predictions -> encode_fn per map -> trim.  ``highres`` [B, D, H, W, C] of
+   ``dtype``; writes ``lowres_out`` [B, Ed, Eh, Ew, C] (dtype) and ``maps_out[7]`` in
+   LR, UD, FB, C, Z, Y, X order with trimmed shapes (volume/utils.py:270-276) in the coder's
+   dtype (RAW -> int32).  ``dims_out[3]`` receives the even-dim padding.  ``workspace`` must
+   hold ``kmp_volume_workspace_bytes`` bytes (may be NULL when that is 0). */
+int kmp_volume_encode(int32_t dtype, const void* highres, int64_t B, int64_t D, int64_t H, int64_t W,
+                      int64_t C, const kmp_predictor* predictor, int32_t coder, void* lowres_out,
+                      void* const maps_out[7], int32_t dims_out[3], const kmp_region* region,
+                      void* workspace, size_t workspace_bytes, kmp_stream_t stream);
+
+/* Replaces volume/encode_decode.py:59-85 ``decode``: pad_lowres/pad_maps -> predictor ->
+   decode_fn per map -> highres_from_lowres_and_maps -> trim.  ``lowres`` [B, Ed, Eh, Ew, C],
+   ``maps[7]`` as produced by kmp_volume_encode, ``dims[3]`` the even padding; writes
+   ``highres_out`` [B, 2Ed-1+dd, 2Eh-1+dh, 2Ew-1+dw, C]. */
+int kmp_volume_decode(int32_t dtype, const void* lowres, const void* const maps[7], int64_t B,
+                      int64_t Ed, int64_t Eh, int64_t Ew, int64_t C, const int32_t dims[3],
+                      const kmp_predictor* predictor, int32_t coder, void* highres_out,
+                      const kmp_region* region, void* workspace, size_t workspace_bytes,
+                      kmp_stream_t stream);
+
+/* Bytes of device workspace the fused calls need for this shape/predictor (0 on the fast path). */
+int64_t kmp_volume_workspace_bytes(int32_t dtype, int64_t B, int64_t D, int64_t H, int64_t W, int64_t C,
+                                   const kmp_predictor* predictor);
+
+/* 2D analogues: image/encode_decode.py:30-85; maps_out[3] in LR, UD, C order. */
+int kmp_image_encode(int32_t dtype, const void* highres, int64_t B, int64_t H, int64_t W, int64_t C,
+                     const kmp_predictor* predictor, int32_t coder, void* lowres_out,
+                     void* const maps_out[3], int32_t dims_out[2], const kmp_region* region,
+                     void* workspace, size_t workspace_bytes, kmp_stream_t stream);
+int kmp_image_decode(int32_t dtype, const void* lowres, const void* const maps[3], int64_t B, int64_t Eh,
+                     int64_t Ew, int64_t C, const int32_t dims[2], const kmp_predictor* predictor,
+                     int32_t coder, void* highres_out, const kmp_region* region, void* workspace,
+                     size_t workspace_bytes, kmp_stream_t stream);
+int64_t kmp_image_workspace_bytes(int32_t dtype, int64_t B, int64_t H, int64_t W, int64_t C,
+                                  const kmp_predictor* predictor);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Primitives (the geometry API re-exported by volume/__init__.py:31-35, image/__init__.py)  */
+/* ``nsp`` = number of spatial axes (2 = image, 3 = volume); ``shape`` holds them z,y,x      */
+/* (image: y,x).                                                                            */
+/* ---------------------------------------------------------------------------------------- */
+
+/* volume/utils.py:77-80, image/utils.py:52-55: out = in[:, ::2, ::2(, ::2)] */
+int kmp_lowres_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3],
+                            int64_t C, void* out, kmp_stream_t stream);
+
+/* volume/utils.py:158-171, image/utils.py:89-96: the 7 (3) parity-class maps, untrimmed. */
+int kmp_maps_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3],
+                          int64_t C, void* const out[7], kmp_stream_t stream);
+
+/* volume/utils.py:37-74, image/utils.py:37-49: [B, cells..., 19 (5), C] training targets. */
+int kmp_targets_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3],
+                             int64_t C, void* out, kmp_stream_t stream);
+
+/* volume/utils.py:174-195, image/utils.py:99-116: interleave lowres [B, L..., C] and the
+   7 (3) maps (shapes as maps_from_highres of a (2L-1)^d grid) into [B, 2L-1..., C]. */
+int kmp_highres_from_lowres_and_maps(int32_t nsp, int32_t dtype, const void* lowres, const void* const maps[7],
+                                     int64_t B, const int64_t lshape[3], int64_t C, void* out,
+                                     kmp_stream_t stream);
+
+/* volume/utils.py:199-210, image/utils.py:120-129: stack of the (2p+2)^d shifted windows of
+   an already padded lowres [B, S..., C] -> [B, S-2p-1..., N, C]. */
+int kmp_features_from_lowres(int32_t nsp, int32_t dtype, const void* lowres, int64_t B, const int64_t shape[3],
+                             int64_t C, int32_t padding, void* out, kmp_stream_t stream);
+
+/* volume/utils.py:83-155, image/utils.py:58-86: float32 aggregation of [B, cells..., K, C]
+   predictions (K = 19 / 5) onto the 7 (3) maps, normalised, cast back to dtype. */
+int kmp_maps_from_predictions(int32_t nsp, int32_t dtype, const void* preds, int64_t B, const int64_t cells[3],
+                              int64_t C, void* const out[7], kmp_stream_t stream);
+
+/* Mean predictor applied to a padded lowres window (the reference test predictor, as used by
+   predictions_fn): == maps_from_predictions(repeat(mean(features_from_lowres(x, p)))) */
+int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B,
+                          const int64_t shape[3], int64_t C, int32_t padding, void* const out[7],
+                          kmp_stream_t stream);
+
+/* Linear predictor on a padded lowres window: per-cell [B, cells..., K, C] predictions in the
+   dtype (MFMA f32), optionally also the f32 pre-cast values (``preds_f32`` may be NULL). */
+int kmp_linear_predict(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],
+                       int64_t C, int32_t padding, const float* weights, const float* bias, void* preds_out,
+                       float* preds_f32, kmp_stream_t stream);
+
+/* jnp.pad on the spatial axes (volume/utils.py:213-260, image/utils.py:132-178):
+   mode 0 = 'symmetric', 1 = 'reflect'.  Negative pads crop (== trim, volume/utils.py:263-276). */
+int kmp_pad(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3], int64_t C,
+            const int64_t pad_lo[3], const int64_t pad_hi[3], int32_t mode, void* out, kmp_stream_t stream);
+
+/* Box copy with dtype conversion -- the slicing and ``.at[box].set`` steps of the chunked
+   driver (volume/encode_decode_chunk.py:101-115): for o in [0, ext) per spatial axis,
+   out[b, out_off + o, c] = cast(in[b, in_off + o, c]).  Integer narrowing wraps; float -> int is
+   the XLA truncating cast. */
+int kmp_copy_box(int32_t nsp, int32_t in_dtype, const void* in, const int64_t in_shape[3], const int64_t in_off[3],
+                 int32_t out_dtype, void* out, const int64_t out_shape[3], const int64_t out_off[3], int64_t B,
+                 int64_t C, const int64_t ext[3], kmp_stream_t stream);
+
+/* Residual coders utils.py:28-55 on n elements.  ``pred_dtype``/``x_dtype`` are the operand
+   dtypes (x = gt for ENCODE, encoded for DECODE); the output is uint8 / uint16 / int32 /
+   uint32 for KMP_CODER_U8 / U16 / RAW / U32. */
+int kmp_code(int32_t direction, int32_t coder, int32_t pred_dtype, const void* pred, int32_t x_dtype,
+             const void* x, int64_t n, void* out, kmp_stream_t stream);
+
+/* Categorical rank coder utils.py:58-111: ``logits`` float32 [n, L]; x/out of ``dtype`` [n]. */
+int kmp_categorical(int32_t direction, const float* logits, int64_t n, int64_t L, int32_t dtype, const void* x,
+                    void* out, kmp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KOMPRESSOR_HIP_H */

@@ -1,0 +1,61 @@
+"""Build ``libkompressor_hip.so`` in-tree with hipcc for gfx950 (no JIT, no torch extension).
+
+``python -m kompressor_amd._build`` or ``__graft_entry__.build()``.  Objects are compiled in
+parallel and cached by source mtime under ``kompressor_amd/build/``.
+"""
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+BUILD = os.path.join(HERE, 'build')
+LIB = os.path.join(HERE, 'libkompressor_hip.so')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wall', '-Wno-unused-function',
+         '-Wno-unused-variable', '-Wno-unused-but-set-variable']
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.hip'))
+
+
+def _headers_mtime():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
+    hs.append(os.path.join(HERE, '..', 'include', 'kompressor_hip.h'))
+    return max(os.path.getmtime(h) for h in hs)
+
+
+def _compile(src, hdr_mtime, verbose):
+    obj = os.path.join(BUILD, os.path.basename(src).replace('.hip', '.o'))
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+        return obj
+    cmd = [HIPCC, *FLAGS, '-c', src, '-o', obj]
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def build(verbose=True, jobs=None):
+    os.makedirs(BUILD, exist_ok=True)
+    hdr = _headers_mtime()
+    srcs = sources()
+    jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB + '.tmp']
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + '.tmp', LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    print(build(verbose='-q' not in sys.argv))

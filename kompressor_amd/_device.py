@@ -1,0 +1,78 @@
+"""Device plumbing: numpy / torch <-> contiguous device tensors, dtype codes, the current stream.
+
+PyTorch-ROCm is used only for device memory, host<->device copies and the stream handle; all
+arithmetic on the hot path runs in ``libkompressor_hip.so``.
+"""
+
+import numpy as np
+import torch
+
+from . import _lib
+
+TORCH_TO_CODE = {torch.uint8: _lib.U8, torch.uint16: _lib.U16, torch.int32: _lib.I32,
+                 torch.float32: _lib.F32, torch.uint32: _lib.U32}
+CODE_TO_TORCH = {v: k for k, v in TORCH_TO_CODE.items()}
+NP_TO_TORCH = {np.dtype(np.uint8): torch.uint8, np.dtype(np.uint16): torch.uint16,
+               np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32,
+               np.dtype(np.uint32): torch.uint32}
+
+_device_checked = False
+
+
+def require_gpu():
+    """Fail loudly unless a gfx950 device is visible (there is no CPU fallback)."""
+    global _device_checked
+    if _device_checked:
+        return
+    if not torch.cuda.is_available():
+        raise RuntimeError('kompressor_amd computes on an MI355X (gfx950) GPU through libkompressor_hip.so; '
+                           'no GPU is visible to this process')
+    if not _lib.lib.kmp_device_ok():
+        raise RuntimeError('kompressor_amd: the visible GPU is not gfx950 (libkompressor_hip.so is built '
+                           'for --offload-arch=gfx950 only)')
+    _device_checked = True
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def is_torch(x):
+    return isinstance(x, torch.Tensor)
+
+
+def to_device(x):
+    """Return ``(tensor, kind)``: a contiguous device tensor and 'torch' / 'numpy' for the result."""
+    require_gpu()
+    if isinstance(x, torch.Tensor):
+        t = x if x.is_cuda else x.to('cuda')
+        return (t if t.is_contiguous() else t.contiguous()), 'torch'
+    a = np.ascontiguousarray(np.asarray(x))
+    if a.dtype not in NP_TO_TORCH:
+        raise TypeError(f'kompressor_amd: unsupported dtype {a.dtype}')
+    return torch.from_numpy(a).to('cuda'), 'numpy'
+
+
+def from_device(t, kind):
+    if kind == 'numpy':
+        return t.cpu().numpy()
+    return t
+
+
+def dtype_code(t):
+    try:
+        return TORCH_TO_CODE[t.dtype]
+    except KeyError:
+        raise TypeError(f'kompressor_amd: unsupported dtype {t.dtype} '
+                        f'(supported: uint8, uint16, int32, uint32, float32)') from None
+
+
+def empty(shape, dtype):
+    return torch.empty(tuple(int(s) for s in shape), dtype=dtype, device='cuda')
+
+
+def prod(shape):
+    p = 1
+    for s in shape:
+        p *= int(s)
+    return p

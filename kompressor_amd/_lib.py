@@ -1,0 +1,122 @@
+"""ctypes binding of ``libkompressor_hip.so`` (the C-ABI in ``include/kompressor_hip.h``).
+
+The shared library is built in-tree by ``kompressor_amd._build`` (``__graft_entry__.build()``).
+Importing this module never falls back to anything: a missing library raises ``ImportError``
+and a missing / non-gfx950 GPU raises ``RuntimeError`` at the first compute call.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('KOMPRESSOR_HIP_LIB', os.path.join(HERE, 'libkompressor_hip.so'))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f'kompressor_amd: {LIB_PATH} is missing -- build it with '
+                      f'`python -m kompressor_amd._build` (hipcc --offload-arch=gfx950)')
+
+lib = ctypes.CDLL(LIB_PATH)
+
+# enums (include/kompressor_hip.h)
+KMP_OK, KMP_ERR_ARG, KMP_ERR_UNSUPPORTED, KMP_ERR_LAUNCH = 0, -1, -2, -3
+U8, U16, I32, F32, U32 = 0, 1, 2, 3, 4
+CODER_RAW, CODER_U8, CODER_U16, CODER_U32 = 0, 1, 2, 3
+ENCODE, DECODE = 0, 1
+PRED_MEAN, PRED_LINEAR = 0, 1
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_vpp = ctypes.POINTER(ctypes.c_void_p)
+_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class Predictor(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('padding', ctypes.c_int32),
+                ('weights', ctypes.c_void_p), ('bias', ctypes.c_void_p)]
+
+
+class Region(ctypes.Structure):
+    _fields_ = [('begin', ctypes.c_int64 * 3), ('end', ctypes.c_int64 * 3)]
+
+
+_PROTOS = {
+    'kmp_version': (ctypes.c_char_p, []),
+    'kmp_last_error': (ctypes.c_char_p, []),
+    'kmp_device_ok': (ctypes.c_int, []),
+    'kmp_volume_encode': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor), _i32,
+                                         _vp, _vpp, _i32p, ctypes.POINTER(Region), _vp, ctypes.c_size_t, _vp]),
+    'kmp_volume_decode': (ctypes.c_int, [_i32, _vp, _vpp, _i64, _i64, _i64, _i64, _i64, _i32p,
+                                         ctypes.POINTER(Predictor), _i32, _vp, ctypes.POINTER(Region), _vp,
+                                         ctypes.c_size_t, _vp]),
+    'kmp_volume_workspace_bytes': (ctypes.c_int64, [_i32, _i64, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor)]),
+    'kmp_image_encode': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor), _i32,
+                                        _vp, _vpp, _i32p, ctypes.POINTER(Region), _vp, ctypes.c_size_t, _vp]),
+    'kmp_image_decode': (ctypes.c_int, [_i32, _vp, _vpp, _i64, _i64, _i64, _i64, _i32p,
+                                        ctypes.POINTER(Predictor), _i32, _vp, ctypes.POINTER(Region), _vp,
+                                        ctypes.c_size_t, _vp]),
+    'kmp_image_workspace_bytes': (ctypes.c_int64, [_i32, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor)]),
+    'kmp_lowres_from_highres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _vp, _vp]),
+    'kmp_maps_from_highres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp]),
+    'kmp_targets_from_highres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _vp, _vp]),
+    'kmp_highres_from_lowres_and_maps': (ctypes.c_int, [_i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _vp, _vp]),
+    'kmp_features_from_lowres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp]),
+    'kmp_maps_from_predictions': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp]),
+    'kmp_mean_predict_maps': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vpp, _vp]),
+    'kmp_linear_predict': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
+    'kmp_pad': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i64p, _i64p, _i32, _vp, _vp]),
+    'kmp_copy_box': (ctypes.c_int, [_i32, _i32, _vp, _i64p, _i64p, _i32, _vp, _i64p, _i64p, _i64, _i64, _i64p,
+                                    _vp]),
+    'kmp_code': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i32, _vp, _i64, _vp, _vp]),
+    'kmp_categorical': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+}
+
+for _name, (_res, _args) in _PROTOS.items():
+    _fn = getattr(lib, _name)  # AttributeError here == the library does not export the C-ABI
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = tuple(_PROTOS)
+
+
+class KompressorHipError(RuntimeError):
+    pass
+
+
+def check(status, what):
+    if status != KMP_OK:
+        msg = lib.kmp_last_error().decode(errors='replace')
+        raise KompressorHipError(f'{what} failed ({status}): {msg}')
+
+
+def version():
+    return lib.kmp_version().decode()
+
+
+# ---------------------------------------------------------------------------------------------
+# small ctypes helpers
+# ---------------------------------------------------------------------------------------------
+
+def i64x3(vals):
+    vals = list(vals) + [0] * (3 - len(vals))
+    return (ctypes.c_int64 * 3)(*vals)
+
+
+def i32xn(vals):
+    vals = list(vals)
+    return (ctypes.c_int32 * max(3, len(vals)))(*(vals + [0] * (3 - len(vals))))
+
+
+def ptrs(tensors, n=7):
+    arr = (ctypes.c_void_p * n)()
+    for i, t in enumerate(tensors):
+        arr[i] = t.data_ptr() if t is not None else None
+    return arr
+
+
+_NP_TO_CODE = {np.dtype(np.uint8): U8, np.dtype(np.uint16): U16, np.dtype(np.int32): I32,
+               np.dtype(np.float32): F32, np.dtype(np.uint32): U32}

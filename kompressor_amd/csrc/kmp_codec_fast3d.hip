@@ -1,0 +1,496 @@
+// kmp_codec_fast3d.hip -- one-pass fused encode / decode for volumes (the metric path).
+//
+// Eligible: C == 1, uint8/uint16, mean predictor with p <= 2, W even with W*sizeof(T) % 16 == 0,
+// (W/2 / VX) * ceil(H/2) <= 1024 threads, 16-B aligned highres, 8-B aligned lowres/maps, and a
+// region (if any) that only restricts z.  Everything else goes to kmp_codec_generic.hip.
+//
+// Output-frame view: output block o = (Z, Y, X) in [0, E)^3 owns the
+// 2x2x2 highres block at 2o; the lowres and the 7 maps are its 8 parity classes, each stored
+// trimmed (volume/utils.py:270-276).  A workgroup owns every (Y, X) of one z-slab of one
+// volume and rolls along z; thread (Y, tx) owns outputs (Y, X..X+VX-1), X = tx*VX, i.e. one
+// 16-byte segment of highres rows 2Y and 2Y+1 in each plane.  Per step j (lowres plane):
+//   1. stream loads for lowres plane j (prefetched one step ahead) and the output plane's
+//      highres rows (encode) or the 7 residual rows (decode);
+//   2. lowres nodes -> LDS ring of R = 2p+2 planes, with the reference's boundary handling
+//      (reflect pad of even dims, volume/utils.py:226-237, and the symmetric neighbourhood pad,
+//      :213-218) done by writing mirrored halo entries -- no extra global reads;
+//   3. cell means of plane c = j-p-1 -> LDS ring of 2 planes (features_from_lowres + mean:
+//      tests/volume/test_encode_decode.py:46-51, integer floor == the f32 mean here);
+//   4. outputs of plane c: the maps_from_predictions aggregation (volume/utils.py:83-155: sums
+//      of 1/2/4 cell means, >> log2(count) == f32 x0.5/x0.25 + truncation for these ranges),
+//      the mod-2^k coder (utils.py:38-55) and 16/8-byte stores.
+// HBM traffic = exactly the algorithmic bytes (each highres / residual byte read or written
+// once) plus one lowres halo plane per slab.
+#include <cstdlib>
+
+#include "kmp_codec.h"
+
+namespace kmp {
+
+constexpr int kColOff = 4;  // LDS column of lowres node / cell x == 0 (room for the left halo)
+
+struct F3 {
+  const void* hi_in;   // encode input highres
+  void* hi_out;        // decode output highres
+  const void* lo_in;   // decode input lowres
+  void* lo_out;        // encode output lowres
+  MapPtrs maps;        // encode outputs / decode inputs
+  int32_t D, H, W;
+  int32_t Lz, Ly, Lx;
+  int32_t Ez, Ey, Ex;
+  int32_t Lcz, Lcy, Lcx;
+  int32_t slab, nslab, zbegin;
+  int32_t txn;
+  int32_t lo_pitch, lo_plane, m_pitch, m_plane;
+};
+
+__device__ __forceinline__ int lsrc(int r, int L, int E) {
+  // lowres source index of padded node r: neighbourhood symmetric pad, then even reflect pad
+  int m = r % (2 * L);
+  if (m < 0) m += 2 * L;
+  m = m < L ? m : 2 * L - 1 - m;
+  int m2 = m % (2 * E);
+  m2 = m2 < E ? m2 : 2 * E - 1 - m2;
+  return m2;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t elem_v16(const uint4& v, int e) {  // element e of a 16-byte vector
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t elem_v8(const uint2& v, int e) {  // element e of an 8-byte vector
+  const uint32_t w[2] = {v.x, v.y};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint2 pack_v8(const uint32_t (&v)[VX]) {
+  if constexpr (sizeof(T) == 2) {
+    return make_uint2((v[0] & 0xffffu) | (v[1] << 16), (v[2] & 0xffffu) | (v[3] << 16));
+  } else {
+    return make_uint2((v[0] & 0xffu) | ((v[1] & 0xffu) << 8) | ((v[2] & 0xffu) << 16) | (v[3] << 24),
+                      (v[4] & 0xffu) | ((v[5] & 0xffu) << 8) | ((v[6] & 0xffu) << 16) | (v[7] << 24));
+  }
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint4 pack_v16(const uint32_t (&ev)[VX], const uint32_t (&od)[VX]) {
+  if constexpr (sizeof(T) == 2) {
+    return make_uint4((ev[0] & 0xffffu) | (od[0] << 16), (ev[1] & 0xffffu) | (od[1] << 16),
+                      (ev[2] & 0xffffu) | (od[2] << 16), (ev[3] & 0xffffu) | (od[3] << 16));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = (ev[2 * q] & 0xffu) | ((od[2 * q] & 0xffu) << 8) | ((ev[2 * q + 1] & 0xffu) << 16) | (od[2 * q + 1] << 24);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <typename V>
+__device__ __forceinline__ V ldg(const void* p) {
+  return *(const V*)p;
+}
+
+template <typename T, int P, bool DEC>
+__global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
+  constexpr int VX = 8 / (int)sizeof(T);  // outputs per thread along x (16 B of highres row)
+  constexpr int R = 2 * P + 2;            // lowres planes in flight
+  constexpr int NB = 2 * P + 2;           // neighbourhood extent
+  constexpr uint32_t N = NB * NB * NB;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* lo_ring = smem;
+  uint32_t* m_ring = smem + R * a.lo_plane;
+
+  const int tid = threadIdx.x;
+  const int tx = tid % a.txn;
+  const int Y = tid / a.txn;
+  const int X = tx * VX;
+  const int64_t b = blockIdx.x / a.nslab;
+  const int Z0 = a.zbegin + (blockIdx.x % a.nslab) * a.slab;
+  int Z1 = Z0 + a.slab;
+  Z1 = Z1 < a.Ez ? Z1 : a.Ez;
+
+  const int64_t hrow = a.W;                      // elements per highres row
+  const int64_t hplane = (int64_t)a.H * a.W;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
+  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
+  const int64_t lplane = (int64_t)a.Ey * a.Ex;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
+
+  const bool vy1 = Y < a.Lcy;  // cell row Y exists (== highres row 2Y+1 exists)
+  const bool vy0 = Y >= 1;     // cell row Y-1 exists
+  const int hx = 2 * X;        // first highres column of this thread
+
+  // Where this thread's lowres nodes must also be written (mirrored halo rows / columns).
+  auto write_nodes = [&](uint32_t* plane, const uint32_t (&nv)[VX]) {
+    auto put_row = [&](int r) {
+      uint32_t* row = plane + (r + P) * a.lo_pitch + kColOff + X;
+      if constexpr (VX == 4) {
+        *(uint4*)row = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+      } else {
+        *(uint4*)row = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+        *(uint4*)(row + 4) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+      }
+      auto pick = [&](int s) {  // nv[s - X] without a runtime-indexed register array
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < VX; ++i) v = (s - X == i) ? nv[i] : v;
+        return v;
+      };
+      for (int q = -P; q < 0; ++q) {
+        const int s = lsrc(q, a.Lx, a.Ex);
+        if (s >= X && s < X + VX) row[q - X] = pick(s);
+      }
+      for (int q = a.Ex; q <= a.Lx - 1 + P; ++q) {
+        const int s = lsrc(q, a.Lx, a.Ex);
+        if (s >= X && s < X + VX) row[q - X] = pick(s);
+      }
+    };
+    put_row(Y);
+    for (int r = -P; r < 0; ++r)
+      if (lsrc(r, a.Ly, a.Ey) == Y) put_row(r);
+    for (int r = a.Ey; r <= a.Ly - 1 + P; ++r)
+      if (lsrc(r, a.Ly, a.Ey) == Y) put_row(r);
+  };
+
+  const int jstart = (Z0 - 1 > 0 ? Z0 - 1 : 0) - P;
+  const int jend = Z1 + P;
+  const int mfirst = Z0 - 1 > 0 ? Z0 - 1 : 0;
+
+  // Prefetched lowres source row for the current step.
+  auto load_lowres_row = [&](int j, uint4& hv, uint2& lv) {
+    const int sz = lsrc(j, a.Lz, a.Ez);
+    if constexpr (DEC) lv = ldg<uint2>(lin + (int64_t)sz * lplane + (int64_t)Y * a.Ex + X);
+    else hv = ldg<uint4>(hin + (int64_t)(2 * sz) * hplane + (int64_t)(2 * Y) * hrow + hx);
+  };
+  uint4 pre_h = make_uint4(0, 0, 0, 0);
+  uint2 pre_l = make_uint2(0, 0);
+  load_lowres_row(jstart, pre_h, pre_l);
+
+  uint4 keep0 = make_uint4(0, 0, 0, 0), keep1 = make_uint4(0, 0, 0, 0);  // encode P==0: plane 2c rows
+  uint2 keep_l = make_uint2(0, 0);                                       // decode P==0: lowres plane c
+
+  for (int j = jstart; j <= jend; ++j) {
+    const int c = j - P - 1;
+    const bool do_m = c >= mfirst && c < a.Lcz;
+    const bool do_out = c >= Z0 && c < Z1;
+    const bool vz1 = c < a.Lcz;  // odd plane 2c+1 exists
+    const bool vz0 = c >= 1;
+
+    const uint4 cur_h = pre_h;
+    const uint2 cur_l = pre_l;
+    if (j < jend) load_lowres_row(j + 1, pre_h, pre_l);
+
+    // ---- stream loads for the output plane ----
+    uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, o0 = e0, o1 = e0;
+    uint2 mv[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
+    uint4 nxt1 = make_uint4(0, 0, 0, 0);
+    if constexpr (!DEC) {
+      if constexpr (P == 0) {
+        if (j >= Z0 && j < Z1 && vy1) nxt1 = ldg<uint4>(hin + (int64_t)(2 * j) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+        if (do_out) {
+          e0 = keep0;
+          e1 = keep1;
+        }
+      } else {
+        if (do_out) {
+          e0 = ldg<uint4>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y) * hrow + hx);
+          if (vy1) e1 = ldg<uint4>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+        }
+      }
+      if (do_out && vz1) {
+        o0 = ldg<uint4>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y) * hrow + hx);
+        if (vy1) o1 = ldg<uint4>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+      }
+    } else {
+      if (do_out) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          int par[3];
+          map_parity(3, k, par);
+          if ((par[0] && !vz1) || (par[1] && !vy1)) continue;
+          const int64_t ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
+          const T* mp = (const T*)a.maps.p[k] + ((b * ez + c) * ey + Y) * a.Ex + X;
+          mv[k] = ldg<uint2>(mp);
+        }
+      }
+    }
+
+    // ---- lowres plane j -> LDS ring ----
+    {
+      uint32_t nv[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) nv[i] = DEC ? elem_v8<T>(cur_l, i) : elem_v16<T>(cur_h, 2 * i);
+      const int slot = ((j % R) + R) % R;
+      write_nodes(lo_ring + slot * a.lo_plane, nv);
+    }
+    if constexpr (!DEC && P == 0) {
+      keep0 = cur_h;
+      keep1 = nxt1;
+    }
+    __syncthreads();
+
+    // ---- cell means of plane c ----
+    if (do_m && vy1) {
+      uint32_t s[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) s[i] = 0;
+#pragma unroll
+      for (int dz = 0; dz < NB; ++dz) {
+        const int slot = (((c - P + dz) % R) + R) % R;
+        const uint32_t* pl = lo_ring + slot * a.lo_plane;
+#pragma unroll
+        for (int dy = 0; dy < NB; ++dy) {
+          const uint32_t* row = pl + (Y + dy) * a.lo_pitch + kColOff + X - P;  // node Y-P+dy
+          uint32_t v[VX + NB - 1];
+#pragma unroll
+          for (int q = 0; q < VX + NB - 1; ++q) v[q] = row[q];
+#pragma unroll
+          for (int i = 0; i < VX; ++i)
+#pragma unroll
+            for (int dx = 0; dx < NB; ++dx) s[i] += v[i + dx];
+        }
+      }
+      uint32_t* mrow = m_ring + (c & 1) * a.m_plane + (Y + 1) * a.m_pitch + kColOff + X;
+      uint32_t mval[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) mval[i] = s[i] / N;
+      if constexpr (VX == 4) {
+        *(uint4*)mrow = make_uint4(mval[0], mval[1], mval[2], mval[3]);
+      } else {
+        *(uint4*)mrow = make_uint4(mval[0], mval[1], mval[2], mval[3]);
+        *(uint4*)(mrow + 4) = make_uint4(mval[4], mval[5], mval[6], mval[7]);
+      }
+    }
+    uint32_t own_lo[VX];
+    if constexpr (DEC) {
+      if constexpr (P == 0) {
+#pragma unroll
+        for (int i = 0; i < VX; ++i) own_lo[i] = elem_v8<T>(keep_l, i);
+        keep_l = cur_l;
+      } else {
+        const int slot = (((c % R) + R) % R);
+        const uint32_t* row = lo_ring + slot * a.lo_plane + (Y + P) * a.lo_pitch + kColOff + X;
+#pragma unroll
+        for (int i = 0; i < VX; ++i) own_lo[i] = row[i];
+      }
+    }
+    __syncthreads();
+
+    if (!do_out) continue;
+
+    // ---- predictions for plane c (cells c-1, c; rows Y-1, Y; cols X-1 .. X+VX-1) ----
+    uint32_t M[2][2][VX + 1];
+    const bool vz[2] = {vz0, vz1};
+    const bool vy[2] = {vy0, vy1};
+    bool vx[VX + 1];
+#pragma unroll
+    for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz) {
+      const uint32_t* pl = m_ring + ((c - 1 + dz) & 1) * a.m_plane;
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const uint32_t* row = pl + (Y + dy) * a.m_pitch + kColOff + X - 1;  // cell row Y-1+dy, col X-1
+        const bool ok = vz[dz] && vy[dy];
+        uint32_t v[VX + 1];
+        v[0] = row[0];
+        if constexpr (VX == 4) {
+          const uint4 w = *(const uint4*)(row + 1);
+          v[1] = w.x; v[2] = w.y; v[3] = w.z; v[4] = w.w;
+        } else {
+          const uint4 w0 = *(const uint4*)(row + 1), w1 = *(const uint4*)(row + 5);
+          v[1] = w0.x; v[2] = w0.y; v[3] = w0.z; v[4] = w0.w;
+          v[5] = w1.x; v[6] = w1.y; v[7] = w1.z; v[8] = w1.w;
+        }
+#pragma unroll
+        for (int q = 0; q <= VX; ++q) M[dz][dy][q] = (ok && vx[q]) ? v[q] : 0u;
+      }
+    }
+    const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+    const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+
+    // pred[k][i] in reference map order LR, UD, FB, C, Z, Y, X
+    uint32_t pred[7][VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pred[0][i] = (M[1][1][i] + M[1][1][i + 1]) >> (nx >> 1);
+      pred[1][i] = (M[1][0][i + 1] + M[1][1][i + 1]) >> (ny >> 1);
+      pred[2][i] = (M[0][1][i + 1] + M[1][1][i + 1]) >> (nz >> 1);
+      pred[3][i] = M[1][1][i + 1];
+      pred[4][i] = (M[1][0][i] + M[1][0][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((ny * nx) >> 1);
+      pred[5][i] = (M[0][1][i] + M[0][1][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((nz * nx) >> 1);
+      pred[6][i] = (M[0][0][i + 1] + M[0][1][i + 1] + M[1][0][i + 1] + M[1][1][i + 1]) >> ((nz * ny) >> 1);
+    }
+
+    if constexpr (!DEC) {
+      // ground truth per class: (plane parity, row parity, x parity) -> vector, element 2i + xpar
+      uint32_t res[7][VX], lov[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        lov[i] = elem_v16<T>(e0, 2 * i);
+        res[0][i] = (elem_v16<T>(o1, 2 * i) - pred[0][i]) & MASK;      // LR (1,1,0)
+        res[1][i] = (elem_v16<T>(o0, 2 * i + 1) - pred[1][i]) & MASK;  // UD (1,0,1)
+        res[2][i] = (elem_v16<T>(e1, 2 * i + 1) - pred[2][i]) & MASK;  // FB (0,1,1)
+        res[3][i] = (elem_v16<T>(o1, 2 * i + 1) - pred[3][i]) & MASK;  // C  (1,1,1)
+        res[4][i] = (elem_v16<T>(o0, 2 * i) - pred[4][i]) & MASK;      // Z  (1,0,0)
+        res[5][i] = (elem_v16<T>(e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
+        res[6][i] = (elem_v16<T>(e0, 2 * i + 1) - pred[6][i]) & MASK;  // X  (0,0,1)
+      }
+      T* lo = (T*)a.lo_out + ((b * a.Ez + c) * a.Ey + Y) * a.Ex + X;
+      *(uint2*)lo = pack_v8<T, VX>(lov);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        int par[3];
+        map_parity(3, k, par);
+        if ((par[0] && !vz1) || (par[1] && !vy1)) continue;
+        const int64_t ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
+        T* mp = (T*)a.maps.p[k] + ((b * ez + c) * ey + Y) * a.Ex + X;
+        *(uint2*)mp = pack_v8<T, VX>(res[k]);
+      }
+    } else {
+      uint32_t dv[7][VX];
+#pragma unroll
+      for (int k = 0; k < 7; ++k)
+#pragma unroll
+        for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + elem_v8<T>(mv[k], i)) & MASK;
+      T* h0 = hout + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y) * hrow + hx;
+      *(uint4*)h0 = pack_v16<T, VX>(own_lo, dv[6]);                    // plane 2c, row 2Y: lowres | X
+      if (vy1) *(uint4*)(h0 + hrow) = pack_v16<T, VX>(dv[5], dv[2]);  // plane 2c, row 2Y+1: Y | FB
+      if (vz1) {
+        T* h1 = h0 + hplane;
+        *(uint4*)h1 = pack_v16<T, VX>(dv[4], dv[1]);                    // plane 2c+1, row 2Y: Z | UD
+        if (vy1) *(uint4*)(h1 + hrow) = pack_v16<T, VX>(dv[0], dv[3]);  // plane 2c+1, row 2Y+1: LR | C
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host: eligibility + launch geometry
+// ------------------------------------------------------------------------------------------
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+template <typename T>
+static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
+                            F3& a, dim3& grid, dim3& block, size_t& lds) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
+  if (env_int("KMP_DISABLE_FAST", 0)) return false;
+  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding > 2) return false;
+  const int P = pred->padding;
+  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[0] > (1 << 30) || g.n[1] > (1 << 30) || g.n[2] > (1 << 30)) return false;
+  const int64_t txn = g.E[2] / VX;
+  if (txn * VX != g.E[2]) return false;
+  const int64_t threads = txn * g.E[1];
+  if (threads > 1024 || threads < 1) return false;
+  int64_t zb = 0, ze = g.E[0];
+  if (region) {
+    if (region->begin[1] > 0 || region->begin[2] > 0 || region->end[1] < g.E[1] || region->end[2] < g.E[2]) return false;
+    zb = region->begin[0] < 0 ? 0 : region->begin[0];
+    ze = region->end[0] > g.E[0] ? g.E[0] : region->end[0];
+    if (ze <= zb) return false;
+  }
+  a.D = (int)g.n[0]; a.H = (int)g.n[1]; a.W = (int)g.n[2];
+  a.Lz = (int)g.L[0]; a.Ly = (int)g.L[1]; a.Lx = (int)g.L[2];
+  a.Ez = (int)g.E[0]; a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
+  a.Lcz = (int)g.Lc[0]; a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
+  a.txn = (int)txn;
+  // LDS: lowres planes rows [-P, Ly-1+P], cols [-P, Lx-1+P] at kColOff; cell planes rows [-1, Lcy), cols [-1, Lcx)
+  a.lo_pitch = (int)((kColOff + g.L[2] + P + VX + 3) / 4 * 4) + 1 * 4;
+  a.lo_plane = (int)(g.L[1] + 2 * P) * a.lo_pitch;
+  a.m_pitch = (int)((kColOff + g.Lc[2] + VX + 3) / 4 * 4) + 4;
+  a.m_plane = (int)((g.Lc[1] > g.E[1] ? g.Lc[1] : g.E[1]) + 1) * a.m_pitch;
+  lds = (size_t)((2 * P + 2) * a.lo_plane + 2 * a.m_plane) * sizeof(uint32_t);
+  if (lds > 64 * 1024) return false;
+  // z slabs: enough workgroups to cover the chip a few times over.
+  const int64_t zext = ze - zb;
+  int64_t want = env_int("KMP_WG_TARGET", 2048);
+  int64_t nslab = ceil_div(want, B > 0 ? B : 1);
+  if (nslab > zext) nslab = zext;
+  if (nslab < 1) nslab = 1;
+  int64_t slab = ceil_div(zext, nslab);
+  const int min_slab = env_int("KMP_MIN_SLAB", 4);
+  if (slab < min_slab) slab = min_slab < zext ? min_slab : zext;
+  nslab = ceil_div(zext, slab);
+  a.slab = (int)slab;
+  a.nslab = (int)nslab;
+  a.zbegin = (int)zb;
+  grid = dim3((unsigned)(B * nslab));
+  block = dim3((unsigned)threads);
+  return B * nslab < (int64_t)1 << 31;
+}
+
+template <typename T>
+int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                    const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
+  if (nsp != 3) return try_fast2d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    F3 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!fast3d_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k)
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+    a.hi_in = hi;
+    a.lo_out = lowres;
+    a.maps = maps;
+    switch (pred->padding) {
+      case 0: fast3d_kernel<T, 0, false><<<grid, block, lds, stream>>>(a); break;
+      case 1: fast3d_kernel<T, 1, false><<<grid, block, lds, stream>>>(a); break;
+      default: fast3d_kernel<T, 2, false><<<grid, block, lds, stream>>>(a); break;
+    }
+    return check_launch("fast3d_encode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                    const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
+  if (nsp != 3) return try_fast2d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    F3 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!fast3d_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k) {
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      a.maps.p[k] = (void*)maps.p[k];
+    }
+    a.hi_out = hi;
+    a.lo_in = lowres;
+    switch (pred->padding) {
+      case 0: fast3d_kernel<T, 0, true><<<grid, block, lds, stream>>>(a); break;
+      case 1: fast3d_kernel<T, 1, true><<<grid, block, lds, stream>>>(a); break;
+      default: fast3d_kernel<T, 2, true><<<grid, block, lds, stream>>>(a); break;
+    }
+    return check_launch("fast3d_decode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+#define KMP_INST(T)                                                                                              \
+  template int try_fast_encode<T>(int, const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,         \
+                                  const MapPtrs&, const kmp_region*, hipStream_t);                               \
+  template int try_fast_decode<T>(int, const T*, const CMapPtrs&, const Geo&, int64_t, int64_t,                  \
+                                  const kmp_predictor*, T*, const kmp_region*, hipStream_t);
+KMP_INST(uint8_t)
+KMP_INST(uint16_t)
+KMP_INST(int32_t)
+KMP_INST(uint32_t)
+
+}  // namespace kmp

@@ -1,0 +1,189 @@
+// kmp_common.h -- shared device/host helpers for libkompressor_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <limits>
+#include <string>
+#include <type_traits>
+
+#include "../../include/kompressor_hip.h"
+
+namespace kmp {
+
+// ------------------------------------------------------------------------------------------
+// Error plumbing: every C entry point returns a kmp_status and leaves a thread-local message.
+// ------------------------------------------------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int status, const std::string& msg);
+int check_launch(const char* what);
+
+#define KMP_REQUIRE(cond, msg)                                         \
+  do {                                                                 \
+    if (!(cond)) return ::kmp::fail(KMP_ERR_ARG, std::string(__func__) + ": " + (msg)); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// dtype traits
+// ------------------------------------------------------------------------------------------
+template <int DT> struct dtype_of;
+template <> struct dtype_of<KMP_U8> { using type = uint8_t; };
+template <> struct dtype_of<KMP_U16> { using type = uint16_t; };
+template <> struct dtype_of<KMP_I32> { using type = int32_t; };
+template <> struct dtype_of<KMP_F32> { using type = float; };
+template <> struct dtype_of<KMP_U32> { using type = uint32_t; };
+
+inline int dtype_size(int dt) {
+  switch (dt) {
+    case KMP_U8: return 1;
+    case KMP_U16: return 2;
+    case KMP_I32: case KMP_F32: case KMP_U32: return 4;
+    default: return 0;
+  }
+}
+
+// Dispatch a runtime dtype to a templated callable: f(T{}) with T the element type.
+template <typename F>
+int dispatch_int_dtype(int dt, F&& f) {  // integer sample dtypes (highres / lowres / maps)
+  switch (dt) {
+    case KMP_U8: return f(uint8_t{});
+    case KMP_U16: return f(uint16_t{});
+    case KMP_I32: return f(int32_t{});
+    case KMP_U32: return f(uint32_t{});
+    default: return fail(KMP_ERR_ARG, "unsupported sample dtype " + std::to_string(dt));
+  }
+}
+template <typename F>
+int dispatch_any_dtype(int dt, F&& f) {
+  if (dt == KMP_F32) return f(float{});
+  return dispatch_int_dtype(dt, f);
+}
+
+// ------------------------------------------------------------------------------------------
+// Reference arithmetic restated on device
+// ------------------------------------------------------------------------------------------
+
+// ``astype(T)`` of a float32 as XLA does it: identity for float;
+// truncation toward zero for integers, saturating at the range, NaN -> 0.
+template <typename T>
+__host__ __device__ __forceinline__ T cast_f32(float v) {
+  if constexpr (std::is_same<T, float>::value) {
+    return v;
+  } else {
+    constexpr double lo = (double)std::numeric_limits<T>::min();
+    constexpr double hi = (double)std::numeric_limits<T>::max();
+    double t = (double)v;
+    if (!(t == t)) return T(0);
+    t = t < 0 ? ceil(t) : floor(t);
+    if (t <= lo) return std::numeric_limits<T>::min();
+    if (t >= hi) return std::numeric_limits<T>::max();
+    return T(t);
+  }
+}
+
+// ``jnp.int32(x)`` on an operand: integers wrap into int32, floats truncate (saturating).
+template <typename T>
+__host__ __device__ __forceinline__ int32_t to_i32(T v) {
+  if constexpr (std::is_same<T, float>::value) return cast_f32<int32_t>(v);
+  else return (int32_t)v;
+}
+
+// Coders: utils.py:28-55.  Every coder is "wrapping int32 add/sub, narrowed to the coder's
+// width": ((a + 2^k) % 2^k) of an int32 equals its low k bits for a floor-mod.
+template <int CODER> struct coder_out;
+template <> struct coder_out<KMP_CODER_RAW> { using type = int32_t; };
+template <> struct coder_out<KMP_CODER_U8> { using type = uint8_t; };
+template <> struct coder_out<KMP_CODER_U16> { using type = uint16_t; };
+template <> struct coder_out<KMP_CODER_U32> { using type = uint32_t; };
+
+template <int CODER>
+__host__ __device__ __forceinline__ typename coder_out<CODER>::type code_encode(int32_t pred, int32_t gt) {
+  return (typename coder_out<CODER>::type)(uint32_t)((uint32_t)gt - (uint32_t)pred);
+}
+template <int CODER>
+__host__ __device__ __forceinline__ typename coder_out<CODER>::type code_decode(int32_t pred, int32_t enc) {
+  return (typename coder_out<CODER>::type)(uint32_t)((uint32_t)pred + (uint32_t)enc);
+}
+
+// numpy/jnp mode='symmetric' source index for any integer i (periodic mirror, period 2n).
+__host__ __device__ __forceinline__ int64_t sym_index(int64_t i, int64_t n) {
+  int64_t m = i % (2 * n);
+  if (m < 0) m += 2 * n;
+  return m < n ? m : 2 * n - 1 - m;
+}
+
+// ------------------------------------------------------------------------------------------
+// Geometry of the reference's single pyramid level (volume/utils.py:226-237, 263-276)
+// ------------------------------------------------------------------------------------------
+struct Geo {
+  int64_t n[3];    // highres extent per spatial axis (unpadded); unused axes = 1
+  int64_t L[3];    // lowres nodes of the padded highres
+  int64_t E[3];    // stored (trimmed) node extent = L - dims
+  int64_t Lc[3];   // cells = L - 1
+  int32_t dims[3]; // even padding
+};
+
+inline Geo make_geo_from_highres(int nsp, const int64_t* sp) {
+  Geo g{};
+  for (int a = 0; a < 3; ++a) {
+    if (a < 3 - nsp) { g.n[a] = 1; g.L[a] = 1; g.E[a] = 1; g.Lc[a] = 1; g.dims[a] = 0; continue; }
+    int64_t n = sp[a - (3 - nsp)];
+    g.n[a] = n;
+    g.dims[a] = (int32_t)((n + 1) % 2);
+    g.L[a] = (n + g.dims[a] + 1) / 2;
+    g.E[a] = g.L[a] - g.dims[a];
+    g.Lc[a] = g.L[a] - 1;
+  }
+  return g;
+}
+
+inline Geo make_geo_from_lowres(int nsp, const int64_t* E, const int32_t* dims) {
+  Geo g{};
+  for (int a = 0; a < 3; ++a) {
+    if (a < 3 - nsp) { g.n[a] = 1; g.L[a] = 1; g.E[a] = 1; g.Lc[a] = 1; g.dims[a] = 0; continue; }
+    int i = a - (3 - nsp);
+    g.E[a] = E[i];
+    g.dims[a] = dims[i];
+    g.L[a] = E[i] + dims[i];
+    g.Lc[a] = g.L[a] - 1;
+    g.n[a] = 2 * g.L[a] - 1 - dims[i];
+  }
+  return g;
+}
+
+// Map tables.  Class 0 is the lowres (all-even) class; classes 1..7 (1..3 in 2D) are the maps
+// in the reference's order.  Parities are (z, y, x); in 2D z is a dummy axis.
+// volume/utils.py:161-169 : LR(1,1,0) UD(1,0,1) FB(0,1,1) C(1,1,1) Z(1,0,0) Y(0,1,0) X(0,0,1)
+// image/utils.py:92-94    : LR(y1,x0) UD(y0,x1) C(y1,x1)
+__host__ __device__ __forceinline__ void map_parity(int nsp, int k, int par[3]) {
+  if (nsp == 3) {
+    const int t[7][3] = {{1, 1, 0}, {1, 0, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    par[0] = t[k][0]; par[1] = t[k][1]; par[2] = t[k][2];
+  } else {
+    const int t[3][2] = {{1, 0}, {0, 1}, {1, 1}};
+    par[0] = 0; par[1] = t[k][0]; par[2] = t[k][1];
+  }
+}
+
+// Extent of map k (0-based, excluding lowres) along axis a in its trimmed (stored) form.
+inline int64_t map_extent(const Geo& g, int nsp, int k, int a) {
+  int par[3];
+  map_parity(nsp, k, par);
+  if (a < 3 - nsp) return 1;
+  return par[a] ? g.Lc[a] : g.E[a];
+}
+
+constexpr int kMaxMaps = 7;
+
+struct MapPtrs {  // passed by value to kernels
+  void* p[kMaxMaps];
+};
+struct CMapPtrs {
+  const void* p[kMaxMaps];
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace kmp

@@ -1,0 +1,106 @@
+"""Built-in predictors: callable ``predictions_fn`` objects that the fused kernels recognise.
+
+The reference leaves the predictor to the caller (``predictions_fn`` slot,
+volume/encode_decode.py:48) and its tests use a "mean of the neighbourhood" double
+(tests/volume/test_encode_decode.py:43-55, tests/image/test_encode_decode.py:43-55).  These
+classes are that predictor (``MeanPredictor``) and a dense per-cell linear predictor
+(``LinearPredictor``, the "learned predictor apply" of the north star).  Called as plain
+``predictions_fn(padded_lowres)`` they return the 7 (3) prediction maps exactly as the
+reference's callback would; passed to ``encode`` / ``decode`` together with a built-in coder
+they run as one fused HIP kernel per direction.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _device as dev
+from . import _lib
+from ._nd import d_mean_predict_maps, d_maps_from_predictions, NPRED, _sp, _ch, _C
+from ._lib import check, lib
+
+
+class MeanPredictor:
+    """``maps_from_predictions(repeat(astype(mean(features_from_lowres(x, p)), dtype)))``."""
+
+    def __init__(self, padding=0, ndim=3):
+        if ndim not in (2, 3):
+            raise ValueError('ndim must be 2 (image) or 3 (volume)')
+        if not isinstance(padding, int) or padding < 0:
+            raise ValueError('padding must be an int >= 0')
+        self.padding, self.ndim = padding, ndim
+
+    def _kmp_predictor(self):
+        return _lib.Predictor(_lib.PRED_MEAN, self.padding, None, None)
+
+    def __call__(self, lowres):
+        t, kind = dev.to_device(lowres)
+        return tuple(dev.from_device(m, kind) for m in d_mean_predict_maps(t, self.padding, self.ndim))
+
+    def __repr__(self):
+        return f'MeanPredictor(padding={self.padding}, ndim={self.ndim})'
+
+
+class LinearPredictor:
+    """``pred[cell, k] = sum_n features[cell, n] * W[n, k] + b[k]`` (float32, MFMA), cast to the
+    sample dtype, then ``maps_from_predictions``.  ``W`` is ``[(2p+2)^ndim, 19 or 5]``."""
+
+    def __init__(self, weights, bias, padding=0, ndim=3):
+        if ndim not in (2, 3):
+            raise ValueError('ndim must be 2 (image) or 3 (volume)')
+        n, k = (2 * padding + 2) ** ndim, NPRED[ndim]
+        w = torch.as_tensor(np.asarray(weights, dtype=np.float32) if not isinstance(weights, torch.Tensor)
+                            else weights, dtype=torch.float32)
+        b = torch.as_tensor(np.asarray(bias, dtype=np.float32) if not isinstance(bias, torch.Tensor)
+                            else bias, dtype=torch.float32)
+        if tuple(w.shape) != (n, k) or tuple(b.shape) != (k,):
+            raise ValueError(f'weights must be [{n}, {k}] and bias [{k}] for padding={padding}, ndim={ndim}')
+        self.padding, self.ndim = padding, ndim
+        self._w_host, self._b_host = w.contiguous(), b.contiguous()
+        self._w = self._b = None
+
+    @property
+    def weights(self):
+        return self._w_host
+
+    @property
+    def bias(self):
+        return self._b_host
+
+    def _device_params(self):
+        if self._w is None:
+            dev.require_gpu()
+            self._w = self._w_host.to('cuda')
+            self._b = self._b_host.to('cuda')
+        return self._w, self._b
+
+    def _kmp_predictor(self):
+        w, b = self._device_params()
+        return _lib.Predictor(_lib.PRED_LINEAR, self.padding, w.data_ptr(), b.data_ptr())
+
+    def predict_cells(self, lowres, with_f32=False):
+        """Per-cell predictions ``[B, cells..., K, C...]`` in the sample dtype (and the f32 pre-cast
+        values if ``with_f32``) for a padded lowres window."""
+        t, kind = dev.to_device(lowres)
+        w, b = self._device_params()
+        nsp = self.ndim
+        S = _sp(t.shape, nsp)
+        cells = [s - 2 * self.padding - 1 for s in S]
+        shape = (t.shape[0], *cells, NPRED[nsp], *_ch(t.shape, nsp))
+        out = dev.empty(shape, t.dtype)
+        f32 = dev.empty(shape, torch.float32) if with_f32 else None
+        check(lib.kmp_linear_predict(nsp, dev.dtype_code(t), t.data_ptr(), t.shape[0], _lib.i64x3(S),
+                                     _C(t.shape, nsp), self.padding, w.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                     f32.data_ptr() if f32 is not None else None, dev.stream()), 'linear_predict')
+        if with_f32:
+            return dev.from_device(out, kind), dev.from_device(f32, kind)
+        return dev.from_device(out, kind)
+
+    def __call__(self, lowres):
+        t, kind = dev.to_device(lowres)
+        cells = self.predict_cells(t)
+        return tuple(dev.from_device(m, kind) for m in d_maps_from_predictions(cells, self.ndim))
+
+    def __repr__(self):
+        return f'LinearPredictor(padding={self.padding}, ndim={self.ndim})'

@@ -1,0 +1,88 @@
+"""Oracle (test infrastructure only): the reference tests' predictor doubles, restated in numpy.
+
+* ``mean_predictions_fn`` -- tests/volume/test_encode_decode.py:43-55 and
+  tests/image/test_encode_decode.py:43-55: mean of the (2p+2)^d neighbourhood in float32,
+  cast to the input dtype, repeated 19x (5x), then ``maps_from_predictions``.
+* ``categorical_predictions_fn`` -- tests/volume/test_encode_decode.py:57-75 and
+  tests/image/test_encode_decode.py:57-74: one constant logit vector tiled everywhere, then
+  ``maps_from_predictions`` and a softmax.  The reference draws the logits with
+  ``jax.random.PRNGKey(1234)``; JAX is absent, so a seeded numpy uniform draw stands in (the
+  reference test checks losslessness and chunk invariance only, which hold for any logits).
+* ``linear_predictions_fn`` -- the build-defined LinearPredictor (no reference counterpart;
+  SURVEY.md §8a row a9'): ``pred[cell, k] = sum_n feat[cell, n] * W[n, k] + b[k]`` in float,
+  cast to the input dtype, then ``maps_from_predictions``.
+"""
+
+import numpy as np
+
+from . import volume as _vol, image as _img
+from .common import cast_from_f32
+
+
+def _ns(ndim):
+    return _vol if ndim == 3 else _img
+
+
+def mean_predictions_fn(padding, ndim=3):
+    ns = _ns(ndim)
+    k = 19 if ndim == 3 else 5
+
+    def predictions_fn(lowres):
+        lowres = np.asarray(lowres)
+        features = ns.features_from_lowres(lowres, padding)
+        axis = ndim + 1
+        pred = np.mean(features.astype(np.float32), axis=axis, keepdims=True, dtype=np.float32)
+        pred = cast_from_f32(pred, lowres.dtype)
+        pred = np.repeat(pred, k, axis=axis)
+        return ns.maps_from_predictions(pred)
+
+    return predictions_fn
+
+
+def categorical_logits(ndim, channels, classes, seed=1234):
+    k = 19 if ndim == 3 else 5
+    rng = np.random.default_rng(seed)
+    return rng.uniform(size=(k, *channels, classes)).astype(np.float32)
+
+
+def categorical_predictions_fn(padding, classes, ndim=3, seed=1234):
+    ns = _ns(ndim)
+
+    def predictions_fn(lowres):
+        lowres = np.asarray(lowres)
+        ch = lowres.shape[ndim + 1:]
+        logits = categorical_logits(ndim, ch, classes, seed)
+        cells = tuple(s - 1 - 2 * padding for s in lowres.shape[1:ndim + 1])
+        pred = np.broadcast_to(logits, (lowres.shape[0], *cells, *logits.shape)).copy()
+        maps = ns.maps_from_predictions(pred)
+        out = []
+        for m in maps:
+            e = np.exp(m - m.max(axis=-1, keepdims=True))
+            out.append((e / e.sum(axis=-1, keepdims=True)).astype(np.float32))
+        return out
+
+    return predictions_fn
+
+
+def linear_predictions(features, weights, bias, dtype):
+    """Per-cell linear predictor on ``features [.., N, C]`` -> ``[.., K, C]`` (float64 math, then the
+    XLA-style cast).  Used as the 1e-5 tolerance reference for the HIP MFMA predictor."""
+    f = features.astype(np.float64)
+    w = np.asarray(weights, np.float64)
+    b = np.asarray(bias, np.float64)
+    n_axis = f.ndim - 2
+    pred = np.moveaxis(np.tensordot(np.moveaxis(f, n_axis, -1), w, axes=([-1], [0])), -1, n_axis)
+    pred = pred + b.reshape((-1, 1))
+    return pred, cast_from_f32(pred.astype(np.float32), dtype)
+
+
+def linear_predictions_fn(padding, weights, bias, ndim=3):
+    ns = _ns(ndim)
+
+    def predictions_fn(lowres):
+        lowres = np.asarray(lowres)
+        features = ns.features_from_lowres(lowres, padding)
+        _, pred = linear_predictions(features, weights, bias, lowres.dtype)
+        return ns.maps_from_predictions(pred)
+
+    return predictions_fn

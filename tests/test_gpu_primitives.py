@@ -1,0 +1,133 @@
+"""HIP geometry primitives and coders vs the CPU oracle (bit-exact), volume and image."""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden, ramp
+
+pytestmark = pytest.mark.gpu
+
+SHAPES3 = [(2, 17, 17, 17, 1), (2, 16, 16, 16, 1), (1, 9, 10, 12, 3), (2, 5, 4, 7, 2, 2)]
+SHAPES2 = [(2, 17, 17, 3), (2, 16, 16, 3), (1, 33, 20, 1), (3, 7, 4, 2, 2)]
+
+
+def _pair(kom, ndim):
+    return (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+
+
+def _rand(shape, dtype, seed=0):
+    info = np.iinfo(dtype)
+    return np.random.default_rng(seed).integers(info.min, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
+
+
+def _eq(a, b):
+    a = a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert a.dtype == b.dtype, (a.dtype, b.dtype)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize('ndim,shape', [(3, s) for s in SHAPES3] + [(2, s) for s in SHAPES2])
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32])
+def test_gathers_and_scatter(kom, ndim, shape, dtype):
+    ns, ons = _pair(kom, ndim)
+    hi = _rand(shape, dtype)
+    _eq(ns.lowres_from_highres(hi), ons.lowres_from_highres(hi))
+    for a, b in zip(ns.maps_from_highres(hi), ons.maps_from_highres(hi)):
+        _eq(a, b)
+    if all(s % 2 == 1 for s in shape[1:1 + ndim]):
+        _eq(ns.targets_from_highres(hi), ons.targets_from_highres(hi))
+        lo, maps = ons.lowres_from_highres(hi), ons.maps_from_highres(hi)
+        _eq(ns.highres_from_lowres_and_maps(lo, maps), hi)
+
+
+@pytest.mark.parametrize('ndim', [3, 2])
+@pytest.mark.parametrize('padding', [0, 1, 2, 3])
+def test_features_and_pads(kom, ndim, padding):
+    ns, ons = _pair(kom, ndim)
+    hi = ramp((2, 17, 17, 17, 1) if ndim == 3 else (2, 17, 17, 3), 65536 if ndim == 3 else 256,
+              np.uint16 if ndim == 3 else np.uint8)
+    lo = ons.lowres_from_highres(hi)
+    padded = ons.pad_neighborhood(lo, padding)
+    _eq(ns.pad_neighborhood(lo, padding), padded)
+    _eq(ns.features_from_lowres(padded, padding), ons.features_from_lowres(padded, padding))
+
+
+@pytest.mark.parametrize('ndim,shape', [(3, (2, 16, 15, 14, 1)), (3, (1, 6, 6, 6, 2)), (2, (2, 16, 15, 3)),
+                                        (2, (1, 4, 6, 1))])
+def test_even_pad_and_trim(kom, ndim, shape):
+    ns, ons = _pair(kom, ndim)
+    hi = _rand(shape, np.uint16)
+    (a, da), (b, db) = ns.utils.pad_highres(hi), ons.pad_highres(hi)
+    assert tuple(da) == tuple(db)
+    _eq(a, b)
+    lo = ons.lowres_from_highres(b)
+    trimmed = ons.trim(lo, db)
+    _eq(ns.utils.trim(lo, db), trimmed)
+    _eq(ns.utils.pad_lowres(trimmed, db), ons.pad_lowres(trimmed, db))
+    maps = ons.trim_maps(ons.maps_from_highres(b), db)
+    for x, y in zip(ns.utils.pad_maps(maps, db), ons.pad_maps(maps, db)):
+        _eq(x, y)
+    for x, y in zip(ns.utils.trim_maps(ons.maps_from_highres(b), db), maps):
+        _eq(x, y)
+
+
+@pytest.mark.parametrize('name', ['mfp_vol_f32', 'mfp_vol_i32', 'mfp_vol_u16', 'mfp_img_f32', 'mfp_img_u8'])
+def test_maps_from_predictions_golden(kom, name):
+    g = load_golden(name)
+    ns = kom.volume if int(g['ndim']) == 3 else kom.image
+    out = ns.maps_from_predictions(g['predictions'])
+    for i, m in enumerate(out):
+        _eq(m, g[f'map{i}'])
+
+
+@pytest.mark.parametrize('ndim', [3, 2])
+def test_maps_from_predictions_targets_identity(kom, ndim):
+    # tests/volume/test_utils.py:275-291: targets -> maps_from_predictions -> reconstruction
+    ns, ons = _pair(kom, ndim)
+    hi = ramp((2, 17, 17, 17, 1) if ndim == 3 else (2, 17, 17, 3), 65536, np.uint16)
+    lo = ns.lowres_from_highres(hi)
+    maps = ns.maps_from_predictions(ns.targets_from_highres(hi))
+    _eq(ns.highres_from_lowres_and_maps(lo, maps), hi)
+
+
+CODER_DTYPES = [np.uint8, np.uint16, np.int32]
+
+
+@pytest.mark.parametrize('coder', ['raw', 'uint8', 'uint16'])
+@pytest.mark.parametrize('pdt', CODER_DTYPES + [np.float32])
+@pytest.mark.parametrize('xdt', CODER_DTYPES)
+def test_coders(kom, coder, pdt, xdt):
+    n = 4097
+    if pdt == np.float32:
+        pred = (np.random.default_rng(1).standard_normal(n) * 300).astype(np.float32)
+    else:
+        pred = _rand((n,), pdt, 1)
+    x = _rand((n,), xdt, 2)
+    enc = getattr(kom.utils, f'encode_values_{coder}')
+    dec = getattr(kom.utils, f'decode_values_{coder}')
+    _eq(enc(pred, x), getattr(oracle.common, f'encode_values_{coder}')(pred, x))
+    _eq(dec(pred, x), getattr(oracle.common, f'decode_values_{coder}')(pred, x))
+
+
+def test_coders_keep_torch(kom):
+    x = torch.arange(100, dtype=torch.int32, device='cuda').to(torch.uint8)
+    out = kom.utils.encode_values_uint8(x, x)
+    assert isinstance(out, torch.Tensor) and out.is_cuda and out.dtype == torch.uint8
+    assert int(out.to(torch.int32).sum()) == 0
+
+
+@pytest.mark.parametrize('ndim', [3, 2])
+@pytest.mark.parametrize('padding', [0, 1, 2])
+def test_mean_predictor_callable(kom, ndim, padding):
+    ns, ons = _pair(kom, ndim)
+    hi = _rand((2, 13, 12, 11, 1) if ndim == 3 else (2, 13, 12, 2), np.uint16, 5)
+    lo = ons.lowres_from_highres(ons.pad_highres(hi)[0])
+    window = ons.pad_neighborhood(lo, padding)
+    got = kom.MeanPredictor(padding, ndim)(window)
+    want = oracle.predictors.mean_predictions_fn(padding, ndim)(window)
+    for a, b in zip(got, want):
+        _eq(a, b)

@@ -1,0 +1,141 @@
+"""CPU-only checks of the product package: host logic and the C-ABI library (no GPU compute)."""
+
+import ast
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT
+
+
+def test_library_exports_every_header_symbol():
+    import kompressor_amd._lib as L
+    header = open(os.path.join(ROOT, 'include', 'kompressor_hip.h')).read()
+    declared = set(re.findall(r'^\s*(?:const char\*|int64_t|int)\s+(kmp_\w+)\s*\(', header, re.M))
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(L.lib, name), name
+    assert set(L.EXPORTED) >= declared
+    assert 'gfx950' in L.version()
+
+
+def test_package_imports_and_version():
+    import kompressor_amd as kom
+    assert isinstance(kom.VERSION, str)  # tests/test_import_module.py:36-40
+    for ns in (kom.volume, kom.image):
+        for name in ('encode', 'decode', 'encode_chunks', 'decode_chunks', 'targets_from_highres',
+                     'lowres_from_highres', 'maps_from_predictions', 'maps_from_highres',
+                     'highres_from_lowres_and_maps', 'features_from_lowres', 'pad_neighborhood',
+                     'encode_values_raw', 'decode_values_raw', 'encode_values_uint8', 'decode_values_uint8',
+                     'encode_values_uint16', 'decode_values_uint16', 'encode_categorical', 'decode_categorical',
+                     'mean_squared_error', 'mean_abs_error', 'mean_charbonnier_error', 'mean_total_variation'):
+            assert callable(getattr(ns, name)), name
+        for name in ('validate_highres', 'validate_lowres', 'validate_chunk', 'validate_padding', 'yield_chunks',
+                     'pad_highres', 'pad_lowres', 'pad_map', 'pad_maps', 'trim', 'trim_maps'):
+            assert callable(getattr(ns.utils, name)), name
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, 'kompressor_amd')
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith('.py'):
+                tree = ast.parse(open(os.path.join(dirpath, f)).read())
+                for node in ast.walk(tree):
+                    if isinstance(node, ast.Import):
+                        assert not any(a.name.split('.')[0] == 'oracle' for a in node.names), f
+                    if isinstance(node, ast.ImportFrom) and node.module:
+                        assert node.module.split('.')[0] != 'oracle', f
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+    import kompressor_amd as kom
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is visible')
+    with pytest.raises(RuntimeError, match='GPU'):
+        kom.volume.lowres_from_highres(np.zeros((1, 3, 3, 3, 1), np.uint16))
+
+
+@pytest.mark.parametrize('max_value', [1, 2, 5, 16, 17, 33, 257])
+@pytest.mark.parametrize('chunk', [4, 5, 6, 11, 32])
+def test_yield_chunks_matches_oracle(max_value, chunk):
+    import kompressor_amd as kom
+    assert list(kom.utils.yield_chunks(max_value, chunk)) == list(oracle.common.yield_chunks(max_value, chunk))
+
+
+def test_validators_volume():
+    # tests/volume/test_utils.py:347-444 re-expressed against kompressor_amd
+    import kompressor_amd as kom
+    V = kom.volume.utils
+    z = lambda s: np.zeros(s, np.uint16)  # noqa: E731
+    with pytest.raises(AssertionError):
+        V.validate_highres(z((2, 3, 3, 3)))
+    with pytest.raises(AssertionError):
+        V.validate_highres(z((0, 3, 3, 3, 1)))
+    for s in [(0, 0, 0), (1, 1, 1), (2, 2, 2), (2, 2, 3), (2, 3, 2), (3, 2, 2), (4, 4, 4), (6, 6, 6)]:
+        with pytest.raises(AssertionError):
+            V.validate_highres(z((2, *s, 3)))
+    for s in [(3, 3, 3), (3, 3, 5), (3, 5, 3), (5, 3, 3)]:
+        assert V.validate_highres(z((2, *s, 3))) == s
+    for s in [(0, 0, 0), (1, 1, 1), (1, 1, 2), (1, 2, 1), (2, 1, 1)]:
+        with pytest.raises(AssertionError):
+            V.validate_lowres(z((2, *s, 3)))
+    for s in [(2, 2, 2), (2, 2, 3), (2, 3, 2), (3, 2, 2)]:
+        assert V.validate_lowres(z((2, *s, 3))) == s
+    for p in [None, -2, -1, 1.0]:
+        with pytest.raises(Exception):
+            V.validate_padding(p)
+    for p in [0, 1]:
+        V.validate_padding(p)
+    for c in [(4,), (4, 4), (4, 4, 4, 4), None, (None, 4, 4), (4, None, 4), (4, 4, None), 3, (3, 4, 4),
+              (4, 3, 4), (4, 4, 3)]:
+        with pytest.raises(Exception):
+            V.validate_chunk(c)
+    for c in [4, 5, (4, 4, 5), (4, 5, 4), (5, 4, 4)]:
+        assert len(V.validate_chunk(c)) == 3
+
+
+def test_validators_image():
+    import kompressor_amd as kom
+    I = kom.image.utils  # noqa: E741
+    z = lambda s: np.zeros(s, np.uint8)  # noqa: E731
+    with pytest.raises(AssertionError):
+        I.validate_highres(z((2, 3, 3)))
+    for s in [(0, 0), (1, 1), (2, 2), (2, 3), (3, 2), (4, 4)]:
+        with pytest.raises(AssertionError):
+            I.validate_highres(z((2, *s, 3)))
+    assert I.validate_highres(z((2, 3, 5, 3))) == (3, 5)
+    for s in [(1, 1), (1, 2), (2, 1)]:
+        with pytest.raises(AssertionError):
+            I.validate_lowres(z((2, *s, 3)))
+    assert I.validate_lowres(z((2, 2, 3, 3))) == (2, 3)
+    for c in [(4,), (4, 4, 4), None, (None, 4), 3, (3, 4)]:
+        with pytest.raises(Exception):
+            I.validate_chunk(c)
+    assert I.validate_chunk(5) == (5, 5)
+
+
+def test_encode_validates_before_touching_the_device():
+    import kompressor_amd as kom
+    pred = kom.MeanPredictor(0, 3)
+    with pytest.raises(AssertionError):
+        kom.volume.encode(pred, kom.volume.encode_values_uint16, np.zeros((2, 1, 3, 3, 1), np.uint16))
+    with pytest.raises(AssertionError):
+        kom.volume.encode(pred, kom.volume.encode_values_uint16, np.zeros((2, 3, 3, 3, 1), np.uint16), padding=-1)
+    with pytest.raises(AssertionError):
+        kom.image.encode(kom.MeanPredictor(0, 2), kom.image.encode_values_uint8, np.zeros((2, 3, 3), np.uint8))
+
+
+def test_encoded_shapes_match_oracle():
+    import kompressor_amd as kom
+    for shape in [(2, 17, 17, 17, 1), (2, 16, 16, 16, 1), (1, 9, 10, 12, 3), (512, 64, 64, 64, 1)]:
+        lo, maps, dims = kom._nd.encoded_shapes(shape, 3)
+        o_hi, o_dims = oracle.volume.pad_highres(np.zeros((1, *shape[1:]), np.uint8))
+        o_lo = oracle.volume.trim(oracle.volume.lowres_from_highres(o_hi), o_dims)
+        o_maps = oracle.volume.trim_maps(oracle.volume.maps_from_highres(o_hi), o_dims)
+        assert dims == o_dims and lo[1:] == o_lo.shape[1:]
+        assert [m[1:] for m in maps] == [m.shape[1:] for m in o_maps]
