@@ -28,8 +28,9 @@ def require_gpu():
         raise RuntimeError('kompressor_amd computes on an MI355X (gfx950) GPU through libkompressor_hip.so; '
                            'no GPU is visible to this process')
     if not _lib.lib.kmp_device_ok():
-        raise RuntimeError('kompressor_amd: the visible GPU is not gfx950 (libkompressor_hip.so is built '
-                           'for --offload-arch=gfx950 only)')
+        arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+        raise RuntimeError(f'kompressor_amd: libkompressor_hip.so (gfx950 only) cannot run on the visible GPU '
+                           f'({arch}): {_lib.lib.kmp_last_error().decode(errors="replace")}')
     _device_checked = True
 
 

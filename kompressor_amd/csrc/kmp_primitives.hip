@@ -346,12 +346,21 @@ const char* kmp_version(void) { return "kompressor_hip 0.1.0 (gfx950)"; }
 const char* kmp_last_error(void) { return g_last_error.c_str(); }
 
 int kmp_device_ok(void) {
+  // The real requirement: this library's code object loads on the current device (gfx950).
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
-  int dev = 0;
-  hipDeviceProp_t prop;
-  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-  return std::string(prop.gcnArchName).rfind("gfx950", 0) == 0 ? 1 : 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    set_error(std::string("no HIP device visible: ") + hipGetErrorString(e));
+    return 0;
+  }
+  hipFuncAttributes attr;
+  e = hipFuncGetAttributes(&attr, (const void*)&pad_kernel<uint8_t>);
+  if (e != hipSuccess) {
+    set_error(std::string("libkompressor_hip has no code object for this device (built for gfx950): ") +
+              hipGetErrorString(e));
+    return 0;
+  }
+  return 1;
 }
 
 int kmp_lowres_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3],
