@@ -9,6 +9,12 @@ import ctypes
 import os
 
 import numpy as np
+# torch must be imported BEFORE the CDLL below: torch ships its own libamdhip64.so (SONAME
+# libamdhip64.so.7); loaded first, our library's NEEDED libamdhip64.so.7 binds to that same
+# runtime, so torch's allocations, streams and events and our launches share ONE HIP runtime.
+# Loaded the other way round the process would carry two runtimes and the second to initialise
+# sees no GPU.
+import torch  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('KOMPRESSOR_HIP_LIB', os.path.join(HERE, 'libkompressor_hip.so'))
