@@ -83,14 +83,16 @@ def cpu_baseline(spec, host, padding, ntiles):
                       f'{len(os.sched_getaffinity(0))} cores), median of 2 after warm-up, {t:.2f} s/round'}
 
 
-def load_traffic(workload, padding):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+def load_traffic(workload, padding, kernel):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, collected by separate --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    same command), or None when no such measurement exists."""
     path = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        data = json.load(f)
-    return data.get(f'{workload}_p{padding}')
+        entry = json.load(f).get(f'{workload}_p{padding}', {}).get(kernel)
+    return entry['hbm_bytes'] if entry else None
 
 
 def main():
@@ -166,7 +168,7 @@ def main():
     algo = 2 * raw
     dominant, t_dom = ('encode', t_enc) if t_enc >= t_dec else ('decode', t_dec)
     achieved = algo / t_dom / 1e9
-    traffic = load_traffic(args.workload, args.padding)
+    traffic = load_traffic(args.workload, args.padding, dominant)
 
     # C4: shard one volume's tiles over the ranks, code them, all-gather the decoded tiles
     c4 = None

@@ -89,12 +89,49 @@ __device__ __forceinline__ uint4 pack_v16(const uint32_t (&ev)[VX], const uint32
   }
 }
 
-template <typename V>
-__device__ __forceinline__ V ldg(const void* p) {
-  return *(const V*)p;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Streaming global access.  NT = 1 marks every highres / residual byte as non-temporal (each is
+// touched exactly once per pass), NT = 0 uses the default cache policy.
+template <int NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <int NT>
+__device__ __forceinline__ uint2 ld8(const void* p) {
+  if constexpr (NT) {
+    const u32x2 v = __builtin_nontemporal_load((const u32x2*)p);
+    return make_uint2(v.x, v.y);
+  } else {
+    return *(const uint2*)p;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr (NT) {
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u32x4*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st8(void* p, uint2 v) {
+  if constexpr (NT) {
+    u32x2 w = {v.x, v.y};
+    __builtin_nontemporal_store(w, (u32x2*)p);
+  } else {
+    *(uint2*)p = v;
+  }
 }
 
-template <typename T, int P, bool DEC>
+template <typename T, int P, bool DEC, int NT>
 __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
   constexpr int VX = 8 / (int)sizeof(T);  // outputs per thread along x (16 B of highres row)
   constexpr int R = 2 * P + 2;            // lowres planes in flight
@@ -164,8 +201,8 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
   // Prefetched lowres source row for the current step.
   auto load_lowres_row = [&](int j, uint4& hv, uint2& lv) {
     const int sz = lsrc(j, a.Lz, a.Ez);
-    if constexpr (DEC) lv = ldg<uint2>(lin + (int64_t)sz * lplane + (int64_t)Y * a.Ex + X);
-    else hv = ldg<uint4>(hin + (int64_t)(2 * sz) * hplane + (int64_t)(2 * Y) * hrow + hx);
+    if constexpr (DEC) lv = ld8<NT>(lin + (int64_t)sz * lplane + (int64_t)Y * a.Ex + X);
+    else hv = ld16<NT>(hin + (int64_t)(2 * sz) * hplane + (int64_t)(2 * Y) * hrow + hx);
   };
   uint4 pre_h = make_uint4(0, 0, 0, 0);
   uint2 pre_l = make_uint2(0, 0);
@@ -193,20 +230,20 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
     uint4 nxt1 = make_uint4(0, 0, 0, 0);
     if constexpr (!DEC) {
       if constexpr (P == 0) {
-        if (j >= Z0 && j < Z1 && vy1) nxt1 = ldg<uint4>(hin + (int64_t)(2 * j) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+        if (j >= Z0 && j < Z1 && vy1) nxt1 = ld16<NT>(hin + (int64_t)(2 * j) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
         if (do_out) {
           e0 = keep0;
           e1 = keep1;
         }
       } else {
         if (do_out) {
-          e0 = ldg<uint4>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y) * hrow + hx);
-          if (vy1) e1 = ldg<uint4>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+          e0 = ld16<NT>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y) * hrow + hx);
+          if (vy1) e1 = ld16<NT>(hin + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
         }
       }
       if (do_out && vz1) {
-        o0 = ldg<uint4>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y) * hrow + hx);
-        if (vy1) o1 = ldg<uint4>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
+        o0 = ld16<NT>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y) * hrow + hx);
+        if (vy1) o1 = ld16<NT>(hin + (int64_t)(2 * c + 1) * hplane + (int64_t)(2 * Y + 1) * hrow + hx);
       }
     } else {
       if (do_out) {
@@ -217,7 +254,7 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
           if ((par[0] && !vz1) || (par[1] && !vy1)) continue;
           const int64_t ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
           const T* mp = (const T*)a.maps.p[k] + ((b * ez + c) * ey + Y) * a.Ex + X;
-          mv[k] = ldg<uint2>(mp);
+          mv[k] = ld8<NT>(mp);
         }
       }
     }
@@ -345,7 +382,7 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
         res[6][i] = (elem_v16<T>(e0, 2 * i + 1) - pred[6][i]) & MASK;  // X  (0,0,1)
       }
       T* lo = (T*)a.lo_out + ((b * a.Ez + c) * a.Ey + Y) * a.Ex + X;
-      *(uint2*)lo = pack_v8<T, VX>(lov);
+      st8<NT>(lo, pack_v8<T, VX>(lov));
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         int par[3];
@@ -353,7 +390,7 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
         if ((par[0] && !vz1) || (par[1] && !vy1)) continue;
         const int64_t ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
         T* mp = (T*)a.maps.p[k] + ((b * ez + c) * ey + Y) * a.Ex + X;
-        *(uint2*)mp = pack_v8<T, VX>(res[k]);
+        st8<NT>(mp, pack_v8<T, VX>(res[k]));
       }
     } else {
       uint32_t dv[7][VX];
@@ -362,12 +399,12 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
 #pragma unroll
         for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + elem_v8<T>(mv[k], i)) & MASK;
       T* h0 = hout + (int64_t)(2 * c) * hplane + (int64_t)(2 * Y) * hrow + hx;
-      *(uint4*)h0 = pack_v16<T, VX>(own_lo, dv[6]);                    // plane 2c, row 2Y: lowres | X
-      if (vy1) *(uint4*)(h0 + hrow) = pack_v16<T, VX>(dv[5], dv[2]);  // plane 2c, row 2Y+1: Y | FB
+      st16<NT>(h0, pack_v16<T, VX>(own_lo, dv[6]));                  // plane 2c, row 2Y: lowres | X
+      if (vy1) st16<NT>(h0 + hrow, pack_v16<T, VX>(dv[5], dv[2]));  // plane 2c, row 2Y+1: Y | FB
       if (vz1) {
         T* h1 = h0 + hplane;
-        *(uint4*)h1 = pack_v16<T, VX>(dv[4], dv[1]);                    // plane 2c+1, row 2Y: Z | UD
-        if (vy1) *(uint4*)(h1 + hrow) = pack_v16<T, VX>(dv[0], dv[3]);  // plane 2c+1, row 2Y+1: LR | C
+        st16<NT>(h1, pack_v16<T, VX>(dv[4], dv[1]));                  // plane 2c+1, row 2Y: Z | UD
+        if (vy1) st16<NT>(h1 + hrow, pack_v16<T, VX>(dv[0], dv[3]));  // plane 2c+1, row 2Y+1: LR | C
       }
     }
   }
@@ -416,7 +453,7 @@ static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   if (lds > 64 * 1024) return false;
   // z slabs: enough workgroups to cover the chip a few times over.
   const int64_t zext = ze - zb;
-  int64_t want = env_int("KMP_WG_TARGET", 2048);
+  int64_t want = env_int("KMP_WG_TARGET", 4096);  // >= 16 slabs / CU: latency hiding beats halo re-reads
   int64_t nslab = ceil_div(want, B > 0 ? B : 1);
   if (nslab > zext) nslab = zext;
   if (nslab < 1) nslab = 1;
@@ -430,6 +467,19 @@ static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   grid = dim3((unsigned)(B * nslab));
   block = dim3((unsigned)threads);
   return B * nslab < (int64_t)1 << 31;
+}
+
+template <typename T, bool DEC>
+static void launch_fast3d(int P, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const F3& a) {
+  const bool nt = env_int("KMP_NT", 1) != 0;  // measured: NT 1-2 % faster (profiles/round1/sweep_volume_p0.log)
+  switch (P * 2 + (nt ? 1 : 0)) {
+    case 0: fast3d_kernel<T, 0, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    case 1: fast3d_kernel<T, 0, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+    case 2: fast3d_kernel<T, 1, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    case 3: fast3d_kernel<T, 1, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+    case 4: fast3d_kernel<T, 2, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    default: fast3d_kernel<T, 2, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+  }
 }
 
 template <typename T>
@@ -447,11 +497,7 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
-    switch (pred->padding) {
-      case 0: fast3d_kernel<T, 0, false><<<grid, block, lds, stream>>>(a); break;
-      case 1: fast3d_kernel<T, 1, false><<<grid, block, lds, stream>>>(a); break;
-      default: fast3d_kernel<T, 2, false><<<grid, block, lds, stream>>>(a); break;
-    }
+    launch_fast3d<T, false>(pred->padding, grid, block, lds, stream, a);
     return check_launch("fast3d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -473,11 +519,7 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     }
     a.hi_out = hi;
     a.lo_in = lowres;
-    switch (pred->padding) {
-      case 0: fast3d_kernel<T, 0, true><<<grid, block, lds, stream>>>(a); break;
-      case 1: fast3d_kernel<T, 1, true><<<grid, block, lds, stream>>>(a); break;
-      default: fast3d_kernel<T, 2, true><<<grid, block, lds, stream>>>(a); break;
-    }
+    launch_fast3d<T, true>(pred->padding, grid, block, lds, stream, a);
     return check_launch("fast3d_decode");
   }
   return KMP_ERR_UNSUPPORTED;
