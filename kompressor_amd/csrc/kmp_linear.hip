@@ -23,6 +23,3 @@ extern "C" int kmp_linear_predict(int32_t, int32_t, const void*, int64_t, const 
                                   const float*, const float*, void*, float*, kmp_stream_t) {
   return kmp::fail(KMP_ERR_UNSUPPORTED, "linear predictor not built yet");
 }
-extern "C" int kmp_categorical(int32_t, const float*, int64_t, int64_t, int32_t, const void*, void*, kmp_stream_t) {
-  return kmp::fail(KMP_ERR_UNSUPPORTED, "categorical coder not built yet");
-}

@@ -158,3 +158,53 @@ def test_image_batch_round_trip_full_size(kom):
     lowres, (maps, dims) = kom.image.encode(pred, kom.image.encode_values_uint8, img)
     rec = kom.image.decode(pred, kom.image.decode_values_uint8, lowres, (maps, dims))
     assert torch.equal(rec, img)
+
+
+def categorical_predictions_fn(kom, logits, padding, ndim):
+    """tests/volume/test_encode_decode.py:57-75 with the fixture's logits: constant logits tiled
+    over every cell, maps_from_predictions (HIP, float32), softmax (torch)."""
+    ns = _ns(kom, ndim)
+    lg = torch.from_numpy(logits).cuda()
+
+    def fn(lowres):
+        cells = [s - 1 - 2 * padding for s in lowres.shape[1:1 + ndim]]
+        pred = lg.expand(lowres.shape[0], *cells, *lg.shape).contiguous()
+        return [torch.softmax(m, dim=-1).contiguous() for m in ns.maps_from_predictions(pred)]
+
+    return fn
+
+
+@pytest.mark.parametrize('name', ['vol_categorical_p0', 'img_categorical_p1'])
+@pytest.mark.parametrize('chunk', [None, 6])
+def test_categorical_matches_golden(kom, name, chunk):
+    g = load_golden(name)
+    ndim, p = int(g['ndim']), int(g['padding'])
+    ns = _ns(kom, ndim)
+    fn = categorical_predictions_fn(kom, g['logits'], p, ndim)
+    hi = torch.from_numpy(g['highres']).cuda()
+    if chunk is None:
+        lowres, (maps, dims) = ns.encode(fn, ns.encode_categorical, hi, padding=p)
+    else:
+        lowres, (maps, dims) = ns.encode_chunks(fn, ns.encode_categorical, hi, chunk=chunk, padding=p)
+    _assert_encoded(g, lowres, maps, dims, ndim)
+    rec = ns.decode(fn, ns.decode_categorical, lowres, (maps, dims), padding=p)
+    assert torch.equal(rec, hi)
+    rec = ns.decode_chunks(fn, ns.decode_categorical, lowres, (maps, dims), chunk=6, padding=p)
+    assert torch.equal(rec, hi)
+
+
+def test_categorical_coder_vs_oracle(kom):
+    import oracle
+    rng = np.random.default_rng(7)
+    for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32)):
+        logits = rng.standard_normal((513, L)).astype(np.float32)
+        logits[::7, 3] = logits[::7, 1]  # ties
+        if L > 4:
+            logits[5, :] = 0.5          # an all-tie row
+        x = rng.integers(0, min(L + 3, np.iinfo(dt).max), size=513).astype(dt)
+        got = kom.utils.encode_categorical(logits, x)
+        want = oracle.common.encode_categorical(logits, x)
+        assert np.array_equal(got, want), L
+        got = kom.utils.decode_categorical(logits, x)
+        want = oracle.common.decode_categorical(logits, x)
+        assert np.array_equal(got, want), L
