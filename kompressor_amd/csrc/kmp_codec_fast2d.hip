@@ -1,17 +1,417 @@
-// kmp_codec_fast2d.hip -- one-pass fused encode / decode for images (placeholder: not yet
-// specialised; every request falls back to the generic two-pass path).
+// kmp_codec_fast2d.hip -- one-pass fused encode / decode for images (config C2).
+//
+// Eligible: C == 1, uint8/uint16, mean predictor with p <= 2 (uint8: p <= 4 would also be exact;
+// kept <= 2), W even with W*sizeof(T) % 16 == 0, Ex/VX <= 256 threads per row, 16-B aligned
+// highres, 8-B aligned lowres/maps, no region (chunked launches use the generic path).
+//
+// Output frame (image/utils.py:89-116): output o = (Y, X) owns the 2x2 highres block at 2o;
+// its 4 parity classes are the lowres and the LR, UD, C maps (trimmed, image/utils.py:188-193).
+// A workgroup is G "row groups" of TXN = Ex/VX threads; group g codes image (b0 + g), all groups
+// the same y-slab, rolling along y.  Per step j (lowres row):
+//   1. stream loads: lowres source row (prefetched one step ahead) and the output row's odd
+//      highres row (encode) or the 3 residual rows (decode);
+//   2. lowres nodes -> the group's LDS ring of 2p+2 rows, mirrored halo columns written by
+//      their owners (even reflect pad image/utils.py:145-156 + symmetric neighbourhood pad
+//      :132-137);
+//   3. cell means of row c = j-p-1 -> LDS ring of 2 rows (features + mean,
+//      tests/image/test_encode_decode.py:46-51);
+//   4. outputs of row c: LR / UD aggregation (image/utils.py:58-86, >> log2(count) == the f32
+//      x0.5 + truncation for these ranges), mod-2^k coder (utils.py:38-55), 8-byte stores.
+#include <cstdlib>
+
 #include "kmp_codec.h"
 
 namespace kmp {
 
+namespace f2 {
+
+constexpr int kColOff = 4;
+
+struct F2 {
+  const void* hi_in;
+  void* hi_out;
+  const void* lo_in;
+  void* lo_out;
+  MapPtrs maps;
+  int64_t B;
+  int32_t H, W;
+  int32_t Ly, Lx, Ey, Ex, Lcy, Lcx;
+  int32_t slab, nslab;
+  int32_t txn, groups, ngroup_blocks;
+  int32_t lo_pitch, m_pitch, group_lds;  // u32 elements
+};
+
+__device__ __forceinline__ int lsrc(int r, int L, int E) {
+  int m = r % (2 * L);
+  if (m < 0) m += 2 * L;
+  m = m < L ? m : 2 * L - 1 - m;
+  int m2 = m % (2 * E);
+  return m2 < E ? m2 : 2 * E - 1 - m2;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <int NT>
+__device__ __forceinline__ uint2 ld8(const void* p) {
+  if constexpr (NT) {
+    const u32x2 v = __builtin_nontemporal_load((const u32x2*)p);
+    return make_uint2(v.x, v.y);
+  } else {
+    return *(const uint2*)p;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr (NT) {
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u32x4*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st8(void* p, uint2 v) {
+  if constexpr (NT) {
+    u32x2 w = {v.x, v.y};
+    __builtin_nontemporal_store(w, (u32x2*)p);
+  } else {
+    *(uint2*)p = v;
+  }
+}
+
 template <typename T>
-int try_fast2d_encode(const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*, const MapPtrs&,
-                      const kmp_region*, hipStream_t) {
-  return KMP_ERR_UNSUPPORTED;
+__device__ __forceinline__ uint32_t e16(const uint4& v, int e) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
 }
 template <typename T>
-int try_fast2d_decode(const T*, const CMapPtrs&, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,
-                      const kmp_region*, hipStream_t) {
+__device__ __forceinline__ uint32_t e8(const uint2& v, int e) {
+  const uint32_t w[2] = {v.x, v.y};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint2 pack8(const uint32_t (&v)[VX]) {
+  if constexpr (sizeof(T) == 2) {
+    return make_uint2((v[0] & 0xffffu) | (v[1] << 16), (v[2] & 0xffffu) | (v[3] << 16));
+  } else {
+    return make_uint2((v[0] & 0xffu) | ((v[1] & 0xffu) << 8) | ((v[2] & 0xffu) << 16) | (v[3] << 24),
+                      (v[4] & 0xffu) | ((v[5] & 0xffu) << 8) | ((v[6] & 0xffu) << 16) | (v[7] << 24));
+  }
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint4 pack16(const uint32_t (&ev)[VX], const uint32_t (&od)[VX]) {
+  if constexpr (sizeof(T) == 2) {
+    return make_uint4((ev[0] & 0xffffu) | (od[0] << 16), (ev[1] & 0xffffu) | (od[1] << 16),
+                      (ev[2] & 0xffffu) | (od[2] << 16), (ev[3] & 0xffffu) | (od[3] << 16));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = (ev[2 * q] & 0xffu) | ((od[2 * q] & 0xffu) << 8) | ((ev[2 * q + 1] & 0xffu) << 16) | (od[2 * q + 1] << 24);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <typename T, int P, bool DEC, int NT>
+__global__ void __launch_bounds__(256) fast2d_kernel(F2 a) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  constexpr int R = 2 * P + 2;
+  constexpr int NB = 2 * P + 2;
+  constexpr uint32_t N = NB * NB;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+
+  const int g = threadIdx.x / a.txn;
+  const int tx = threadIdx.x % a.txn;
+  const int X = tx * VX;
+  const int slab_i = blockIdx.x % a.nslab;
+  const int64_t b = (int64_t)(blockIdx.x / a.nslab) * a.groups + g;
+  const bool live = g < a.groups && b < a.B;  // idle lanes still take part in the barriers
+  const int Y0 = slab_i * a.slab;
+  int Y1 = Y0 + a.slab;
+  Y1 = Y1 < a.Ey ? Y1 : a.Ey;
+
+  uint32_t* lo_ring = smem + (g < a.groups ? g : 0) * a.group_lds;
+  uint32_t* m_ring = lo_ring + R * a.lo_pitch;
+
+  const int64_t bb = live ? b : 0;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + bb * (int64_t)a.H * a.W;
+  T* hout = DEC ? (T*)a.hi_out + bb * (int64_t)a.H * a.W : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + bb * (int64_t)a.Ey * a.Ex : nullptr;
+  const int hx = 2 * X;
+
+  auto write_nodes = [&](uint32_t* row, const uint32_t (&nv)[VX]) {
+    uint32_t* r = row + kColOff + X;
+    *(uint4*)r = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+    if constexpr (VX == 8) *(uint4*)(r + 4) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+    auto pick = [&](int s) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < VX; ++i) v = (s - X == i) ? nv[i] : v;
+      return v;
+    };
+    for (int q = -P; q < 0; ++q) {
+      const int s = lsrc(q, a.Lx, a.Ex);
+      if (s >= X && s < X + VX) r[q - X] = pick(s);
+    }
+    for (int q = a.Ex; q <= a.Lx - 1 + P; ++q) {
+      const int s = lsrc(q, a.Lx, a.Ex);
+      if (s >= X && s < X + VX) r[q - X] = pick(s);
+    }
+  };
+
+  const int jstart = (Y0 - 1 > 0 ? Y0 - 1 : 0) - P;
+  const int jend = Y1 + P;
+  const int mfirst = Y0 - 1 > 0 ? Y0 - 1 : 0;
+
+  auto load_lowres_row = [&](int j, uint4& hv, uint2& lv) {
+    if (!live) return;
+    const int sy = lsrc(j, a.Ly, a.Ey);
+    if constexpr (DEC) lv = ld8<NT>(lin + (int64_t)sy * a.Ex + X);
+    else hv = ld16<NT>(hin + (int64_t)(2 * sy) * a.W + hx);
+  };
+  uint4 pre_h = make_uint4(0, 0, 0, 0);
+  uint2 pre_l = make_uint2(0, 0);
+  load_lowres_row(jstart, pre_h, pre_l);
+  uint4 keep_e = make_uint4(0, 0, 0, 0);  // encode P==0: highres row 2c
+  uint2 keep_l = make_uint2(0, 0);        // decode P==0: lowres row c
+
+  for (int j = jstart; j <= jend; ++j) {
+    const int c = j - P - 1;
+    const bool do_m = c >= mfirst && c < a.Lcy;
+    const bool do_out = live && c >= Y0 && c < Y1;
+    const bool vy1 = c < a.Lcy;
+    const bool vy0 = c >= 1;
+
+    const uint4 cur_h = pre_h;
+    const uint2 cur_l = pre_l;
+    if (j < jend) load_lowres_row(j + 1, pre_h, pre_l);
+
+    uint4 e0 = make_uint4(0, 0, 0, 0), o0 = e0;
+    uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
+    if constexpr (!DEC) {
+      if (do_out) {
+        if constexpr (P == 0) e0 = keep_e;
+        else e0 = ld16<NT>(hin + (int64_t)(2 * c) * a.W + hx);
+        if (vy1) o0 = ld16<NT>(hin + (int64_t)(2 * c + 1) * a.W + hx);
+      }
+    } else {
+      if (do_out) {
+        if (vy1) mv[0] = ld8<NT>((const T*)a.maps.p[0] + ((bb * a.Lcy + c) * a.Ex + X));
+        mv[1] = ld8<NT>((const T*)a.maps.p[1] + ((bb * a.Ey + c) * a.Ex + X));
+        if (vy1) mv[2] = ld8<NT>((const T*)a.maps.p[2] + ((bb * a.Lcy + c) * a.Ex + X));
+      }
+    }
+
+    {
+      uint32_t nv[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) nv[i] = DEC ? e8<T>(cur_l, i) : e16<T>(cur_h, 2 * i);
+      const int slot = ((j % R) + R) % R;
+      if (live) write_nodes(lo_ring + slot * a.lo_pitch, nv);
+    }
+    if constexpr (!DEC && P == 0) keep_e = cur_h;
+    __syncthreads();
+
+    if (live && do_m) {
+      uint32_t s[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) s[i] = 0;
+#pragma unroll
+      for (int dy = 0; dy < NB; ++dy) {
+        const int slot = (((c - P + dy) % R) + R) % R;
+        const uint32_t* row = lo_ring + slot * a.lo_pitch + kColOff + X - P;
+        uint32_t v[VX + NB - 1];
+#pragma unroll
+        for (int q = 0; q < VX + NB - 1; ++q) v[q] = row[q];
+#pragma unroll
+        for (int i = 0; i < VX; ++i)
+#pragma unroll
+          for (int dx = 0; dx < NB; ++dx) s[i] += v[i + dx];
+      }
+      uint32_t* mrow = m_ring + (c & 1) * a.m_pitch + kColOff + X;
+      *(uint4*)mrow = make_uint4(s[0] / N, s[1] / N, s[2] / N, s[3] / N);
+      if constexpr (VX == 8) *(uint4*)(mrow + 4) = make_uint4(s[4] / N, s[5] / N, s[6] / N, s[7] / N);
+    }
+    uint32_t own_lo[VX];
+    if constexpr (DEC) {
+      if constexpr (P == 0) {
+#pragma unroll
+        for (int i = 0; i < VX; ++i) own_lo[i] = e8<T>(keep_l, i);
+        keep_l = cur_l;
+      } else {
+        const uint32_t* row = lo_ring + (((c % R) + R) % R) * a.lo_pitch + kColOff + X;
+#pragma unroll
+        for (int i = 0; i < VX; ++i) own_lo[i] = row[i];
+      }
+    }
+    __syncthreads();
+    if (!do_out) continue;
+
+    // cells: rows c-1 (index 0), c (index 1); cols X-1 .. X+VX-1
+    uint32_t M[2][VX + 1];
+    bool vx[VX + 1];
+#pragma unroll
+    for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const uint32_t* row = m_ring + ((c - 1 + dy) & 1) * a.m_pitch + kColOff + X - 1;
+      const bool ok = dy ? vy1 : vy0;
+      uint32_t v[VX + 1];
+      v[0] = row[0];
+      const uint4 w0 = *(const uint4*)(row + 1);
+      v[1] = w0.x; v[2] = w0.y; v[3] = w0.z; v[4] = w0.w;
+      if constexpr (VX == 8) {
+        const uint4 w1 = *(const uint4*)(row + 5);
+        v[5] = w1.x; v[6] = w1.y; v[7] = w1.z; v[8] = w1.w;
+      }
+#pragma unroll
+      for (int q = 0; q <= VX; ++q) M[dy][q] = (ok && vx[q]) ? v[q] : 0u;
+    }
+    const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+    uint32_t pred[3][VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pred[0][i] = (M[1][i] + M[1][i + 1]) >> (nx >> 1);  // LR: cells (c, x-1), (c, x)
+      pred[1][i] = (M[0][i + 1] + M[1][i + 1]) >> (ny >> 1);  // UD: cells (c-1, x), (c, x)
+      pred[2][i] = M[1][i + 1];                               // C
+    }
+    if constexpr (!DEC) {
+      uint32_t lov[VX], res[3][VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        lov[i] = e16<T>(e0, 2 * i);
+        res[0][i] = (e16<T>(o0, 2 * i) - pred[0][i]) & MASK;      // LR (1,0)
+        res[1][i] = (e16<T>(e0, 2 * i + 1) - pred[1][i]) & MASK;  // UD (0,1)
+        res[2][i] = (e16<T>(o0, 2 * i + 1) - pred[2][i]) & MASK;  // C  (1,1)
+      }
+      st8<NT>((T*)a.lo_out + ((bb * a.Ey + c) * a.Ex + X), pack8<T, VX>(lov));
+      if (vy1) st8<NT>((T*)a.maps.p[0] + ((bb * a.Lcy + c) * a.Ex + X), pack8<T, VX>(res[0]));
+      st8<NT>((T*)a.maps.p[1] + ((bb * a.Ey + c) * a.Ex + X), pack8<T, VX>(res[1]));
+      if (vy1) st8<NT>((T*)a.maps.p[2] + ((bb * a.Lcy + c) * a.Ex + X), pack8<T, VX>(res[2]));
+    } else {
+      uint32_t dv[3][VX];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + e8<T>(mv[k], i)) & MASK;
+      T* h0 = hout + (int64_t)(2 * c) * a.W + hx;
+      st16<NT>(h0, pack16<T, VX>(own_lo, dv[1]));                // row 2c: lowres | UD
+      if (vy1) st16<NT>(h0 + a.W, pack16<T, VX>(dv[0], dv[2]));  // row 2c+1: LR | C
+    }
+  }
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+template <typename T>
+static bool geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region, F2& a,
+                     dim3& grid, dim3& block, size_t& lds) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  if (env_int("KMP_DISABLE_FAST", 0)) return false;
+  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding > 2 || region) return false;
+  const int P = pred->padding;
+  const int64_t H = g.n[1], W = g.n[2];
+  if (W % 2 != 0 || (W * (int64_t)sizeof(T)) % 16 != 0 || H > (1 << 30) || W > (1 << 30)) return false;
+  const int64_t txn = g.E[2] / VX;
+  if (txn * VX != g.E[2] || txn > 256 || txn < 1) return false;
+  a.B = B;
+  a.H = (int)H; a.W = (int)W;
+  a.Ly = (int)g.L[1]; a.Lx = (int)g.L[2]; a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
+  a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
+  a.txn = (int)txn;
+  a.groups = (int)(256 / txn);
+  a.lo_pitch = (int)((kColOff + g.L[2] + P + VX + 3) / 4 * 4) + 4;
+  a.m_pitch = (int)((kColOff + g.Lc[2] + VX + 3) / 4 * 4) + 4;
+  a.group_lds = (2 * P + 2) * a.lo_pitch + 2 * a.m_pitch;
+  lds = (size_t)a.groups * a.group_lds * sizeof(uint32_t);
+  if (lds > 64 * 1024) return false;
+  const int64_t gblocks = ceil_div(B, a.groups);
+  int64_t want = env_int("KMP_WG_TARGET_2D", 2048);
+  int64_t nslab = ceil_div(want, gblocks);
+  if (nslab > g.E[1]) nslab = g.E[1];
+  if (nslab < 1) nslab = 1;
+  int64_t slab = ceil_div(g.E[1], nslab);
+  const int min_slab = env_int("KMP_MIN_SLAB_2D", 8);
+  if (slab < min_slab) slab = min_slab < g.E[1] ? min_slab : g.E[1];
+  nslab = ceil_div(g.E[1], slab);
+  a.slab = (int)slab;
+  a.nslab = (int)nslab;
+  a.ngroup_blocks = (int)gblocks;
+  grid = dim3((unsigned)(gblocks * nslab));
+  block = dim3((unsigned)(a.groups * txn));
+  return gblocks * nslab < ((int64_t)1 << 31);
+}
+
+template <typename T, bool DEC>
+static void launch(int P, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const F2& a) {
+  const bool nt = env_int("KMP_NT", 1) != 0;
+  switch (P * 2 + (nt ? 1 : 0)) {
+    case 0: fast2d_kernel<T, 0, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    case 1: fast2d_kernel<T, 0, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+    case 2: fast2d_kernel<T, 1, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    case 3: fast2d_kernel<T, 1, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+    case 4: fast2d_kernel<T, 2, DEC, 0><<<grid, block, lds, stream>>>(a); break;
+    default: fast2d_kernel<T, 2, DEC, 1><<<grid, block, lds, stream>>>(a); break;
+  }
+}
+
+}  // namespace f2
+
+template <typename T>
+int try_fast2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                      const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    f2::F2 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!f2::geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 3; ++k)
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+    a.hi_in = hi;
+    a.lo_out = lowres;
+    a.maps = maps;
+    f2::launch<T, false>(pred->padding, grid, block, lds, stream, a);
+    return check_launch("fast2d_encode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int try_fast2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                      const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    f2::F2 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!f2::geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 3; ++k) {
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      a.maps.p[k] = (void*)maps.p[k];
+    }
+    a.hi_out = hi;
+    a.lo_in = lowres;
+    f2::launch<T, true>(pred->padding, grid, block, lds, stream, a);
+    return check_launch("fast2d_decode");
+  }
   return KMP_ERR_UNSUPPORTED;
 }
 

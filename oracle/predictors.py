@@ -76,13 +76,55 @@ def linear_predictions(features, weights, bias, dtype):
     return pred, cast_from_f32(pred.astype(np.float32), dtype)
 
 
+def fma_f32(a, b, c):
+    """Correctly rounded float32 fused multiply-add, vectorised: the exact a*b + c rounded once.
+
+    a*b of two float32 is exact in float64; TwoSum gives s + e == a*b + c exactly; rounding s to
+    float32 equals rounding the exact value unless s sits exactly on a float32 midpoint (the
+    only double-rounding case, since float64 rounding is monotone and midpoints are float64
+    representable), where the sign of e decides."""
+    a = np.asarray(a, np.float32).astype(np.float64)
+    b = np.asarray(b, np.float32).astype(np.float64)
+    c = np.asarray(c, np.float32).astype(np.float64)
+    p = a * b                          # exact
+    s = p + c                          # TwoSum: s + e == p + c exactly
+    bb = s - p
+    e = (p - (s - bb)) + (c - bb)
+    r = s.astype(np.float32)           # round half to even
+    r64 = r.astype(np.float64)
+    with np.errstate(invalid='ignore'):
+        nb = np.nextafter(r, np.where(s > r64, np.float32(np.inf), np.float32(-np.inf)).astype(np.float32))
+        gap = np.abs(nb.astype(np.float64) - r64)
+        tie = (s != r64) & (2 * np.abs(s - r64) == gap)
+        # on a tie r is the even neighbour; the exact value lies beyond the midpoint iff e points
+        # the same way as s - r
+        away = tie & (e != 0) & (np.sign(e) == np.sign(s - r64))
+    return np.where(away, nb, r).astype(np.float32)
+
+
+def linear_fma_chain(features, weights, bias):
+    """The build's LinearPredictor arithmetic, bit for bit: acc = b[k]; acc = fma(f[n], W[n, k], acc)
+    for n = 0..N-1 (what the f32 MFMA computes, kmp_linear.hip).  ``features [.., N, C]`` ->
+    float32 ``[.., K, C]``."""
+    f = np.asarray(features).astype(np.float32)
+    w = np.asarray(weights, np.float32)
+    b = np.asarray(bias, np.float32)
+    n_axis = f.ndim - 2
+    f = np.moveaxis(f, n_axis, -1)  # [.., C, N]
+    acc = np.broadcast_to(b, f.shape[:-1] + b.shape).astype(np.float32).copy()  # [.., C, K]
+    for n in range(w.shape[0]):
+        acc = fma_f32(f[..., n:n + 1], w[n], acc)
+    return np.moveaxis(acc, -1, n_axis)  # [.., K, C]
+
+
 def linear_predictions_fn(padding, weights, bias, ndim=3):
+    """LinearPredictor as a predictions_fn: the exact fma chain, cast to the dtype, aggregated."""
     ns = _ns(ndim)
 
     def predictions_fn(lowres):
         lowres = np.asarray(lowres)
         features = ns.features_from_lowres(lowres, padding)
-        _, pred = linear_predictions(features, weights, bias, lowres.dtype)
+        pred = cast_from_f32(linear_fma_chain(features, weights, bias), lowres.dtype)
         return ns.maps_from_predictions(pred)
 
     return predictions_fn

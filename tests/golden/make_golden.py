@@ -105,6 +105,12 @@ def main():
     codec_case('img_rand_u16_c2_p1', rand((2, 30, 31, 2), np.uint16, 40), 1, 2)
     codec_case('img_tile256_p0', rand((2, 256, 256, 1), np.uint8, 0), 0, 2, check_loops=False)
     codec_case('img_ramp_i32_raw_p0', ramp((2, 17, 17, 3), 256, np.int32), 0, 2)
+    # shapes eligible for the one-pass kernels (C == 1, W*itemsize % 16 == 0), odd and even H/D
+    codec_case('vol_fast_u16_p2', rand((2, 11, 9, 16, 1), np.uint16, 60), 2, 3)
+    codec_case('vol_fast_u8_p1', rand((3, 9, 14, 32, 1), np.uint8, 61), 1, 3)
+    codec_case('img_fast_u8_p1', rand((3, 30, 32, 1), np.uint8, 62), 1, 2)
+    codec_case('img_fast_u8_p0', rand((5, 33, 48, 1), np.uint8, 63), 0, 2)
+    codec_case('img_fast_u16_p2', rand((2, 17, 16, 1), np.uint16, 64), 2, 2)
     # categorical rank coder (reference tests use 256 classes on uint8, :217-356)
     categorical_case('vol_categorical_p0', ramp((2, 9, 9, 9, 1), 256, np.uint8), 0, 3)
     categorical_case('img_categorical_p1', ramp((2, 17, 17, 3), 256, np.uint8), 1, 2)

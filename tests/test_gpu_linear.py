@@ -1,0 +1,78 @@
+"""LinearPredictor (f32 MFMA) parity: float32 intermediates bit-exact to the oracle's fma chain and
+within the north star's 1e-5 of a float64 reference; residual maps bit-exact; lossless."""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import predictors as OP
+
+pytestmark = pytest.mark.gpu
+
+
+def _weights(ndim, padding, seed, dtype):
+    n, k = (2 * padding + 2) ** ndim, 19 if ndim == 3 else 5
+    rng = np.random.default_rng(seed)
+    w = (1.0 / n + rng.standard_normal((n, k)) * (0.3 / n)).astype(np.float32)  # ~ a noisy mean
+    b = (rng.standard_normal(k) * (3.0 if dtype == np.uint8 else 50.0)).astype(np.float32)
+    return w, b
+
+
+CASES = [(3, 0, (2, 9, 10, 12, 1), np.uint16), (3, 1, (2, 8, 9, 7, 1), np.uint16), (3, 0, (1, 9, 8, 16, 2), np.uint8),
+         (3, 0, (4, 64, 64, 64, 1), np.uint16), (2, 0, (3, 33, 20, 1), np.uint8), (2, 1, (2, 30, 31, 2), np.uint16),
+         (2, 2, (2, 17, 17, 1), np.uint8)]
+
+
+def _data(shape, dtype, seed):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+
+
+@pytest.mark.parametrize('ndim,p,shape,dtype', CASES)
+def test_linear_cell_predictions(kom, ndim, p, shape, dtype):
+    ons = oracle.volume if ndim == 3 else oracle.image
+    hi = _data(shape, dtype, 1)
+    w, b = _weights(ndim, p, 2, dtype)
+    window = ons.pad_neighborhood(ons.lowres_from_highres(ons.pad_highres(hi)[0]), p)
+    pred = kom.LinearPredictor(w, b, p, ndim)
+    cells_t, cells_f = pred.predict_cells(window, with_f32=True)
+    feats = ons.features_from_lowres(window, p)
+    exact = OP.linear_fma_chain(feats, w, b)
+    assert cells_f.dtype == np.float32 and cells_f.shape == exact.shape
+    assert np.array_equal(cells_f.view(np.uint32), exact.view(np.uint32)), 'f32 MFMA != k-ordered fma chain'
+    f64, _ = OP.linear_predictions(feats, w, b, dtype)
+    scale = np.tensordot(np.abs(np.moveaxis(feats.astype(np.float64), ndim + 1, -1)), np.abs(w), axes=([-1], [0]))
+    scale = np.moveaxis(scale, -1, ndim + 1) + np.abs(b).reshape(-1, 1)
+    assert np.all(np.abs(cells_f - f64) <= 1e-5 * scale + 1e-6), 'north-star 1e-5 tolerance'
+    assert np.array_equal(cells_t, oracle.common.cast_from_f32(exact, dtype))
+
+
+@pytest.mark.parametrize('ndim,p,shape,dtype', CASES)
+def test_linear_codec(kom, ndim, p, shape, dtype):
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    hi = _data(shape, dtype, 3)
+    w, b = _weights(ndim, p, 4, dtype)
+    pred = kom.LinearPredictor(w, b, p, ndim)
+    enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if dtype == np.uint16 else \
+               (ns.encode_values_uint8, ns.decode_values_uint8)
+    oenc = ons.encode_values_uint16 if dtype == np.uint16 else ons.encode_values_uint8
+    want_lo, (want_maps, want_dims) = ons.encode(OP.linear_predictions_fn(p, w, b, ndim), oenc, hi, padding=p)
+    for fn in (pred, lambda x: pred(x)):  # fused kernels, then the callback path
+        lo, (maps, dims) = ns.encode(fn, enc, hi, padding=p)
+        assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+        for a, c in zip(maps, want_maps):
+            assert np.array_equal(a, c)
+        assert np.array_equal(ns.decode(fn, dec, lo, (maps, dims), padding=p), hi)
+
+
+def test_linear_chunks(kom):
+    hi = _data((2, 17, 16, 15, 1), np.uint16, 5)
+    w, b = _weights(3, 1, 6, np.uint16)
+    pred = kom.LinearPredictor(w, b, 1, 3)
+    lo, (maps, dims) = kom.volume.encode(pred, kom.volume.encode_values_uint16, hi, padding=1)
+    for chunk in (6, (6, 11, 7)):
+        lo2, (maps2, dims2) = kom.volume.encode_chunks(pred, kom.volume.encode_values_uint16, hi, chunk=chunk, padding=1)
+        assert np.array_equal(lo, lo2) and all(np.array_equal(a, c) for a, c in zip(maps, maps2))
+        rec = kom.volume.decode_chunks(pred, kom.volume.decode_values_uint16, lo, (maps, dims), chunk=chunk, padding=1)
+        assert np.array_equal(rec, hi)
