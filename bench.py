@@ -43,6 +43,7 @@ def parse():
     ap.add_argument('--workload', choices=sorted(WORKLOADS), default='volume')
     ap.add_argument('--padding', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--eager', action='store_true', help='launch through Python each step instead of hipGraph replay')
     ap.add_argument('--cpu-tiles', type=int, default=0, help='tiles in the CPU baseline sample (0 = all)')
     return ap.parse_args()
 
@@ -120,7 +121,7 @@ def main():
     hi = torch.from_numpy(host).cuda()
     lowres, maps, dims = _nd._alloc_encoded(hi, coder, ndim)
     rec = torch.empty_like(hi)
-    ws = torch.empty(1, dtype=torch.uint8, device='cuda')
+    ws = torch.empty(max(1, _nd.workspace_bytes(hi, predictor, ndim)), dtype=torch.uint8, device='cuda')
 
     def encode():
         _nd.fused_encode_into(hi, predictor, coder, lowres, maps, ndim, workspace=ws)
@@ -137,7 +138,29 @@ def main():
     for _ in range(args.warmup):
         encode()
         decode()
-    stream = torch.cuda.current_stream()  # the stream the kernels are launched on (dev.stream())
+    if args.eager:
+        run_enc, run_dec = encode, decode
+    else:
+        # one hipGraph per direction: replays the same single kernel launch without the Python /
+        # ctypes launch path (the launch-bound part of a ~0.1 ms step)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            encode()
+            decode()
+        torch.cuda.current_stream().wait_stream(side)
+        g_enc, g_dec = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_enc):
+            encode()
+        with torch.cuda.graph(g_dec):
+            decode()
+        run_enc, run_dec = g_enc.replay, g_dec.replay
+        for _ in range(2):
+            run_enc()
+            run_dec()
+        torch.cuda.synchronize()
+        assert torch.equal(rec, hi), 'graph replay round trip is not lossless'
+    stream = torch.cuda.current_stream()  # the stream the kernels / graphs are launched on
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -146,9 +169,9 @@ def main():
     t0 = time.perf_counter()
     for e0, e1, e2 in ev:
         e0.record(stream)
-        encode()
+        run_enc()
         e1.record(stream)
-        decode()
+        run_dec()
         e2.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -207,6 +230,7 @@ def main():
                        'tile': list(spec['shape'][1:-1]), 'predictor': f'MeanPredictor(padding={args.padding})',
                        'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
+            'launch': 'eager (ctypes per call)' if args.eager else 'hipGraph replay (one graph per direction)',
             'roofline': {'bound': 'hbm', 'kernel': f'fast3d_kernel {dominant}' if ndim == 3 else f'{dominant}',
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),

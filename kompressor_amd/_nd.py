@@ -370,6 +370,14 @@ def encoded_shapes(shape, nsp):
     return lo, maps, dims
 
 
+def workspace_bytes(h, predictor, nsp):
+    """Device workspace the fused calls may need for highres ``h`` (0 on the one-pass path)."""
+    B, sp, C = h.shape[0], _sp(h.shape, nsp), _C(h.shape, nsp)
+    pstruct = predictor._kmp_predictor()
+    fn = lib.kmp_volume_workspace_bytes if nsp == 3 else lib.kmp_image_workspace_bytes
+    return int(fn(dev.dtype_code(h), B, *sp, C, ctypes.byref(pstruct)))
+
+
 def fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=None, workspace=None):
     B, sp, C = h.shape[0], _sp(h.shape, nsp), _C(h.shape, nsp)
     pstruct = predictor._kmp_predictor()
