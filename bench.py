@@ -43,7 +43,7 @@ def parse():
     ap.add_argument('--workload', choices=sorted(WORKLOADS), default='volume')
     ap.add_argument('--padding', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--eager', action='store_true', help='launch through Python each step instead of hipGraph replay')
+    ap.add_argument("--graph", action="store_true", help="replay each direction from a hipGraph instead of eager ctypes launches")
     ap.add_argument('--cpu-tiles', type=int, default=0, help='tiles in the CPU baseline sample (0 = all)')
     return ap.parse_args()
 
@@ -138,11 +138,11 @@ def main():
     for _ in range(args.warmup):
         encode()
         decode()
-    if args.eager:
+    if not args.graph:
         run_enc, run_dec = encode, decode
     else:
         # one hipGraph per direction: replays the same single kernel launch without the Python /
-        # ctypes launch path (the launch-bound part of a ~0.1 ms step)
+        # ctypes launch path (measured: no gain at this size, profiles/round1/bench_graph_vs_eager.log)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -230,7 +230,7 @@ def main():
                        'tile': list(spec['shape'][1:-1]), 'predictor': f'MeanPredictor(padding={args.padding})',
                        'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
-            'launch': 'eager (ctypes per call)' if args.eager else 'hipGraph replay (one graph per direction)',
+            'launch': 'hipGraph replay (one graph per direction)' if args.graph else 'eager (one ctypes launch per direction)',
             'roofline': {'bound': 'hbm', 'kernel': f'fast3d_kernel {dominant}' if ndim == 3 else f'{dominant}',
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),
