@@ -14,6 +14,10 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
 def pytest_configure(config):
+    # the product library is built in-tree (git-ignored); build it once if this checkout lacks it
+    if not os.path.exists(os.path.join(ROOT, 'kompressor_amd', 'libkompressor_hip.so')):
+        import __graft_entry__
+        __graft_entry__._load_builder().build(verbose=False)
     config.addinivalue_line('markers', 'gpu: needs an MI355X (gfx950) GPU and the built libkompressor_hip.so')
 
 
