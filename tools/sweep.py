@@ -18,7 +18,10 @@ def main():
     lo, maps, dims = _nd._alloc_encoded(hi, coder, ndim)
     rec = torch.empty_like(hi)
     ws = torch.empty(1, dtype=torch.uint8, device='cuda')
-    configs = [dict(KMP_WG_TARGET=str(w), KMP_MIN_SLAB=str(s), KMP_NT=str(nt)) for w in (1024, 2048, 4096, 8192) for s in (2, 4) for nt in (0, 1)]
+    if len(sys.argv) > 3:
+        configs = json.loads(sys.argv[3])
+    else:
+        configs = [dict(KMP_WG_TARGET=str(w), KMP_MIN_SLAB=str(s), KMP_NT=str(nt)) for w in (1024, 2048, 4096, 8192) for s in (2, 4) for nt in (0, 1)]
     res = {i: ([], []) for i in range(len(configs))}
     for rnd in range(8):
         for i, cfg in enumerate(configs):
