@@ -175,6 +175,14 @@ int kmp_copy_box(int32_t nsp, int32_t in_dtype, const void* in, const int64_t in
                  int32_t out_dtype, void* out, const int64_t out_shape[3], const int64_t out_off[3], int64_t B,
                  int64_t C, const int64_t ext[3], kmp_stream_t stream);
 
+/* Tile split / reassembly for the batched metric workload (BASELINE configs C3/C4): the
+   reference codes a batch of independent arrays along its leading axis (every primitive is
+   [:, ...]-parallel, volume/utils.py:80,161-169); this turns ONE volume [D, H, W, C] (image
+   [H, W, C]) into the batch [n, Tz, Ty, Tx, C] of its tiles in z-major tile order
+   (direction 0) and back (direction 1).  Every extent must be a multiple of the tile's. */
+int kmp_tiles(int32_t nsp, int32_t dtype, int32_t direction, const void* src, const int64_t shape[3], int64_t C,
+              const int64_t tile[3], void* dst, kmp_stream_t stream);
+
 /* Residual coders utils.py:28-55 on n elements.  ``pred_dtype``/``x_dtype`` are the operand
    dtypes (x = gt for ENCODE, encoded for DECODE); the output is uint8 / uint16 / int32 /
    uint32 for KMP_CODER_U8 / U16 / RAW / U32. */

@@ -79,6 +79,7 @@ _PROTOS = {
                                     _vp]),
     'kmp_code': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i32, _vp, _i64, _vp, _vp]),
     'kmp_categorical': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    'kmp_tiles': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64p, _i64, _i64p, _vp, _vp]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():
