@@ -32,6 +32,12 @@ WORKLOADS = {
     'image': dict(ndim=2, shape=(1024, 256, 256, 1), dtype=np.uint8,
                   metric='encode+decode GB/s/GPU (device-resident), 1024 x 256² uint8 image tiles',
                   name='1024 uint8 images of 256^2 (BASELINE config C2)'),
+    # C5: 2048^3 float32 = 4096 chunks of 128^3 over 8 GPUs -> 512 chunks (4 GiB) per GPU,
+    # host-resident (pinned), streamed H2D -> kernel -> D2H
+    'stream': dict(ndim=3, shape=(512, 128, 128, 128, 1), dtype=np.float32,
+                   metric='encode+decode GB/s/GPU (pinned host -> GPU -> host, H2D/kernel/D2H overlapped), '
+                          '2048³ float32 as 128³ chunks',
+                   name='2048^3 float32 streamed as 128^3 chunks, 512 chunks per GPU (BASELINE config C5)'),
 }
 
 
@@ -45,11 +51,16 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument("--graph", action="store_true", help="replay each direction from a hipGraph instead of eager ctypes launches")
     ap.add_argument('--cpu-tiles', type=int, default=0, help='tiles in the CPU baseline sample (0 = all)')
+    ap.add_argument('--e2e-chunk', type=int, default=32, help='tiles per H2D/D2H copy in the end-to-end leg')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the pinned-host end-to-end leg')
+    ap.add_argument('--stream-tiles', type=int, default=0, help='stream workload: chunks per GPU (0 = 512)')
     return ap.parse_args()
 
 
 def synthetic(spec, seed):
     # default_rng(seed).integers over the dtype's full range
+    if spec['dtype'] == np.float32:
+        return np.random.default_rng(seed).standard_normal(spec['shape'], dtype=np.float32)
     info = np.iinfo(spec['dtype'])
     rng = np.random.default_rng(seed)
     return rng.integers(0, int(info.max) + 1, size=spec['shape'], dtype=np.int64).astype(spec['dtype'])
@@ -84,6 +95,36 @@ def cpu_baseline(spec, host, padding, ntiles):
                       f'{len(os.sched_getaffinity(0))} cores), median of 2 after warm-up, {t:.2f} s/round'}
 
 
+def e2e_leg(kom, host, predictor, ndim, chunk, reps=3):
+    """Host-resident rate: pinned host tiles -> H2D -> fused encode -> D2H, then the encoded
+    maps back through H2D -> fused decode -> D2H, copies and kernels overlapped across 3 HIP
+    streams (kompressor_amd.stream.TileStream).  Median of ``reps`` after one warm-up."""
+    src = kom.stream.pinned(host.shape, torch.from_numpy(host[:0]).dtype)
+    src.copy_(torch.from_numpy(host))
+    ts = kom.stream.TileStream(predictor, host.shape[1:], src.dtype, chunk, 3, ndim)
+    lo, maps = ts.alloc_encoded(host.shape[0])
+    out = kom.stream.pinned(host.shape, src.dtype)
+    te, td = [], []
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ts.encode(src, lo, maps)
+        ts.synchronize()
+        t1 = time.perf_counter()
+        ts.decode(lo, maps, out)
+        ts.synchronize()
+        t2 = time.perf_counter()
+        if i:
+            te.append(t1 - t0)
+            td.append(t2 - t1)
+    assert torch.equal(out.view(torch.uint8), src.view(torch.uint8)), 'end-to-end round trip is not lossless'
+    te, td = float(np.median(te)), float(np.median(td))
+    raw = src.numel() * src.element_size()
+    return {'GBps': round(raw / (te + td) / 1e9, 3), 'ms_encode': round(te * 1e3, 3), 'ms_decode': round(td * 1e3, 3),
+            'chunk_tiles': chunk, 'streams': 3, 'host_memory': 'pinned',
+            'note': 'raw bytes / (t_enc + t_dec), each direction timed from pinned host input to pinned host output'}
+
+
 def load_traffic(workload, padding, kernel):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, collected by separate --pmc FETCH_SIZE / WRITE_SIZE passes of this
@@ -96,9 +137,7 @@ def load_traffic(workload, padding, kernel):
     return entry['hbm_bytes'] if entry else None
 
 
-def main():
-    args = parse()
-    spec = WORKLOADS[args.workload]
+def init_dist():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -109,11 +148,80 @@ def main():
     else:
         dist = None
         torch.cuda.set_device(0)
+    return world, rank, dist
+
+
+def timed_steps(run_enc, run_dec, steps, dist):
+    """EXACTLY ``steps`` (encode, decode) pairs bracketed by barrier + synchronize; HIP events on
+    the launch stream give the per-direction kernel time.  Returns wall seconds and mean
+    per-direction seconds, each the max over ranks."""
+    stream = torch.cuda.current_stream()  # the stream the kernels / graphs are launched on
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        run_enc()
+        e1.record(stream)
+        run_dec()
+        e2.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_enc = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
+    t_dec = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
+    if dist:
+        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, t_enc, t_dec = tt.tolist()
+    return elapsed, t_enc, t_dec
+
+
+def c4_reassembly(kom, hi, predictor, ndim, dist, world, ws):
+    """BASELINE config C4: ONE volume's tiles sharded over the ranks (kompressor_amd.shard), each
+    rank codes its shard, then one RCCL all-gather reassembles the decoded tiles everywhere.
+    Timed as a whole, separately from ``value``."""
+    from kompressor_amd import _nd
+    hi = hi.clone()
+    dist.broadcast(hi.view(torch.uint8), 0)   # every rank holds the same volume (rank 0's)
+    n = hi.shape[0]
+    shard = kom.shard.local_shard(hi).contiguous()
+    coder = _nd.NATURAL_CODER[hi.dtype]
+    lo_s, maps_s, dims_s = _nd._alloc_encoded(shard, coder, ndim)
+    rec_s = torch.empty_like(shard)
+    times = []
+    for i in range(6):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _nd.fused_encode_into(shard, predictor, coder, lo_s, maps_s, ndim, workspace=ws)
+        _nd.fused_decode_into(lo_s, maps_s, dims_s, predictor, coder, rec_s, ndim, workspace=ws)
+        full = kom.shard.all_gather_tiles(rec_s, n)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t)
+    assert torch.equal(full, hi), 'C4 reassembled volume differs from the input'
+    tt = torch.tensor([float(np.median(times[1:]))], dtype=torch.float64, device='cuda')
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    raw = hi.numel() * hi.element_size()
+    return {'tiles_per_rank': int(shard.shape[0]), 'ms_codec_plus_allgather': round(tt.item() * 1e3, 4),
+            'volume_GBps': round(raw / tt.item() / 1e9, 2),
+            'collective': 'all_gather_into_tensor (RCCL) of per-rank decoded tile slabs'}
+
+
+def main():
+    args = parse()
+    if args.workload == 'stream':
+        return main_stream(args)
+    spec = WORKLOADS[args.workload]
+    world, rank, dist = init_dist()
 
     import kompressor_amd as kom
     from kompressor_amd import _nd
     ndim = spec['ndim']
-    ns = kom.volume if ndim == 3 else kom.image
     predictor = kom.MeanPredictor(args.padding, ndim)
     coder = _nd.NATURAL_CODER[torch.uint16 if spec['dtype'] == np.uint16 else torch.uint8]
 
@@ -160,29 +268,7 @@ def main():
             run_dec()
         torch.cuda.synchronize()
         assert torch.equal(rec, hi), 'graph replay round trip is not lossless'
-    stream = torch.cuda.current_stream()  # the stream the kernels / graphs are launched on
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        e0.record(stream)
-        run_enc()
-        e1.record(stream)
-        run_dec()
-        e2.record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t_enc = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
-    t_dec = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
-    if dist:
-        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, t_enc, t_dec = tt.tolist()
+    elapsed, t_enc, t_dec = timed_steps(run_enc, run_dec, args.steps, dist)
 
     raw = hi.numel() * hi.element_size()           # raw highres bytes per rank per step
     value = raw * world * args.steps / elapsed / 1e9
@@ -193,28 +279,11 @@ def main():
     achieved = algo / t_dom / 1e9
     traffic = load_traffic(args.workload, args.padding, dominant)
 
-    # C4: shard one volume's tiles over the ranks, code them, all-gather the decoded tiles
-    c4 = None
-    if dist:
-        per = spec['shape'][0] // world
-        shard = hi[:per].contiguous()
-        lo_s, maps_s, dims_s = _nd._alloc_encoded(shard, coder, ndim)
-        rec_s = torch.empty_like(shard)
-        full = torch.empty((per * world, *shard.shape[1:]), dtype=torch.int16, device='cuda')
-        times = []
-        for i in range(6):
-            dist.barrier()
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            _nd.fused_encode_into(shard, predictor, coder, lo_s, maps_s, ndim, workspace=ws)
-            _nd.fused_decode_into(lo_s, maps_s, dims_s, predictor, coder, rec_s, ndim, workspace=ws)
-            dist.all_gather_into_tensor(full, rec_s.view(torch.int16))
-            torch.cuda.synchronize()
-            times.append(time.perf_counter() - t)
-        tt = torch.tensor([float(np.median(times[1:]))], dtype=torch.float64, device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        c4 = {'tiles_per_rank': per, 'ms_codec_plus_allgather': round(tt.item() * 1e3, 4),
-              'volume_GBps': round(raw / tt.item() / 1e9, 2), 'collective': 'all_gather_into_tensor (RCCL)'}
+    c4 = c4_reassembly(kom, hi, predictor, ndim, dist, world, ws) if dist else None
+
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = e2e_leg(kom, host, predictor, ndim, args.e2e_chunk)
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -231,14 +300,127 @@ def main():
                        'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
             'launch': 'hipGraph replay (one graph per direction)' if args.graph else 'eager (one ctypes launch per direction)',
-            'roofline': {'bound': 'hbm', 'kernel': f'fast3d_kernel {dominant}' if ndim == 3 else f'{dominant}',
+            'roofline': {'bound': 'hbm', 'kernel': f'fast3d_kernel {dominant}' if ndim == 3 else f'fast2d_kernel {dominant}',
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),
                          'traffic': traffic, 'algorithmic_bytes_per_launch': algo},
             'cpu_baseline': base,
         }
+        if e2e:
+            line['e2e_host'] = e2e
         if c4:
             line['c4_reassembly'] = c4
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def main_stream(args):
+    """BASELINE config C5: each GPU streams its 512 chunks of 128^3 float32 (4 GiB) from pinned
+    host memory through the codec and back (kompressor_amd.stream.TileStream, 3 streams).  One
+    step = the encode stream + the decode stream of all the rank's chunks; ``value`` = raw
+    bytes of all ranks / wall time.  Chunks are independent, so ranks share nothing."""
+    spec = dict(WORKLOADS['stream'])
+    n = args.stream_tiles or spec['shape'][0]
+    spec['shape'] = (n, *spec['shape'][1:])
+    world, rank, dist = init_dist()
+    import kompressor_amd as kom
+    from kompressor_amd import _nd
+    predictor = kom.MeanPredictor(args.padding, 3)
+    chunk_shape = spec['shape'][1:]
+    # synthetic float32 chunks: 16 distinct random chunks tiled over the batch (the codec's cost
+    # is data-independent; this keeps host generation of 4 GiB to a copy)
+    seed_chunks = np.random.default_rng(rank).standard_normal((min(16, n), *chunk_shape), dtype=np.float32)
+    src = kom.stream.pinned(spec['shape'], torch.float32)
+    for b in range(0, n, seed_chunks.shape[0]):
+        e = min(n, b + seed_chunks.shape[0])
+        src[b:e].copy_(torch.from_numpy(seed_chunks[:e - b]))
+    ts = kom.stream.TileStream(predictor, chunk_shape, torch.float32, 1, 3, 3)
+    lo, maps = ts.alloc_encoded(n)
+    out = kom.stream.pinned(spec['shape'], torch.float32)
+
+    def step():
+        ts.encode(src, lo, maps)
+        ts.synchronize()
+        t = time.perf_counter()
+        ts.decode(lo, maps, out)
+        ts.synchronize()
+        return t
+
+    step()
+    assert torch.equal(out.view(torch.uint32), src.view(torch.uint32)), 'C5 round trip is not lossless'
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t_enc = 0.0
+    for _ in range(args.steps):
+        t_s = time.perf_counter()
+        t_mid = step()
+        t_enc += t_mid - t_s
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_dec = elapsed - t_enc
+    if dist:
+        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, t_enc, t_dec = tt.tolist()
+    raw = src.numel() * 4
+
+    # kernel roofline of the same codec device-resident (the uint32 path: cell-mean + residual
+    # launches of kmp_codec_generic.hip) on a 64-chunk slice
+    k = min(64, n)
+    d_hi = src[:k].cuda().view(torch.uint32)
+    coder = _nd.NATURAL_CODER[torch.uint32]
+    d_lo, d_maps, d_dims = _nd._alloc_encoded(d_hi, coder, 3)
+    d_rec = torch.empty_like(d_hi)
+    ws = torch.empty(max(1, _nd.workspace_bytes(d_hi, predictor, 3)), dtype=torch.uint8, device='cuda')
+    enc = lambda: _nd.fused_encode_into(d_hi, predictor, coder, d_lo, d_maps, 3, workspace=ws)  # noqa: E731
+    dec = lambda: _nd.fused_decode_into(d_lo, d_maps, d_dims, predictor, coder, d_rec, 3, workspace=ws)  # noqa: E731
+    enc(), dec()
+    _, k_enc, k_dec = timed_steps(enc, dec, 5, None)
+    assert torch.equal(d_rec, d_hi)
+    kraw = d_hi.numel() * 4
+    dominant, t_dom = ('encode', k_enc) if k_enc >= k_dec else ('decode', k_dec)
+    achieved = 2 * kraw / t_dom / 1e9
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import volume as OV, predictors as OP
+        sample = src[:2].numpy().view(np.uint32)
+        pf = OP.mean_predictions_fn(args.padding, 3)
+        t = time.perf_counter()
+        lo_o, enc_o = OV.encode(pf, OV.encode_values_uint32, sample, padding=args.padding)
+        back = OV.decode(pf, OV.decode_values_uint32, lo_o, enc_o, padding=args.padding)
+        t = time.perf_counter() - t
+        assert np.array_equal(back, sample)
+        base = {'value': round(sample.nbytes / t / 1e9, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
+                'sample': f'2 of {n} chunks of 128^3, numpy restatement (oracle/, uint32 bit-cast, 1 thread), '
+                          f'{t:.2f} s'}
+    if rank == 0:
+        line = {
+            'metric': spec['metric'], 'value': round(raw * world * args.steps / elapsed / 1e9, 3), 'unit': 'GB/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'u32 (float32 bit-cast)', 'data': 'synthetic (standard normal float32)',
+            'config': {'workload': spec['name'], 'global_batch': n * world, 'tile': list(chunk_shape[:3]),
+                       'predictor': f'MeanPredictor(padding={args.padding})', 'streams': 3, 'chunk_per_copy': 1,
+                       'parallelism': f'chunks sharded, dp{world}' if world > 1 else 'single GPU'},
+            'ms_encode': round(t_enc / args.steps * 1e3, 3), 'ms_decode': round(t_dec / args.steps * 1e3, 3),
+            'roofline': {'bound': 'hbm', 'kernel': f'generic u32 {dominant} (cell_mean + residual launches)',
+                         'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'algorithmic_bytes_per_launch': 2 * kraw,
+                         'device_resident_ms': {'encode': round(k_enc * 1e3, 4), 'decode': round(k_dec * 1e3, 4),
+                                                'chunks': k}},
+            'link': {'h2d_plus_d2h_bytes_per_step': 4 * raw,
+                     'note': 'each direction moves the raw volume host->device and its coded form back'},
+            'cpu_baseline': base,
+        }
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

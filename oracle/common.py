@@ -54,6 +54,17 @@ def decode_values_uint16(pred, encoded):
     return _modular(as_int32(pred) + as_int32(encoded), 65536, np.uint16)
 
 
+def encode_values_uint32(pred, gt):
+    """Build extension (no reference counterpart): the mod-2^16 coder of
+    utils.py:48-50 widened to 2^32 for bit-cast float32 samples, ``uint32(gt - pred) mod 2^32``."""
+    return ((np.asarray(gt).astype(np.int64) - np.asarray(pred).astype(np.int64)) % (1 << 32)).astype(np.uint32)
+
+
+def decode_values_uint32(pred, encoded):
+    """Inverse of :func:`encode_values_uint32` (the utils.py:53-55 analogue)."""
+    return ((np.asarray(pred).astype(np.int64) + np.asarray(encoded).astype(np.int64)) % (1 << 32)).astype(np.uint32)
+
+
 # ---------------------------------------------------------------------------------------------
 # Categorical rank coder -- utils.py:58-111
 # ---------------------------------------------------------------------------------------------

@@ -31,7 +31,16 @@ def mean_predictions_fn(padding, ndim=3):
         lowres = np.asarray(lowres)
         features = ns.features_from_lowres(lowres, padding)
         axis = ndim + 1
-        pred = np.mean(features.astype(np.float32), axis=axis, keepdims=True, dtype=np.float32)
+        if features.dtype.itemsize < 4:
+            pred = np.mean(features.astype(np.float32), axis=axis, keepdims=True, dtype=np.float32)
+        else:
+            # 32-bit samples: the f32 sum is inexact, so its order matters.  XLA's reduce order is
+            # not pinned by the reference (its tests only use values < 2^24, where every order is
+            # exact); the build fixes the feature order (z-major, y, x), one rounding per add.
+            pred = np.zeros(features.shape[:axis] + (1,) + features.shape[axis + 1:], np.float32)
+            for n in range(features.shape[axis]):
+                pred += np.take(features, [n], axis=axis).astype(np.float32)
+            pred = pred / np.float32(features.shape[axis])
         pred = cast_from_f32(pred, lowres.dtype)
         pred = np.repeat(pred, k, axis=axis)
         return ns.maps_from_predictions(pred)

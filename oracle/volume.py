@@ -12,7 +12,8 @@ import numpy as np
 
 from .common import (cast_from_f32, validate_padding, yield_chunks,  # noqa: F401
                      encode_values_raw, decode_values_raw, encode_values_uint8, decode_values_uint8,
-                     encode_values_uint16, decode_values_uint16, encode_categorical, decode_categorical)
+                     encode_values_uint16, decode_values_uint16, encode_categorical, decode_categorical,
+                     encode_values_uint32, decode_values_uint32)
 
 MAP_NAMES = ('lr', 'ud', 'fb', 'c', 'z', 'y', 'x')
 
