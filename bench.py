@@ -152,33 +152,49 @@ def init_dist():
 
 
 def timed_steps(run_enc, run_dec, steps, dist):
-    """EXACTLY ``steps`` (encode, decode) pairs bracketed by barrier + synchronize; HIP events on
-    the launch stream give the per-direction kernel time.  Returns wall seconds and mean
-    per-direction seconds, each the max over ranks."""
-    stream = torch.cuda.current_stream()  # the stream the kernels / graphs are launched on
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    """EXACTLY ``steps`` (encode, decode) pairs bracketed by barrier + synchronize on both sides;
+    wall seconds, max over ranks.  Nothing else is enqueued inside the region."""
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        e0.record(stream)
+    for _ in range(steps):
         run_enc()
-        e1.record(stream)
         run_dec()
-        e2.record(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t_enc = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
-    t_dec = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
     if dist:
-        tt = torch.tensor([elapsed, t_enc, t_dec], dtype=torch.float64, device='cuda')
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, t_enc, t_dec = tt.tolist()
-    return elapsed, t_enc, t_dec
+        elapsed = tt.item()
+    return elapsed
+
+
+def direction_times(run_enc, run_dec, n, dist):
+    """Average kernel duration per direction from HIP events on the launch stream, each over
+    ``n`` back-to-back launches of that direction (one event pair per run, so the markers do
+    not add to every launch); max over ranks.  This is what ``roofline.achieved`` divides by
+    and what the committed rocprofv3 kernel statistics must agree with."""
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    torch.cuda.synchronize()
+    ev[0].record(stream)
+    for _ in range(n):
+        run_enc()
+    ev[1].record(stream)
+    for _ in range(n):
+        run_dec()
+    ev[2].record(stream)
+    torch.cuda.synchronize()
+    t_enc = ev[0].elapsed_time(ev[1]) / n / 1e3
+    t_dec = ev[1].elapsed_time(ev[2]) / n / 1e3
+    if dist:
+        tt = torch.tensor([t_enc, t_dec], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_enc, t_dec = tt.tolist()
+    return t_enc, t_dec
 
 
 def c4_reassembly(kom, hi, predictor, ndim, dist, world, ws):
@@ -268,7 +284,8 @@ def main():
             run_dec()
         torch.cuda.synchronize()
         assert torch.equal(rec, hi), 'graph replay round trip is not lossless'
-    elapsed, t_enc, t_dec = timed_steps(run_enc, run_dec, args.steps, dist)
+    elapsed = timed_steps(run_enc, run_dec, args.steps, dist)
+    t_enc, t_dec = direction_times(run_enc, run_dec, max(args.steps, 10), dist)
 
     raw = hi.numel() * hi.element_size()           # raw highres bytes per rank per step
     value = raw * world * args.steps / elapsed / 1e9
@@ -382,7 +399,7 @@ def main_stream(args):
     enc = lambda: _nd.fused_encode_into(d_hi, predictor, coder, d_lo, d_maps, 3, workspace=ws)  # noqa: E731
     dec = lambda: _nd.fused_decode_into(d_lo, d_maps, d_dims, predictor, coder, d_rec, 3, workspace=ws)  # noqa: E731
     enc(), dec()
-    _, k_enc, k_dec = timed_steps(enc, dec, 5, None)
+    k_enc, k_dec = direction_times(enc, dec, 5, None)
     assert torch.equal(d_rec, d_hi)
     kraw = d_hi.numel() * 4
     dominant, t_dom = ('encode', k_enc) if k_enc >= k_dec else ('decode', k_dec)

@@ -9,7 +9,7 @@ mkdir -p $OUT
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --steps 20 > $OUT/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-e2e --steps 20 > $OUT/prof.log 2>&1
 rc=$?
 tail -3 $OUT/pytest_gpu.log; cat $OUT/bench.log | tail -2
 exit $rc
