@@ -1,0 +1,25 @@
+"""Launch the fused volume/image codec N times per direction (for rocprofv3 --kernel-trace --stats).
+    python tools/ktime.py [volume|image] [padding] [reps]"""
+import os, sys
+import numpy as np, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import kompressor_amd as kom
+from kompressor_amd import _nd
+
+wl = sys.argv[1] if len(sys.argv) > 1 else 'volume'
+p = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+ndim = 3 if wl == 'volume' else 2
+shape, dt = ((512, 64, 64, 64, 1), np.uint16) if ndim == 3 else ((1024, 256, 256, 1), np.uint8)
+host = np.random.default_rng(0).integers(0, np.iinfo(dt).max + 1, size=shape, dtype=np.int64).astype(dt)
+hi = torch.from_numpy(host).cuda()
+pred = kom.MeanPredictor(p, ndim)
+coder = _nd.NATURAL_CODER[hi.dtype]
+lo, maps, dims = _nd._alloc_encoded(hi, coder, ndim)
+rec = torch.empty_like(hi)
+for _ in range(reps):
+    _nd.fused_encode_into(hi, pred, coder, lo, maps, ndim)
+    _nd.fused_decode_into(lo, maps, dims, pred, coder, rec, ndim)
+torch.cuda.synchronize()
+assert torch.equal(rec, hi)
+print('ok', os.environ.get('KMP_TAG', ''))

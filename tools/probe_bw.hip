@@ -43,6 +43,69 @@ __global__ void merge8(const u32x2* __restrict__ in, u32x4* __restrict__ b, int6
   }
 }
 
+// block-owned regions: block k streams its own ``region`` bytes in 16 KiB steps (the codec's
+// z-slab walk), optionally with XCD-contiguous block order
+__global__ void region_copy(const u32x4* __restrict__ a, u32x4* __restrict__ b, int64_t region16, int steps,
+                            int xcd_per) {
+  const int blk = xcd_per > 0 ? (int)(blockIdx.x % 8) * xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int64_t base = (int64_t)blk * region16;
+  const int64_t per_step = region16 / steps;
+  for (int s = 0; s < steps; ++s)
+    for (int64_t i = threadIdx.x; i < per_step; i += blockDim.x) {
+      const int64_t o = base + s * per_step + i;
+      __builtin_nontemporal_store(__builtin_nontemporal_load(a + o), b + o);
+    }
+}
+
+// row-strided reads: a wave covers 2 KiB = 16 lines of 128 B; instruction 1 reads the even
+// lines (8 x 128 B at 256 B stride, the codec's "row 2Y" loads), instruction 2 the odd lines.
+// STRIDED = 0 reads the same 2 KiB as two contiguous 1 KiB halves.  Writes 2 x 1 KiB contiguous.
+template <int STRIDED>
+__global__ void rows_copy(const u32x4* __restrict__ a, u32x4* __restrict__ b, int64_t nchunks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c < nchunks; c += nw) {
+    const int64_t base = c * 128;  // 2 KiB in 16-B units
+    int64_t i0, i1;
+    if (STRIDED) {
+      i0 = base + (lane >> 3) * 16 + (lane & 7);
+      i1 = i0 + 8;
+    } else {
+      i0 = base + lane;
+      i1 = base + 64 + lane;
+    }
+    u32x4 v0 = __builtin_nontemporal_load(a + i0);
+    u32x4 v1 = __builtin_nontemporal_load(a + i1);
+    __builtin_nontemporal_store(v0, b + base + lane);
+    __builtin_nontemporal_store(v1, b + base + 64 + lane);
+  }
+}
+
+// codec-shaped copy: the exact access pattern of the volume encode at C3 (512 tiles of 64^3 u16,
+// 256-thread workgroup = one z-slab of one tile, wave w owns rows 8w..8w+7, lane = (row, 8 x 16 B)):
+// per output plane, read rows 2Y, 2Y+1 of planes 2c, 2c+1 (4 x 16 B per lane), write 8 x 8 B per
+// lane into 8 separate [512, 32, 32, 32] arrays.  No arithmetic.
+__global__ void __launch_bounds__(256) codec_shape(const uint16_t* __restrict__ hi, uint16_t* __restrict__ out,
+                                                   int nslab) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tx = lane & 7, Y = w * 8 + (lane >> 3), X = tx * 4;
+  const int b = blockIdx.x / nslab, sl = blockIdx.x % nslab;
+  const int slab = 32 / nslab;
+  const uint16_t* t = hi + (int64_t)b * 262144;
+  for (int c = sl * slab; c < (sl + 1) * slab; ++c) {
+    const uint16_t* p = t + 2 * c * 4096 + 2 * Y * 64 + 2 * X;
+    u32x4 e0 = __builtin_nontemporal_load((const u32x4*)p);
+    u32x4 e1 = __builtin_nontemporal_load((const u32x4*)(p + 64));
+    u32x4 o0 = __builtin_nontemporal_load((const u32x4*)(p + 4096));
+    u32x4 o1 = __builtin_nontemporal_load((const u32x4*)(p + 4096 + 64));
+    const int64_t o = (int64_t)b * 32768 + c * 1024 + Y * 32 + X;
+    u32x2 v[8] = {{e0.x, e0.y}, {e0.z, e0.w}, {e1.x, e1.y}, {e1.z, e1.w}, {o0.x, o0.y}, {o0.z, o0.w}, {o1.x, o1.y}, {o1.z, o1.w}};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(v[k], (u32x2*)(out + (int64_t)k * 16777216 + o));
+  }
+}
+
 int main() {
   const size_t bytes = 256ull << 20;
   const int64_t n16 = bytes / 16;
@@ -70,6 +133,29 @@ int main() {
     char nm[64];
     snprintf(nm, sizeof nm, "copy16 grid=%d", blocks);
     run(nm, [&] { copy16<<<blocks, 256>>>((const u32x4*)a, (u32x4*)b, n16); });
+  }
+  for (int nslab : {1, 4, 8, 32}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "codec_shape nslab=%d", nslab);
+    run(nm, [&] { codec_shape<<<512 * nslab, 256>>>((const uint16_t*)a, (uint16_t*)b, nslab); });
+  }
+  for (int blocks : {4096, 8192}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "rows contiguous grid=%d", blocks);
+    run(nm, [&] { rows_copy<0><<<blocks, 256>>>((const u32x4*)a, (u32x4*)b, n16 / 128); });
+    snprintf(nm, sizeof nm, "rows strided grid=%d", blocks);
+    run(nm, [&] { rows_copy<1><<<blocks, 256>>>((const u32x4*)a, (u32x4*)b, n16 / 128); });
+  }
+  for (int steps : {1, 4}) {
+    for (int xcd : {0, 1}) {
+      for (int64_t region : {16384, 65536}) {
+        const int64_t r16 = region / 16 * steps / (region == 16384 ? steps : 1);
+        const int blocks = (int)(n16 / r16);
+        char nm[96];
+        snprintf(nm, sizeof nm, "region %lldK steps=%d xcd=%d", (long long)(r16 * 16 / 1024), steps, xcd);
+        run(nm, [&] { region_copy<<<blocks, 256>>>((const u32x4*)a, (u32x4*)b, r16, steps, xcd ? blocks / 8 : 0); });
+      }
+    }
   }
   const int64_t per = n16 / 4;  // u32x2 elements per output stream
   for (int blocks : {2048, 4096, 8192}) {
