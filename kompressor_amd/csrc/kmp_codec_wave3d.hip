@@ -1,23 +1,27 @@
-// kmp_codec_wave3d.hip -- barrier-free one-pass volume encode / decode for the mean predictor
-// with p == 0 (the metric path: BASELINE config C3, MeanPredictor(0) on uint16 64^3 tiles).
+// kmp_codec_wave3d.hip -- one-pass volume encode / decode for the mean predictor with p == 0
+// (the metric path: BASELINE config C3, MeanPredictor(0) + the uint16 coder on 64^3 tiles).
 //
 // Same arithmetic as kmp_codec_fast3d.hip (which keeps p = 1, 2), different data movement:
-// every wavefront is independent.  A wave owns ROWS = 64 / TXN consecutive output rows
-// (TXN = Ex / VX lanes per row, VX outputs per lane = 8 bytes of lowres) of one z-slab of one
-// tile and rolls along z; all neighbour exchange is cross-lane (ds_bpermute shuffles), so there
-// is no LDS ring and no workgroup barrier:
-//   * node row y+1 of a cell is the shuffle of the lane TXN below; the wave's last row loads
-//     its own halo row (mirrored at the even-padded edge, volume/utils.py:226-237), and its
-//     first row loads the row above to build the cell-mean row y-1;
-//   * node x+VX is the shuffle of the next lane; the row's last lane mirrors it;
-//   * the cell-mean planes c-1 / c and the node row of plane c live in registers across steps.
-// Per step j (node plane j) a lane computes the cell means of plane c = j-1 (2x2x2 node sums,
-// floor / 8 == the reference test predictor's f32 mean + truncation, tests/volume/
-// test_encode_decode.py:46-51), the 19-way aggregation onto the 7 maps for output plane c
-// (volume/utils.py:83-155, sums of 1/2/4 means >> log2(count) == its f32 x0.5 / x0.25 +
-// truncation here), and the mod-2^k coder (utils.py:38-55).  Global loads run one step ahead:
-// node row j+1 and the stream rows of output plane j are issued during step j, consumed in
-// step j+1 (two register sets alternated by unrolling the step loop by two).
+//   * A workgroup owns PL = 2 consecutive output planes of one tile and issues EVERY global load
+//     of its planes up front (node rows of node planes c0-1 .. c0+PL, the stream rows of its PL
+//     output planes), then computes: no z-rolling, no LDS, no barrier.  Short workgroups
+//     dispatched in order keep the resident set on one contiguous window of the volume -- the
+//     access order that reaches the probe ceiling for this shape (tools/probe_bw.hip
+//     codec_shape: 6.0 TB/s at one plane per workgroup vs 4.9 TB/s for 4-plane rolling slabs).
+//   * Tile-per-XCD block order: XCD x = blockIdx % 8 codes whole tiles, so the two z-halo node
+//     planes a workgroup shares with its neighbours are L2 hits (default-policy loads): HBM
+//     traffic measured by PMC equals the algorithmic bytes (profiles/pmc_traffic.json).
+//   * Every wavefront is independent: it owns ROWS = 64 / TXN output rows (TXN = Ex / VX lanes
+//     per row, VX outputs per lane = 8 bytes of lowres).  Neighbour exchange is cross-lane
+//     (ds_bpermute shuffles): node row y+1 from the lane TXN below, node x+VX from the next lane
+//     (mirrored on the row's last lane: even reflect pad, volume/utils.py:226-237); the wave's
+//     first / last row loads one halo row each.
+// Per output plane c a lane forms the cell means of planes c-1 and c (2x2x2 node sums, floor / 8
+// == the reference test predictor's f32 mean + truncation, tests/volume/test_encode_decode.py:
+// 46-51), the 19-way aggregation onto the 7 maps (volume/utils.py:83-155: sums of 1/2/4 means
+// >> log2(count) == its f32 x0.5 / x0.25 + truncation for these ranges) and the mod-2^k coder
+// (utils.py:38-55), then writes lowres + 7 maps (8 B per lane each) or the 2x2x2 highres block
+// rows (16 B per lane each).
 #include <cstdlib>
 
 #include "kmp_codec.h"
@@ -36,6 +40,10 @@ __device__ __forceinline__ uint2 ld8(const void* p) {
   const u32x2 v = __builtin_nontemporal_load((const u32x2*)p);
   return make_uint2(v.x, v.y);
 }
+// default-policy loads: for bytes another workgroup re-reads soon (z-halo node rows), which must
+// stay in L2 rather than stream past it
+__device__ __forceinline__ uint4 ld16c(const void* p) { return *(const uint4*)p; }
+__device__ __forceinline__ uint2 ld8c(const void* p) { return *(const uint2*)p; }
 __device__ __forceinline__ void st16(void* p, uint4 v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, (u32x4*)p);
@@ -103,13 +111,14 @@ struct W3 {
   int32_t slab, nslab, zbegin, zend;
   int32_t txn, rows, nwv, nyg;
   int32_t xcd_per;  // > 0: XCD-contiguous block order (blocks per XCD), 0: identity
+  int32_t nt_nodes; // plane kernel: 1 = non-temporal node-row loads, 0 = default policy (L2-shared halo)
 };
 
-// rows a lane reads for one node plane: its own, and the halo rows of the wave's edge rows
+// rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row
 template <bool DEC>
 struct NodeRows {
   using V = typename std::conditional<DEC, uint2, uint4>::type;
-  V own, up, dn;
+  V own, halo;
 };
 // encode: the non-node rows of output plane q (plane 2q row 2Y+1, plane 2q+1 rows 2Y, 2Y+1)
 // decode: the 7 residual rows of output plane q
@@ -119,268 +128,9 @@ struct OutRows {
   uint2 mv[7];
 };
 
-template <typename T, bool DEC>
-__global__ void __launch_bounds__(256) wave3d_kernel(W3 a) {
-  constexpr int VX = 8 / (int)sizeof(T);
-  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
-  using NR = NodeRows<DEC>;
-  using OR = OutRows<DEC>;
-
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
-  const int X = tx * VX;
-  // Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8).  With xcd_per > 0 the logical
-  // block order is remapped so that each XCD walks ONE contiguous run of blocks: consecutive
-  // z-slabs of a tile (which share a halo plane) meet in the same L2, and each XCD streams its
-  // own contiguous 1/8 of the volume.
-  int blk = a.xcd_per > 0 ? (int)(blockIdx.x % 8) * a.xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const int yg = blk % a.nyg;
-  blk /= a.nyg;
-  const int sl = blk % a.nslab;
-  const int64_t b = blk / a.nslab;
-  const int Y0 = (yg * a.nwv + wv) * a.rows;
-  if (Y0 >= a.Ey) return;  // a whole idle wave: nothing in this kernel waits on it
-  const int Y = Y0 + r;
-  const bool live = Y < a.Ey;
-  const int Yc = live ? Y : a.Ey - 1;  // idle lanes keep valid addresses; they only feed shuffles
-  const int Z0 = a.zbegin + sl * a.slab;
-  const int Z1 = Z0 + a.slab < a.zend ? Z0 + a.slab : a.zend;
-  if (Z0 >= Z1) return;
-
-  const bool first = r == 0;
-  const bool last = r == a.rows - 1 || Y == a.Ey - 1;
-  const bool vy1 = Y < a.Lcy;  // cell row Y (== highres row 2Y+1) exists
-  const bool vy0 = Y >= 1;     // cell row Y-1 exists
-  const bool need_up = live && first && Y0 >= 1;
-  const bool need_dn = live && last && vy1;
-  const int yup = Y0 >= 1 ? Y0 - 1 : 0;
-  const int ydn = lsrc(Yc + 1, a.Ly, a.Ey);
-  const bool xlast = tx == a.txn - 1;
-
-  // 32-bit offsets inside one tile; 64-bit tile bases
-  const int hplane = a.H * a.W;
-  const int lplane = a.Ey * a.Ex;
-  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
-  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
-  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
-  const int hx = 2 * X;
-  const int ho_own = 2 * Yc * a.W + hx, ho_up = 2 * yup * a.W + hx, ho_dn = 2 * ydn * a.W + hx;
-  const int lo_own = Yc * a.Ex + X, lo_up = yup * a.Ex + X, lo_dn = ydn * a.Ex + X;
-
-  // map k: [B, ez, ey, Ex] with ez = Lcz / Ez and ey = Lcy / Ey by its parity
-  const T* mbase[7];
-  int mplane[7];
-  bool mok_y[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    int par[3];
-    map_parity(3, k, par);
-    const int ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
-    mplane[k] = ey * a.Ex;
-    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + Yc * a.Ex + X;
-    mok_y[k] = live && (!par[1] || vy1);
-  }
-
-  auto load_nodes = [&](int j, NR& N) {
-    const int sz = lsrc(j, a.Lz, a.Ez);
-    if constexpr (DEC) {
-      const T* p = lin + sz * lplane;
-      if (live) N.own = ld8(p + lo_own);
-      if (need_up) N.up = ld8(p + lo_up);
-      if (need_dn) N.dn = ld8(p + lo_dn);
-    } else {
-      const T* p = hin + 2 * sz * hplane;
-      if (live) N.own = ld16(p + ho_own);
-      if (need_up) N.up = ld16(p + ho_up);
-      if (need_dn) N.dn = ld16(p + ho_dn);
-    }
-  };
-  auto load_out = [&](int q, OR& O) {
-    const bool vz1 = q < a.Lcz;
-    if constexpr (DEC) {
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        int par[3];
-        map_parity(3, k, par);
-        if (mok_y[k] && (!par[0] || vz1)) O.mv[k] = ld8(mbase[k] + q * mplane[k]);
-      }
-    } else {
-      const T* p = hin + 2 * q * hplane;
-      if (live && vy1) O.e1 = ld16(p + ho_own + a.W);
-      if (live && vz1) O.o0 = ld16(p + hplane + ho_own);
-      if (live && vz1 && vy1) O.o1 = ld16(p + hplane + ho_own + a.W);
-    }
-  };
-  auto nodes_of = [&](const typename NR::V& v, uint32_t (&n)[VX]) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) n[i] = el8<T>(v, i);
-      else n[i] = el16<T>(v, 2 * i);
-    }
-  };
-
-  // cross-step state
-  uint32_t Sp[VX], Sup[VX];            // 2x2 node sums of the previous node plane (own / above row)
-  uint32_t Mo_p[VX + 1], Ma_p[VX + 1];  // cell means of plane c-1: row Y / row Y-1, cols X-1 .. X+VX-1
-  typename NR::V prev_own{};            // node row of plane c (lowres output / decode own samples)
-#pragma unroll
-  for (int i = 0; i < VX; ++i) Sp[i] = Sup[i] = 0;
-#pragma unroll
-  for (int i = 0; i <= VX; ++i) Mo_p[i] = Ma_p[i] = 0;
-
-  const int jstart = Z0 - 1 > 0 ? Z0 - 1 : 0;
-  const int jend = Z1;
-
-  auto step = [&](int j, const NR& Nc, NR& Nn, const OR& Oc, OR& On) __attribute__((always_inline)) {
-    if (j < jend) load_nodes(j + 1, Nn);
-    if (j >= Z0 && j < Z1) load_out(j, On);
-
-    // ---- 2x2 node sums of node plane j: rows Y (own), Y-1 (wave's first row) ----
-    uint32_t n[VX], nu[VX], nd[VX];
-    nodes_of(Nc.own, n);
-    nodes_of(Nc.up, nu);
-    nodes_of(Nc.dn, nd);
-    uint32_t nx1 = shdn(n[0], 1), nux1 = shdn(nu[0], 1), ndx1 = shdn(nd[0], 1);
-    if (xlast) {  // node X+VX = Ex: the mirrored node Ex-1 (even pad), or no cell at all (odd)
-      nx1 = n[VX - 1];
-      nux1 = nu[VX - 1];
-      ndx1 = nd[VX - 1];
-    }
-    uint32_t h[VX], hu[VX], hd[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      h[i] = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
-      hu[i] = nu[i] + (i + 1 < VX ? nu[i + 1] : nux1);
-      hd[i] = nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1);
-    }
-    uint32_t S[VX], Su[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t below = shdn(h[i], a.txn);
-      S[i] = h[i] + (last ? hd[i] : below);
-      Su[i] = hu[i] + h[i];
-    }
-
-    const int c = j - 1;
-    if (j > jstart) {
-      // ---- cell means of plane c (nodes planes c, c+1): floor(sum of 8 / 8) ----
-      uint32_t Mo[VX + 1], Ma[VX + 1];
-#pragma unroll
-      for (int i = 0; i < VX; ++i) {
-        Mo[i + 1] = (Sp[i] + S[i]) >> 3;
-        const uint32_t mu = (Sup[i] + Su[i]) >> 3;
-        const uint32_t above = shup(Mo[i + 1], a.txn);
-        Ma[i + 1] = first ? mu : above;
-      }
-      Mo[0] = shup(Mo[VX], 1);
-      Ma[0] = shup(Ma[VX], 1);
-
-      if (c >= Z0 && c < Z1) {
-        const bool vz1 = c < a.Lcz, vz0 = c >= 1;
-        // M[dz][dy][q]: cell plane c-1+dz, row Y-1+dy, col X-1+q (0 where the cell is absent)
-        uint32_t M[2][2][VX + 1];
-        bool vx[VX + 1];
-#pragma unroll
-        for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
-#pragma unroll
-        for (int q = 0; q <= VX; ++q) {
-          M[0][0][q] = (vz0 && vy0 && vx[q]) ? Ma_p[q] : 0u;
-          M[0][1][q] = (vz0 && vy1 && vx[q]) ? Mo_p[q] : 0u;
-          M[1][0][q] = (vz1 && vy0 && vx[q]) ? Ma[q] : 0u;
-          M[1][1][q] = (vz1 && vy1 && vx[q]) ? Mo[q] : 0u;
-        }
-        const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
-        const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
-        uint32_t pred[7][VX];  // LR, UD, FB, C, Z, Y, X
-#pragma unroll
-        for (int i = 0; i < VX; ++i) {
-          const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-          pred[0][i] = (M[1][1][i] + M[1][1][i + 1]) >> (nx >> 1);
-          pred[1][i] = (M[1][0][i + 1] + M[1][1][i + 1]) >> (ny >> 1);
-          pred[2][i] = (M[0][1][i + 1] + M[1][1][i + 1]) >> (nz >> 1);
-          pred[3][i] = M[1][1][i + 1];
-          pred[4][i] = (M[1][0][i] + M[1][0][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((ny * nx) >> 1);
-          pred[5][i] = (M[0][1][i] + M[0][1][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((nz * nx) >> 1);
-          pred[6][i] = (M[0][0][i + 1] + M[0][1][i + 1] + M[1][0][i + 1] + M[1][1][i + 1]) >> ((nz * ny) >> 1);
-        }
-        if (live) {
-          if constexpr (!DEC) {
-            const uint4 e0 = prev_own;
-            uint32_t res[7][VX], lov[VX];
-#pragma unroll
-            for (int i = 0; i < VX; ++i) {
-              lov[i] = el16<T>(e0, 2 * i);
-              res[0][i] = (el16<T>(Oc.o1, 2 * i) - pred[0][i]) & MASK;      // LR (1,1,0)
-              res[1][i] = (el16<T>(Oc.o0, 2 * i + 1) - pred[1][i]) & MASK;  // UD (1,0,1)
-              res[2][i] = (el16<T>(Oc.e1, 2 * i + 1) - pred[2][i]) & MASK;  // FB (0,1,1)
-              res[3][i] = (el16<T>(Oc.o1, 2 * i + 1) - pred[3][i]) & MASK;  // C  (1,1,1)
-              res[4][i] = (el16<T>(Oc.o0, 2 * i) - pred[4][i]) & MASK;      // Z  (1,0,0)
-              res[5][i] = (el16<T>(Oc.e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
-              res[6][i] = (el16<T>(e0, 2 * i + 1) - pred[6][i]) & MASK;     // X  (0,0,1)
-            }
-            st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-              int par[3];
-              map_parity(3, k, par);
-              if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
-            }
-          } else {
-            uint32_t own[VX], dv[7][VX];
-#pragma unroll
-            for (int i = 0; i < VX; ++i) own[i] = el8<T>(prev_own, i);
-#pragma unroll
-            for (int k = 0; k < 7; ++k)
-#pragma unroll
-              for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(Oc.mv[k], i)) & MASK;
-            T* h0 = hout + 2 * c * hplane + ho_own;
-            st16(h0, pack16<T, VX>(own, dv[6]));                    // plane 2c, row 2Y: lowres | X
-            if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[5], dv[2]));  // plane 2c, row 2Y+1: Y | FB
-            if (vz1) {
-              T* h1 = h0 + hplane;
-              st16(h1, pack16<T, VX>(dv[4], dv[1]));                    // plane 2c+1, row 2Y: Z | UD
-              if (vy1) st16(h1 + a.W, pack16<T, VX>(dv[0], dv[3]));  // plane 2c+1, row 2Y+1: LR | C
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q <= VX; ++q) {
-        Mo_p[q] = Mo[q];
-        Ma_p[q] = Ma[q];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      Sp[i] = S[i];
-      Sup[i] = Su[i];
-    }
-    prev_own = Nc.own;
-  };
-
-  NR NA{}, NB{};
-  OR OA{}, OB{};
-  load_nodes(jstart, NA);
-  for (int j = jstart; j <= jend; j += 2) {
-    step(j, NA, NB, OA, OB);
-    if (j + 1 > jend) break;
-    step(j + 1, NB, NA, OB, OA);
-  }
-}
-
-
-// Plane-block form (the default): a workgroup owns PL consecutive output planes of one tile and
-// issues EVERY global load of its planes up front -- node rows of node planes c0-1 .. c0+PL
-// (the two outer ones are the z halo, read again by the neighbouring plane-blocks and served by
-// L2 when those run on the same XCD) and the stream rows of its PL output planes -- then
-// computes.  Short workgroups dispatched in order keep the set of resident workgroups on one
-// contiguous window of the volume, which is what reaches the probe ceiling for this access
-// shape (tools/probe_bw.hip codec_shape: 6.0 TB/s at one plane per workgroup vs 4.9 TB/s for
-// 4-plane rolling slabs).
-template <typename T, bool DEC, int PL>
-__global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
+// WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
+template <typename T, bool DEC, int PL, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   using NR = NodeRows<DEC>;
@@ -426,6 +176,7 @@ __global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
   T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
   const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
   const int hx = 2 * X;
+  // a lane is never both the wave's first and last row (host eligibility), so one halo row each
   const int ho_own = 2 * Yc * a.W + hx, ho_up = 2 * yup * a.W + hx, ho_dn = 2 * ydn * a.W + hx;
   const int lo_own = Yc * a.Ex + X, lo_up = yup * a.Ex + X, lo_dn = ydn * a.Ex + X;
 
@@ -453,14 +204,20 @@ __global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
     const int sz = lsrc(q, a.Lz, a.Ez);
     if constexpr (DEC) {
       const T* p = lin + sz * lplane;
-      if (live) N[t].own = ld8(p + lo_own);
-      if (need_up) N[t].up = ld8(p + lo_up);
-      if (need_dn) N[t].dn = ld8(p + lo_dn);
+      if (a.nt_nodes) {
+        if (live) N[t].own = ld8(p + lo_own);
+      } else {
+        if (live) N[t].own = ld8c(p + lo_own);
+      }
+      if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
     } else {
       const T* p = hin + 2 * sz * hplane;
-      if (live) N[t].own = ld16(p + ho_own);
-      if (need_up) N[t].up = ld16(p + ho_up);
-      if (need_dn) N[t].dn = ld16(p + ho_dn);
+      if (a.nt_nodes) {
+        if (live) N[t].own = ld16(p + ho_own);
+      } else {
+        if (live) N[t].own = ld16c(p + ho_own);
+      }
+      if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
     }
   }
 #pragma unroll
@@ -488,36 +245,35 @@ __global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
   uint32_t S[PL + 2][VX], Su[PL + 2][VX];
 #pragma unroll
   for (int t = 0; t < PL + 2; ++t) {
-    uint32_t n[VX], nu[VX], nd[VX];
+    // own node row, and the halo row (row Y0-1 on the wave's first row, Y+1 on its last row)
+    uint32_t n[VX], nh[VX];
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       if constexpr (DEC) {
-        n[i] = el8<T>(N[t].own, i); nu[i] = el8<T>(N[t].up, i); nd[i] = el8<T>(N[t].dn, i);
+        n[i] = el8<T>(N[t].own, i); nh[i] = el8<T>(N[t].halo, i);
       } else {
-        n[i] = el16<T>(N[t].own, 2 * i); nu[i] = el16<T>(N[t].up, 2 * i); nd[i] = el16<T>(N[t].dn, 2 * i);
+        n[i] = el16<T>(N[t].own, 2 * i); nh[i] = el16<T>(N[t].halo, 2 * i);
       }
     }
-    uint32_t nx1 = shdn(n[0], 1), nux1 = shdn(nu[0], 1), ndx1 = shdn(nd[0], 1);
+    uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1);
     if (xlast) {
       nx1 = n[VX - 1];
-      nux1 = nu[VX - 1];
-      ndx1 = nd[VX - 1];
+      nhx1 = nh[VX - 1];
     }
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
-      const uint32_t hu = nu[i] + (i + 1 < VX ? nu[i + 1] : nux1);
-      const uint32_t hd = nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1);
+      const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
       const uint32_t below = shdn(h, a.txn);
-      S[t][i] = h + (last ? hd : below);
-      Su[t][i] = hu + h;
+      S[t][i] = h + (last ? hh : below);
+      Su[t][i] = hh + h;
     }
   }
 
-  // ---- cell means of cell planes c0-1+m (m = 0..PL): rows Y / Y-1, cols X-1 .. X+VX-1 ----
+  // ---- cell means of cell plane c0-1+m (m = 0..PL): rows Y / Y-1, cols X-1 .. X+VX-1; computed
+  // just before the output plane that first needs them so that at most two sets are live ----
   uint32_t Mo[PL + 1][VX + 1], Ma[PL + 1][VX + 1];
-#pragma unroll
-  for (int m = 0; m <= PL; ++m) {
+  auto cell_means = [&](int m) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       Mo[m][i + 1] = (S[m][i] + S[m + 1][i]) >> 3;
@@ -527,9 +283,9 @@ __global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
     }
     Mo[m][0] = shup(Mo[m][VX], 1);
     Ma[m][0] = shup(Ma[m][VX], 1);
-  }
+  };
+  cell_means(0);
 
-  if (!live) return;
   bool vx[VX + 1];
 #pragma unroll
   for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
@@ -539,6 +295,8 @@ __global__ void __launch_bounds__(256) wave3d_plane_kernel(W3 a) {
   for (int u = 0; u < PL; ++u) {
     const int c = c0 + u;
     if (c >= Z1) break;
+    cell_means(u + 1);  // all lanes (shuffles), before the idle ones drop out
+    if (!live) continue;
     const bool vz1 = c < a.Lcz, vz0 = c >= 1;
     uint32_t M[2][2][VX + 1];
 #pragma unroll
@@ -616,7 +374,7 @@ static int w3_env(const char* name, int dflt) {
 
 template <typename T>
 static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
-                            bool roll, int pl, w3::W3& a, dim3& grid, dim3& block) {
+                            int pl, w3::W3& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
   if (w3_env("KMP_DISABLE_WAVE", 0) || w3_env("KMP_DISABLE_FAST", 0)) return false;
@@ -626,6 +384,7 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   const int64_t txn = g.E[2] / VX;
   if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
   const int64_t rows = 64 / txn;
+  if (g.E[1] % rows == 1) return false;  // a one-row wave would need both halo rows
   const int64_t waves = ceil_div(g.E[1], rows);
   const int64_t nwv = waves < 4 ? waves : 4;
   const int64_t nyg = ceil_div(waves, nwv);
@@ -644,39 +403,23 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   const int64_t zext = ze - zb;
   a.zbegin = (int)zb;
   a.zend = (int)ze;
-  int64_t nslab, slab;
-  if (roll) {
-    // rolling z slabs (KMP_W3_ROLL=1): enough workgroups to cover the chip several times over
-    const int64_t want = w3_env("KMP_W3_WG_TARGET", 4096);
-    nslab = ceil_div(want, B * nyg > 0 ? B * nyg : 1);
-    if (nslab > zext) nslab = zext;
-    if (nslab < 1) nslab = 1;
-    slab = ceil_div(zext, nslab);
-    const int64_t min_slab = w3_env("KMP_W3_MIN_SLAB", 4);
-    if (slab < min_slab) slab = min_slab < zext ? min_slab : zext;
-    nslab = ceil_div(zext, slab);
-  } else {
-    slab = pl;  // plane blocks of PL output planes
-    nslab = ceil_div(zext, slab);
-  }
-  a.slab = (int)slab;
+  const int64_t nslab = ceil_div(zext, (int64_t)pl);  // plane blocks of PL output planes
+  a.slab = pl;
   a.nslab = (int)nslab;
   const int64_t nblk = B * nslab * nyg;
-  if (roll) {
-    a.xcd_per = (w3_env("KMP_W3_XCD", 0) && nblk % 8 == 0) ? (int)(nblk / 8) : 0;
-  } else {
-    a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
-  }
+  a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
+  a.nt_nodes = w3_env("KMP_W3_NT_NODES", 0);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);
 }
 
 template <typename T, bool DEC>
-static void launch_wave3d(bool roll, int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
-  if (roll) w3::wave3d_kernel<T, DEC><<<grid, block, 0, stream>>>(a);
-  else if (pl == 2) w3::wave3d_plane_kernel<T, DEC, 2><<<grid, block, 0, stream>>>(a);
-  else w3::wave3d_plane_kernel<T, DEC, 1><<<grid, block, 0, stream>>>(a);
+static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
+  // PL = 2 at 3 waves / SIMD is the measured optimum at C3 (profiles/round1/kprof_wave3d.log):
+  // PL = 1 re-reads twice the z halo per output plane; forcing 4 waves / SIMD spills
+  if (pl == 1) w3::wave3d_plane_kernel<T, DEC, 1, 4><<<grid, block, 0, stream>>>(a);
+  else w3::wave3d_plane_kernel<T, DEC, 2, 3><<<grid, block, 0, stream>>>(a);
 }
 
 template <typename T>
@@ -685,16 +428,15 @@ int try_wave3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w3::W3 a{};
     dim3 grid, block;
-    const bool roll = w3_env("KMP_W3_ROLL", 0) != 0;
-    const int pl = w3_env("KMP_W3_PL", 1) == 2 ? 2 : 1;
-    if (!wave3d_geometry<T>(g, B, C, pred, region, roll, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    const int pl = w3_env("KMP_W3_PL", 2) == 1 ? 1 : 2;
+    if (!wave3d_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
-    launch_wave3d<T, false>(roll, pl, grid, block, stream, a);
+    launch_wave3d<T, false>(pl, grid, block, stream, a);
     return check_launch("wave3d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -706,9 +448,8 @@ int try_wave3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w3::W3 a{};
     dim3 grid, block;
-    const bool roll = w3_env("KMP_W3_ROLL", 0) != 0;
-    const int pl = w3_env("KMP_W3_PL", 1) == 2 ? 2 : 1;
-    if (!wave3d_geometry<T>(g, B, C, pred, region, roll, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    const int pl = w3_env("KMP_W3_PL", 2) == 1 ? 1 : 2;
+    if (!wave3d_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -716,7 +457,7 @@ int try_wave3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64
     }
     a.hi_out = hi;
     a.lo_in = lowres;
-    launch_wave3d<T, true>(roll, pl, grid, block, stream, a);
+    launch_wave3d<T, true>(pl, grid, block, stream, a);
     return check_launch("wave3d_decode");
   }
   return KMP_ERR_UNSUPPORTED;
