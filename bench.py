@@ -129,7 +129,7 @@ def kernel_name(ndim, padding):
     # the one-pass kernel the C layer dispatches for this workload (kmp_codec_*.hip)
     if ndim == 3:
         return 'wave3d_plane_kernel' if padding == 0 else 'fast3d_kernel'
-    return 'fast2d_kernel'
+    return 'wave2d_kernel' if padding == 0 else 'fast2d_kernel'
 
 
 def load_traffic(workload, padding, kernel):

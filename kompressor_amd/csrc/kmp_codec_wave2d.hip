@@ -1,0 +1,249 @@
+// kmp_codec_wave2d.hip -- one-pass image encode / decode for the mean predictor with p == 0
+// (BASELINE config C2: MeanPredictor(0) + the uint8 coder on 1024 images of 256^2).
+//
+// The 2D counterpart of kmp_codec_wave3d.hip.  A workgroup owns NW * ROWS consecutive output
+// rows of one image; each of its waves owns ROWS = 64 / TXN of them (TXN = Ex / VX lanes per
+// row, VX outputs per lane = 8 bytes of lowres) and issues all its loads up front: highres rows
+// 2Y and 2Y+1 per lane, plus one halo row on the wave's first row (node row Y0-1, for the cell
+// row above) and on its last row (node row Y+1, mirrored at the even-padded edge,
+// image/utils.py:145-156).  Neighbours come from cross-lane shuffles (node x+VX from the next
+// lane, node row y+1 and the cell row above from the lane TXN away); no LDS, no barrier.
+// Per output (Y, X..X+VX-1): cell means of rows Y-1 and Y (2x2 node sums, floor / 4 == the
+// reference test predictor's f32 mean + truncation, tests/image/test_encode_decode.py:46-51),
+// the 5-way aggregation onto LR / UD / C (image/utils.py:58-86: sums of 1/2 means
+// >> log2(count) == its f32 x0.5 + truncation), and the mod-2^k coder (utils.py:38-55).
+// Image-per-XCD block order keeps the workgroup-edge halo rows in one L2.
+#include <cstdlib>
+
+#include "kmp_wave.h"
+
+namespace kmp {
+namespace w2 {
+
+using namespace wv;
+
+struct W2 {
+  const void* hi_in;
+  void* hi_out;
+  const void* lo_in;
+  void* lo_out;
+  MapPtrs maps;
+  int32_t H, W;
+  int32_t Ly, Lx, Ey, Ex, Lcy, Lcx;
+  int32_t txn, rows, nwv, ngrp;  // lanes per row, rows per wave, waves per workgroup, workgroups per image
+  int32_t xcd_per;               // > 0: image-per-XCD block order (workgroups per image)
+};
+
+template <typename T, bool DEC>
+__global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+
+  const int lane = threadIdx.x & 63;
+  const int wv_ = threadIdx.x >> 6;
+  const int tx = lane % a.txn;
+  const int r = lane / a.txn;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int grp = blk % a.ngrp;
+  const int64_t b = blk / a.ngrp;
+  const int Y0 = (grp * a.nwv + wv_) * a.rows;
+  if (Y0 >= a.Ey) return;  // whole idle wave
+  const int Y = Y0 + r;
+  const bool live = Y < a.Ey;
+  const int Yc = live ? Y : a.Ey - 1;
+  const bool first = r == 0;
+  const bool last = r == a.rows - 1 || Y == a.Ey - 1;
+  const bool vy1 = Y < a.Lcy;  // cell row Y (== highres row 2Y+1) exists
+  const bool vy0 = Y >= 1;
+  const bool need_halo = live && ((first && Y0 >= 1) || (last && vy1));
+  const int yh = first ? (Y0 >= 1 ? Y0 - 1 : 0) : lsrc(Yc + 1, a.Ly, a.Ey);
+  const bool xlast = tx == a.txn - 1;
+
+  const int64_t himg = (int64_t)a.H * a.W;
+  const int hx = 2 * X;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * himg;
+  T* hout = DEC ? (T*)a.hi_out + b * himg : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
+  const int64_t m_lr = (b * a.Lcy + Yc) * a.Ex + X;  // LR and C maps: [B, Lcy, Ex]
+  const int64_t m_ud = (b * a.Ey + Yc) * a.Ex + X;   // UD map and lowres: [B, Ey, Ex]
+
+  // ---- every load up front ----
+  V own{}, halo{};
+  uint4 o0 = make_uint4(0, 0, 0, 0);
+  uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
+  if constexpr (DEC) {
+    if (live) own = ld8c(lin + Yc * a.Ex + X);
+    if (need_halo) halo = ld8c(lin + yh * a.Ex + X);
+    if (live && vy1) mv[0] = ld8((const T*)a.maps.p[0] + m_lr);
+    if (live) mv[1] = ld8((const T*)a.maps.p[1] + m_ud);
+    if (live && vy1) mv[2] = ld8((const T*)a.maps.p[2] + m_lr);
+  } else {
+    if (live) own = ld16c(hin + 2 * Yc * a.W + hx);  // node row: re-read as a neighbour's halo
+    if (need_halo) halo = ld16c(hin + 2 * yh * a.W + hx);
+    if (live && vy1) o0 = ld16(hin + (2 * Yc + 1) * a.W + hx);
+  }
+
+  // ---- 2x2 node sums: row Y, and on the wave's first row also row Y-1 ----
+  uint32_t n[VX], nh[VX];
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    if constexpr (DEC) {
+      n[i] = el8<T>(own, i);
+      nh[i] = el8<T>(halo, i);
+    } else {
+      n[i] = el16<T>(own, 2 * i);
+      nh[i] = el16<T>(halo, 2 * i);
+    }
+  }
+  uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1);
+  if (xlast) {  // node X+VX = Ex: the mirrored node Ex-1 (even pad), or no cell at all (odd)
+    nx1 = n[VX - 1];
+    nhx1 = nh[VX - 1];
+  }
+  uint32_t M1[VX + 1], M0[VX + 1];  // cell rows Y / Y-1, cols X-1 .. X+VX-1
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
+    const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
+    const uint32_t below = shdn(h, a.txn);
+    M1[i + 1] = (h + (last ? hh : below)) >> 2;
+    const uint32_t above = shup(M1[i + 1], a.txn);
+    M0[i + 1] = first ? (hh + h) >> 2 : above;
+  }
+  M1[0] = shup(M1[VX], 1);
+  M0[0] = shup(M0[VX], 1);
+  if (!live) return;
+
+  bool vx[VX + 1];
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) {
+    M1[q] = (vy1 && vx[q]) ? M1[q] : 0u;
+    M0[q] = (vy0 && vx[q]) ? M0[q] : 0u;
+  }
+  const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+  uint32_t pred[3][VX];  // LR, UD, C
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+    pred[0][i] = (M1[i] + M1[i + 1]) >> (nx >> 1);      // LR: cells (Y, x-1), (Y, x)
+    pred[1][i] = (M0[i + 1] + M1[i + 1]) >> (ny >> 1);  // UD: cells (Y-1, x), (Y, x)
+    pred[2][i] = M1[i + 1];                             // C
+  }
+  if constexpr (!DEC) {
+    uint32_t lov[VX], res[3][VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      lov[i] = el16<T>(own, 2 * i);
+      res[0][i] = (el16<T>(o0, 2 * i) - pred[0][i]) & MASK;       // LR (1,0)
+      res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;  // UD (0,1)
+      res[2][i] = (el16<T>(o0, 2 * i + 1) - pred[2][i]) & MASK;   // C  (1,1)
+    }
+    st8((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
+    if (vy1) st8((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
+    st8((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
+    if (vy1) st8((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+  } else {
+    uint32_t dv[3][VX];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(mv[k], i)) & MASK;
+    T* h0 = hout + 2 * Yc * a.W + hx;
+    st16(h0, pack16<T, VX>(n, dv[1]));                    // row 2Y: lowres | UD
+    if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[0], dv[2]));  // row 2Y+1: LR | C
+  }
+}
+
+}  // namespace w2
+
+static int w2_env(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+template <typename T>
+static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
+                            w2::W2& a, dim3& grid, dim3& block) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
+  if (w2_env("KMP_DISABLE_WAVE", 0) || w2_env("KMP_DISABLE_FAST", 0)) return false;
+  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0 || region) return false;
+  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;  // 32-bit offsets inside an image
+  const int64_t txn = g.E[2] / VX;
+  if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
+  const int64_t rows = 64 / txn;
+  if (g.E[1] % rows == 1) return false;  // a one-row wave would need both halo rows
+  const int64_t waves = ceil_div(g.E[1], rows);
+  const int64_t nwv = waves < 4 ? waves : 4;
+  const int64_t ngrp = ceil_div(waves, nwv);
+  a.H = (int)g.n[1]; a.W = (int)g.n[2];
+  a.Ly = (int)g.L[1]; a.Lx = (int)g.L[2];
+  a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
+  a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
+  a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)nwv; a.ngrp = (int)ngrp;
+  a.xcd_per = (w2_env("KMP_W2_XCD", 1) && B % 8 == 0) ? (int)ngrp : 0;
+  const int64_t nblk = B * ngrp;
+  grid = dim3((unsigned)nblk);
+  block = dim3((unsigned)(64 * nwv));
+  return nblk < ((int64_t)1 << 31);
+}
+
+template <typename T>
+int try_wave2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                      const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    w2::W2 a{};
+    dim3 grid, block;
+    if (!wave2d_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 3; ++k)
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+    a.hi_in = hi;
+    a.lo_out = lowres;
+    a.maps = maps;
+    w2::wave2d_kernel<T, false><<<grid, block, 0, stream>>>(a);
+    return check_launch("wave2d_encode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int try_wave2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                      const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    w2::W2 a{};
+    dim3 grid, block;
+    if (!wave2d_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 3; ++k) {
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      a.maps.p[k] = (void*)maps.p[k];
+    }
+    a.hi_out = hi;
+    a.lo_in = lowres;
+    w2::wave2d_kernel<T, true><<<grid, block, 0, stream>>>(a);
+    return check_launch("wave2d_decode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+#define KMP_W2_INST(T)                                                                                    \
+  template int try_wave2d_encode<T>(const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,     \
+                                    const MapPtrs&, const kmp_region*, hipStream_t);                      \
+  template int try_wave2d_decode<T>(const T*, const CMapPtrs&, const Geo&, int64_t, int64_t,              \
+                                    const kmp_predictor*, T*, const kmp_region*, hipStream_t);
+KMP_W2_INST(uint8_t)
+KMP_W2_INST(uint16_t)
+KMP_W2_INST(int32_t)
+KMP_W2_INST(uint32_t)
+
+}  // namespace kmp

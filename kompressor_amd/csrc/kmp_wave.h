@@ -1,0 +1,83 @@
+// kmp_wave.h -- register-level helpers shared by the barrier-free wave kernels
+// (kmp_codec_wave3d.hip, kmp_codec_wave2d.hip): streaming vector loads / stores, element
+// (un)packing of 8- and 16-byte row segments, the padded-node index map, and cross-lane shuffles.
+#pragma once
+
+#include "kmp_codec.h"
+
+namespace kmp {
+namespace wv {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld8(const void* p) {
+  const u32x2 v = __builtin_nontemporal_load((const u32x2*)p);
+  return make_uint2(v.x, v.y);
+}
+// default-policy loads: for bytes another workgroup re-reads soon (z-halo node rows), which must
+// stay in L2 rather than stream past it
+__device__ __forceinline__ uint4 ld16c(const void* p) { return *(const uint4*)p; }
+__device__ __forceinline__ uint2 ld8c(const void* p) { return *(const uint2*)p; }
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, (u32x4*)p);
+}
+__device__ __forceinline__ void st8(void* p, uint2 v) {
+  u32x2 w = {v.x, v.y};
+  __builtin_nontemporal_store(w, (u32x2*)p);
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t el16(const uint4& v, int e) {  // element e of 16 bytes
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t el8(const uint2& v, int e) {  // element e of 8 bytes
+  const uint32_t w[2] = {v.x, v.y};
+  if constexpr (sizeof(T) == 2) return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+  else return (w[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint2 pack8(const uint32_t (&v)[VX]) {
+  if constexpr (sizeof(T) == 2) {
+    return make_uint2((v[0] & 0xffffu) | (v[1] << 16), (v[2] & 0xffffu) | (v[3] << 16));
+  } else {
+    return make_uint2((v[0] & 0xffu) | ((v[1] & 0xffu) << 8) | ((v[2] & 0xffu) << 16) | (v[3] << 24),
+                      (v[4] & 0xffu) | ((v[5] & 0xffu) << 8) | ((v[6] & 0xffu) << 16) | (v[7] << 24));
+  }
+}
+template <typename T, int VX>
+__device__ __forceinline__ uint4 pack16(const uint32_t (&ev)[VX], const uint32_t (&od)[VX]) {  // interleave
+  if constexpr (sizeof(T) == 2) {
+    return make_uint4((ev[0] & 0xffffu) | (od[0] << 16), (ev[1] & 0xffffu) | (od[1] << 16),
+                      (ev[2] & 0xffffu) | (od[2] << 16), (ev[3] & 0xffffu) | (od[3] << 16));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = (ev[2 * q] & 0xffu) | ((od[2 * q] & 0xffu) << 8) | ((ev[2 * q + 1] & 0xffu) << 16) | (od[2 * q + 1] << 24);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+__device__ __forceinline__ int lsrc(int r, int L, int E) {
+  // stored node index of padded node r along an axis (even reflect pad: node E -> E - 1)
+  int m = r % (2 * L);
+  if (m < 0) m += 2 * L;
+  m = m < L ? m : 2 * L - 1 - m;
+  int m2 = m % (2 * E);
+  return m2 < E ? m2 : 2 * E - 1 - m2;
+}
+
+__device__ __forceinline__ uint32_t shdn(uint32_t v, int d) { return (uint32_t)__shfl_down((int)v, d, 64); }
+__device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
+
+}  // namespace wv
+}  // namespace kmp
