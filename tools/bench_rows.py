@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Throughput of every SURVEY.md §8(a) row on the GPU, against the HBM roofline, with the CPU
+oracle timed beside it on a small sample of the same workload.
+
+    python tools/bench_rows.py [--reps N] [--rows name,name,...] [--no-cpu]
+
+One JSON line per row: {"row", "what", "GBps", "frac", "us", "algo_bytes", "cpu_GBps", "cpu_sample"}.
+``GBps`` = algorithmic bytes per call (inputs read + outputs written once) over the
+HIP-event time of ``reps`` back-to-back calls on device-resident inputs.  bench.py remains the
+headline (C3); this covers the secondary rows (p = 1, 2, LinearPredictor, chunked drivers, the
+reference-style callback path, categorical coder, primitives, tiling).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+PEAK = 8000.0
+
+
+def gpu_time(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps / 1e3
+
+
+def cpu_time(fn, budget=3.0):
+    t = time.perf_counter()
+    fn()
+    first = time.perf_counter() - t
+    n = max(1, min(5, int(budget / max(first, 1e-3))))
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    return (time.perf_counter() - t) / n
+
+
+def rand(shape, dtype, seed=0):
+    info = np.iinfo(dtype)
+    return np.random.default_rng(seed).integers(0, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--rows', default='')
+    ap.add_argument('--no-cpu', action='store_true')
+    args = ap.parse_args()
+    want = set(filter(None, args.rows.split(',')))
+
+    import kompressor_amd as kom
+    from kompressor_amd import _nd
+    import oracle
+    from oracle import predictors as OP
+    torch.cuda.set_device(0)
+
+    vol_h = rand((512, 64, 64, 64, 1), np.uint16)
+    vol = torch.from_numpy(vol_h).cuda()
+    img_h = rand((1024, 256, 256, 1), np.uint8)
+    img = torch.from_numpy(img_h).cuda()
+    V, I = kom.volume, kom.image
+    OV, OI = oracle.volume, oracle.image
+    raw_v, raw_i = vol.numel() * 2, img.numel()
+
+    def emit(row, what, algo, t, cpu=None):
+        line = {'row': row, 'what': what, 'GBps': round(algo / t / 1e9, 1), 'frac': round(algo / t / 1e9 / PEAK, 4),
+                'us': round(t * 1e6, 2), 'algo_bytes': int(algo)}
+        if cpu:
+            line['cpu_GBps'] = round(cpu[0], 5)
+            line['cpu_sample'] = cpu[1]
+        print(json.dumps(line), flush=True)
+
+    def cpu_codec(ons, pf, enc, dec, sample, padding):
+        if args.no_cpu:
+            return None
+
+        def rnd():
+            lo, e = ons.encode(pf, enc, sample, padding=padding)
+            ons.decode(pf, dec, lo, e, padding=padding)
+        t = cpu_time(rnd)
+        return sample.nbytes * 2 * 2 / t / 1e9, f'{sample.shape[0]} tiles, oracle encode+decode, 1 thread'
+
+    def codec_rows(tag, ns, ons, x, xh, pred, opf, enc, dec, oenc, odec, padding, raw, ndim):
+        if want and tag not in want:
+            return
+        coder = _nd.NATURAL_CODER[x.dtype]
+        lo, maps, dims = _nd._alloc_encoded(x, coder, ndim)
+        rec = torch.empty_like(x)
+        ws = torch.empty(max(1, _nd.workspace_bytes(x, pred, ndim)), dtype=torch.uint8, device='cuda')
+        fe = lambda: _nd.fused_encode_into(x, pred, coder, lo, maps, ndim, workspace=ws)  # noqa: E731
+        fd = lambda: _nd.fused_decode_into(lo, maps, dims, pred, coder, rec, ndim, workspace=ws)  # noqa: E731
+        fe(), fd()
+        torch.cuda.synchronize()
+        assert torch.equal(rec, x), tag
+        te, td = gpu_time(fe, args.reps), gpu_time(fd, args.reps)
+        cpu = cpu_codec(ons, opf, oenc, odec, xh[:2], padding)
+        emit(tag + ':encode', f'fused encode {pred!r}', 2 * raw, te, cpu)
+        emit(tag + ':decode', f'fused decode {pred!r}', 2 * raw, td)
+
+    for p in (0, 1, 2):
+        codec_rows(f'volume_mean_p{p}', V, OV, vol, vol_h, kom.MeanPredictor(p, 3), OP.mean_predictions_fn(p, 3),
+                   V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16, OV.decode_values_uint16,
+                   p, raw_v, 3)
+    for p in (0, 1):
+        codec_rows(f'image_mean_p{p}', I, OI, img, img_h, kom.MeanPredictor(p, 2), OP.mean_predictions_fn(p, 2),
+                   I.encode_values_uint8, I.decode_values_uint8, OI.encode_values_uint8, OI.decode_values_uint8,
+                   p, raw_i, 2)
+    rng = np.random.default_rng(1)
+    for p in (0, 1):
+        n = (2 * p + 2) ** 3
+        w = (1.0 / n + rng.standard_normal((n, 19)) * (0.3 / n)).astype(np.float32)
+        b = np.zeros(19, np.float32)
+        codec_rows(f'volume_linear_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3),
+                   OP.linear_predictions_fn(p, w, b, 3), V.encode_values_uint16, V.decode_values_uint16,
+                   OV.encode_values_uint16, OV.decode_values_uint16, p, raw_v, 3)
+
+    # chunked drivers (encode_decode_chunk.py:33-117) at C3, chunk 32 (the reference default)
+    if not want or 'volume_chunks' in want:
+        pred = kom.MeanPredictor(0, 3)
+        lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, vol)
+        te = gpu_time(lambda: V.encode_chunks(pred, V.encode_values_uint16, vol, chunk=32), 3)
+        td = gpu_time(lambda: V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=32), 3)
+        emit('volume_chunks:encode', 'encode_chunks chunk=32, fused region launches', 2 * raw_v, te)
+        emit('volume_chunks:decode', 'decode_chunks chunk=32, fused region launches', 2 * raw_v, td)
+
+    # the reference-style callback path: a plain predictions_fn + coder, primitive kernels only
+    if not want or 'volume_callback' in want:
+        pred = kom.MeanPredictor(0, 3)
+        cb = lambda lowres: pred(lowres)  # noqa: E731  (not recognised as fused: the reference's step sequence)
+        sub = vol[:128]
+        lo, (maps, dims) = V.encode(cb, V.encode_values_uint16, sub)
+        te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), 3)
+        td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), 3)
+        emit('volume_callback:encode', 'callback encode (pad, gathers, predictor, 7 coders, trims)', sub.numel() * 4, te)
+        emit('volume_callback:decode', 'callback decode (pads, predictor, 7 coders, scatter, trim)', sub.numel() * 4, td)
+
+    # categorical rank coder (utils.py:58-111): 1M elements x 256 float32 logits
+    if not want or 'categorical' in want:
+        n, L = 1 << 20, 256
+        logits = torch.rand((n, L), device='cuda')
+        gt = torch.from_numpy(rand((n,), np.uint8)).cuda()
+        enc = kom.volume.encode_categorical(logits, gt)
+        te = gpu_time(lambda: kom.volume.encode_categorical(logits, gt), args.reps)
+        td = gpu_time(lambda: kom.volume.decode_categorical(logits, enc), args.reps)
+        cpu = None
+        if not args.no_cpu:
+            lh, gh = logits[:4096].cpu().numpy(), gt[:4096].cpu().numpy()
+            t = cpu_time(lambda: oracle.common.encode_categorical(lh, gh))
+            cpu = (4096 * (L * 4 + 2) / t / 1e9, '4096 elements, oracle stable argsort, 1 thread')
+        emit('categorical:encode', 'rank coder encode, L=256', n * (L * 4 + 2), te, cpu)
+        emit('categorical:decode', 'rank coder decode, L=256', n * (L * 4 + 2), td)
+
+    # geometry primitives (volume/utils.py) on the C3 tile batch
+    if not want or 'primitives' in want:
+        hp, _ = _nd.d_pad_highres(vol, 3)                       # [512, 65^3]
+        lowres = _nd.d_lowres_from_highres(hp, 3)
+        gt_maps = _nd.d_maps_from_highres(hp, 3)
+        n_hp = hp.numel() * 2
+        emit('pad_highres', 'reflect pad 64^3 -> 65^3', raw_v + n_hp, gpu_time(lambda: _nd.d_pad_highres(vol, 3), args.reps))
+        emit('lowres_from_highres', 'x[:, ::2, ::2, ::2]', lowres.numel() * 4,
+             gpu_time(lambda: _nd.d_lowres_from_highres(hp, 3), args.reps))
+        emit('maps_from_highres', '7 parity-class gathers', n_hp - lowres.numel() * 2 + sum(m.numel() * 2 for m in gt_maps),
+             gpu_time(lambda: _nd.d_maps_from_highres(hp, 3), args.reps))
+        emit('highres_from_lowres_and_maps', '8-way interleave', 2 * n_hp,
+             gpu_time(lambda: _nd.d_highres_from_lowres_and_maps(lowres, gt_maps, 3), args.reps))
+        feats = _nd.d_features_from_lowres(lowres, 0, 3)
+        emit('features_from_lowres', 'p=0: 8 shifted windows', lowres.numel() * 2 + feats.numel() * 2,
+             gpu_time(lambda: _nd.d_features_from_lowres(lowres, 0, 3), args.reps))
+        preds = feats[..., :1, :].expand(*feats.shape[:4], 19, 1).contiguous()
+        mp = _nd.d_maps_from_predictions(preds, 3)
+        emit('maps_from_predictions', 'f32 19-way aggregation', preds.numel() * 2 + sum(m.numel() * 2 for m in mp),
+             gpu_time(lambda: _nd.d_maps_from_predictions(preds, 3), args.reps))
+        volume = vol.view(8, 8, 8, 64, 64, 64).permute(0, 3, 1, 4, 2, 5).reshape(512, 512, 512, 1)
+        emit('tiles:split', '512^3 volume -> 512 x 64^3', 2 * raw_v,
+             gpu_time(lambda: kom.tiles.volume_to_tiles(volume, 64), args.reps))
+        emit('tiles:assemble', '512 x 64^3 -> 512^3 volume', 2 * raw_v,
+             gpu_time(lambda: kom.tiles.tiles_to_volume(vol, (512, 512, 512)), args.reps))
+        a, b2 = vol.view(-1), torch.empty_like(vol).view(-1)
+        emit('code_u16', 'mod-2^16 coder, flat', 3 * raw_v,
+             gpu_time(lambda: _nd.d_code(0, kom._lib.CODER_U16, a, b2), args.reps))
+
+
+if __name__ == '__main__':
+    main()
