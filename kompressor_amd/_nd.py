@@ -502,13 +502,56 @@ def _chunk_list(L, chunk, nsp, progress_fn):
     return chunks
 
 
-def d_process_chunks(predictions_fn, code_fn, lowres, reference_maps, chunk, padding, progress_fn, nsp):
-    validate_padding(padding)
-    validate_chunk(chunk, nsp)
-    L = validate_lowres_shape(lowres.shape, nsp)
+def fused_chunk_regions(chunk_list, E, nsp):
+    """Output-frame regions for the fused chunked drivers.
+
+    The reference codes one chunk window at a time (encode_decode_chunk.py:98-115) and its tests
+    pin that the result equals the whole-array call (tests/volume/test_encode_decode.py:509-539).
+    The fused kernels never materialise windows, so the chunks of one slab along the leading
+    spatial axis (consecutive in the reference's z-major order) are merged into ONE launch
+    whenever together they cover that slab's whole cross-section -- the normal case; a chunk that
+    is not part of such a covered slab keeps its own launch.  ``covered`` is False when the chunks
+    leave part of the output unreached (a progress_fn that filters chunks): the callers then run
+    the reference's step sequence instead, whose unreached map entries stay zero (``zeros_like``,
+    :91).  Returns ``(regions, covered)``."""
+    boxes = [[(i0, min(i1, e)) for ((i0, i1), _), e in zip(ranges, E)] for ranges in chunk_list]
+    regions, full = [], np.zeros(tuple(E), dtype=bool)
+    done = np.zeros(E[0], dtype=bool)  # leading-axis planes written by a full-slab launch
+    k = 0
+    while k < len(boxes):
+        lead = boxes[k][0]
+        j = k
+        cross = np.zeros(tuple(E[1:]), dtype=bool)
+        while j < len(boxes) and boxes[j][0] == lead:
+            cross[tuple(slice(a, b) for a, b in boxes[j][1:])] = True
+            j += 1
+        if cross.all():
+            # overlapping windows (yield_chunks steps by chunk - 3) rewrite planes an earlier slab
+            # already wrote with identical values: launch only the planes not yet written
+            a = lead[0]
+            while a < lead[1]:
+                if done[a]:
+                    a += 1
+                    continue
+                b = a
+                while b < lead[1] and not done[b]:
+                    b += 1
+                regions.append([(a, b)] + [(0, e) for e in E[1:]])
+                done[a:b] = True
+                a = b
+        else:
+            regions.extend(boxes[k:j])
+        k = j
+    for r in regions:
+        full[tuple(slice(a, b) for a, b in r)] = True
+    return regions, bool(full.all())
+
+
+def d_process_chunks(predictions_fn, code_fn, lowres, reference_maps, chunk_list, padding, nsp):
+    """encode_decode_chunk.py:77-117 over an already enumerated (and progress_fn-filtered) chunk list."""
     padded = d_pad_neighborhood(lowres, padding, nsp)
     coded = [_zeros(r.shape, r.dtype) for r in reference_maps]
-    for ranges in _chunk_list(L, chunk, nsp, progress_fn):
+    for ranges in chunk_list:
         starts = [i0 - p0 for (i0, _), (p0, _) in ranges]
         ext = [(i1 + p1 + 2 * padding) - (i0 - p0) for (i0, i1), (p0, p1) in ranges]
         window = d_crop(padded, starts, ext, nsp)
@@ -522,6 +565,14 @@ def d_process_chunks(predictions_fn, code_fn, lowres, reference_maps, chunk, pad
     return coded
 
 
+def _chunks_for(L, chunk, padding, progress_fn, nsp):
+    # process_chunks' checks (encode_decode_chunk.py:77-96), then the one progress_fn call
+    validate_padding(padding)
+    validate_chunk(chunk, nsp)
+    _require(all(l >= 2 for l in L), f'lowres spatial dims must be >= 2, got {tuple(L)}')
+    return list(_chunk_list(L, chunk, nsp, progress_fn))
+
+
 def encode_chunks(predictions_fn, encode_fn, highres, chunk, padding, progress_fn, nsp):
     dims = highres_dims(highres.shape, nsp)
     padded_shape = (highres.shape[0], *[s + d for s, d in zip(_sp(highres.shape, nsp), dims)],
@@ -529,24 +580,23 @@ def encode_chunks(predictions_fn, encode_fn, highres, chunk, padding, progress_f
     validate_highres_shape(padded_shape, nsp)
     validate_padding(padding)
     h, kind = dev.to_device(highres)
+    L = [(s + 1) // 2 for s in _sp(padded_shape, nsp)]
+    chunk_list = _chunks_for(L, chunk, padding, progress_fn, nsp)
     plan = fused_plan(predictions_fn, encode_fn, padding, h.dtype, nsp, _lib.ENCODE)
     if plan is not None:
         predictor, coder = plan
         lowres, maps, dims = _alloc_encoded(h, coder, nsp)
-        L = [e + d for e, d in zip(_sp(lowres.shape, nsp), dims)]
-        E = _sp(lowres.shape, nsp)
-        ws = None
-        for ranges in _chunk_list(L, chunk, nsp, progress_fn):
-            region = [(i0, min(i1, e)) for ((i0, i1), _), e in zip(ranges, E)]
-            fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=region, workspace=ws)
-        encoded = tuple(maps)
-    else:
-        hp, dims = d_pad_highres(h, nsp)
-        lowres = d_lowres_from_highres(hp, nsp)
-        gt_maps = d_maps_from_highres(hp, nsp)
-        coded = d_process_chunks(predictions_fn, encode_fn, lowres, gt_maps, chunk, padding, progress_fn, nsp)
-        encoded = d_trim_maps(coded, dims, nsp)
-        lowres = d_trim(lowres, dims, nsp)
+        regions, covered = fused_chunk_regions(chunk_list, _sp(lowres.shape, nsp), nsp)
+        if covered:
+            for region in regions:
+                fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=region)
+            return dev.from_device(lowres, kind), (tuple(dev.from_device(m, kind) for m in maps), tuple(dims))
+    hp, dims = d_pad_highres(h, nsp)
+    lowres = d_lowres_from_highres(hp, nsp)
+    gt_maps = d_maps_from_highres(hp, nsp)
+    coded = d_process_chunks(predictions_fn, encode_fn, lowres, gt_maps, chunk_list, padding, nsp)
+    encoded = d_trim_maps(coded, dims, nsp)
+    lowres = d_trim(lowres, dims, nsp)
     return dev.from_device(lowres, kind), (tuple(dev.from_device(m, kind) for m in encoded), tuple(dims))
 
 
@@ -557,20 +607,23 @@ def decode_chunks(predictions_fn, decode_fn, lowres, encoded, chunk, padding, pr
     validate_lowres_shape(lowres.shape, nsp)
     lo, kind = dev.to_device(lowres)
     maps = [_dev(m) for m in encoded_maps]
+    E = _sp(lo.shape, nsp)
+    L = [e + d for e, d in zip(E, dims)]
+    chunk_list = _chunks_for(L, chunk, padding, progress_fn, nsp)
     plan = fused_plan(predictions_fn, decode_fn, padding, lo.dtype, nsp, _lib.DECODE)
     if plan is not None and all(m.dtype == CODER_DTYPE[plan[1]] for m in maps):
         predictor, coder = plan
         _check_encoded_maps(lo, maps, dims, nsp)
-        E = _sp(lo.shape, nsp)
-        L = [e + d for e, d in zip(E, dims)]
-        out = dev.empty((lo.shape[0], *[2 * e - 1 + d for e, d in zip(E, dims)], *_ch(lo.shape, nsp)), lo.dtype)
-        for ranges in _chunk_list(L, chunk, nsp, progress_fn):
-            region = [(i0, min(i1, e)) for ((i0, i1), _), e in zip(ranges, E)]
-            fused_decode_into(lo, maps, dims, predictor, coder, out, nsp, region=region)
-        return dev.from_device(out, kind)
+        regions, covered = fused_chunk_regions(chunk_list, E, nsp)
+        if covered:
+            out = dev.empty((lo.shape[0], *[2 * e - 1 + d for e, d in zip(E, dims)], *_ch(lo.shape, nsp)),
+                            lo.dtype)
+            for region in regions:
+                fused_decode_into(lo, maps, dims, predictor, coder, out, nsp, region=region)
+            return dev.from_device(out, kind)
     lo_p = d_pad_lowres(lo, dims, nsp)
     maps_p = d_pad_maps(maps, dims, nsp)
-    decoded = d_process_chunks(predictions_fn, decode_fn, lo_p, maps_p, chunk, padding, progress_fn, nsp)
+    decoded = d_process_chunks(predictions_fn, decode_fn, lo_p, maps_p, chunk_list, padding, nsp)
     hi = d_highres_from_lowres_and_maps(lo_p, decoded, nsp)
     return dev.from_device(d_trim(hi, dims, nsp), kind)
 

@@ -32,6 +32,7 @@ struct W2 {
   int32_t Ly, Lx, Ey, Ex, Lcy, Lcx;
   int32_t txn, rows, nwv, ngrp;  // lanes per row, rows per wave, waves per workgroup, workgroups per image
   int32_t xcd_per;               // > 0: image-per-XCD block order (workgroups per image)
+  int32_t ybeg, yend;            // output rows written (a chunked-driver region; all rows otherwise)
 };
 
 template <typename T, bool DEC>
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   }
   M1[0] = shup(M1[VX], 1);
   M0[0] = shup(M0[VX], 1);
-  if (!live) return;
+  if (!live || Y < a.ybeg || Y >= a.yend) return;
 
   bool vx[VX + 1];
 #pragma unroll
@@ -175,7 +176,14 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
   if (w2_env("KMP_DISABLE_WAVE", 0) || w2_env("KMP_DISABLE_FAST", 0)) return false;
-  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0 || region) return false;
+  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0) return false;
+  int64_t yb = 0, ye = g.E[1];
+  if (region) {  // only row ranges (full width): the fused chunked drivers' merged slabs
+    if (region->begin[2] > 0 || region->end[2] < g.E[2]) return false;
+    yb = region->begin[1] < 0 ? 0 : region->begin[1];
+    ye = region->end[1] > g.E[1] ? g.E[1] : region->end[1];
+    if (ye <= yb) return false;
+  }
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;  // 32-bit offsets inside an image
   const int64_t txn = g.E[2] / VX;
@@ -191,6 +199,8 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)nwv; a.ngrp = (int)ngrp;
   a.xcd_per = (w2_env("KMP_W2_XCD", 1) && B % 8 == 0) ? (int)ngrp : 0;
+  a.ybeg = (int)yb;
+  a.yend = (int)ye;
   const int64_t nblk = B * ngrp;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));

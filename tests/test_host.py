@@ -139,3 +139,28 @@ def test_encoded_shapes_match_oracle():
         o_maps = oracle.volume.trim_maps(oracle.volume.maps_from_highres(o_hi), o_dims)
         assert dims == o_dims and lo[1:] == o_lo.shape[1:]
         assert [m[1:] for m in maps] == [m.shape[1:] for m in o_maps]
+
+
+def test_fused_chunk_regions_merge_and_cover():
+    from kompressor_amd._nd import fused_chunk_regions, yield_chunks
+    from itertools import product
+    E = (32, 32, 32)
+    L = (33, 33, 33)
+    chunks = list(product(*[yield_chunks(l, 32) for l in L]))
+    regions, covered = fused_chunk_regions(chunks, E, 3)
+    assert covered
+    # one launch per distinct slab, overlapping planes launched once
+    assert [r[0] for r in regions] == [(0, 30), (30, 32)]
+    assert all(r[1:] == [(0, 32), (0, 32)] for r in regions)
+    # odd extents, small chunks, 2D
+    for E2, L2, c in [((8, 9), (9, 9), 6), ((17, 16), (17, 17), 11), ((5, 5), (5, 5), 4)]:
+        ch = list(product(*[yield_chunks(l, c) for l in L2]))
+        regs, cov = fused_chunk_regions(ch, E2, 2)
+        assert cov
+        lead = np.zeros(E2[0], int)
+        for r in regs:
+            lead[r[0][0]:r[0][1]] += 1
+        assert (lead == 1).all()
+    # a filtered chunk list leaves outputs unreached -> not covered
+    regs, cov = fused_chunk_regions(chunks[:-1], E, 3)
+    assert not cov
