@@ -486,8 +486,10 @@ template <typename T>
 int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                     const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
   if (nsp != 3) return try_fast2d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
-  {  // p == 0: the barrier-free wave kernel (kmp_codec_wave3d.hip)
-    const int st = try_wave3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
+  {  // p == 0: the barrier-free wave kernel (kmp_codec_wave3d.hip) / fused linear (kmp_codec_linear3d.hip)
+    int st = try_wave3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
@@ -512,7 +514,9 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
                     const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
   if (nsp != 3) return try_fast2d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
   {
-    const int st = try_wave3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    int st = try_wave3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {

@@ -1,0 +1,490 @@
+// kmp_codec_linear3d.hip -- one-pass volume encode / decode for the LinearPredictor with p == 0
+// (SURVEY.md §8a row a9': the north star's "learned-predictor apply").
+//
+// pred[cell, k] = fma-chain over n = 0..7 of feat[cell, n] * W[n, k], started from b[k]
+// (kmp_linear.hip, oracle.predictors.linear_fma_chain), cast to the sample dtype
+// (XLA truncating / saturating astype), then maps_from_predictions (volume/utils.py:83-155) and
+// the mod-2^k coder (utils.py:38-55).  Features are the 2x2x2 lowres nodes of the cell in the
+// reference's order (n = dz*4 + dy*2 + dx, features_from_lowres volume/utils.py:199-210).
+//
+// Data movement is the plane-block scheme of kmp_codec_wave3d.hip with PL = 1: a workgroup owns
+// one output plane c of one tile, its waves own 8 rows each, all loads are issued up front, and
+// x / y+1 neighbours come from cross-lane shuffles.  A lane evaluates only the channels the
+// outputs actually read: 14 of cell plane c (ch 0-4, 6-12, 15, 16) and 5 of plane c-1 (ch 5,
+// 13, 14, 17, 18) for its 4 cells -- 19 channel-cells per output, no recomputation.  The
+// channels row Y+1 needs from row Y (3, 9, 10, 16, 17) go down by shuffle inside a wave and
+// through LDS across waves (one barrier).
+//
+// The 8x19 matvec runs on packed f32 VALU FMAs (v_pk_fma_f32, two cells per instruction): on
+// CDNA4 the f32 MFMA rate equals the packed-VALU f32 rate, and keeping the cells in the lanes
+// that own them avoids the cell <-> MFMA-fragment transposes.  Every FMA is correctly rounded
+// and in the same n order, so the f32 values are bit-identical to kmp_linear.hip's MFMA chain.
+#include <cstdlib>
+
+#include "kmp_wave.h"
+
+namespace kmp {
+namespace l3 {
+
+using namespace wv;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct L3 {
+  const void* hi_in;
+  void* hi_out;
+  const void* lo_in;
+  void* lo_out;
+  MapPtrs maps;
+  const float* W;  // [8, 19] row-major
+  const float* b;  // [19]
+  int32_t D, H, W_;
+  int32_t Lz, Ly, Lx, Ez, Ey, Ex, Lcz, Lcy, Lcx;
+  int32_t zbegin, zend;
+  int32_t txn, rows, nwv;
+  int32_t xcd_per;
+};
+
+template <typename T>
+__device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: trunc, saturate, NaN -> 0
+  constexpr float hi = sizeof(T) == 2 ? 65535.0f : 255.0f;
+  return (uint32_t)fminf(fmaxf(v, 0.0f), hi);
+}
+
+// channel k of the linear predictor for 4 cells (features f[n][cell]), cast to T.  ``Wt`` is the
+// LDS copy of the weights, channel-major [19][8] followed by the bias [19]: uniform ds_reads
+// (broadcast), so the 171 constants never compete for scalar registers.
+template <typename T, int K>
+__device__ __forceinline__ void channel(const float (&f)[8][4], const float* Wt, uint32_t (&out)[4]) {
+  const float4 wa = *(const float4*)(Wt + K * 8), wb = *(const float4*)(Wt + K * 8 + 4);
+  const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+  const float bk = Wt[19 * 8 + K];
+  f32x2 a0 = {bk, bk}, a1 = {bk, bk};
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const f32x2 wv2 = {w[n], w[n]};
+    a0 = __builtin_elementwise_fma((f32x2){f[n][0], f[n][1]}, wv2, a0);
+    a1 = __builtin_elementwise_fma((f32x2){f[n][2], f[n][3]}, wv2, a1);
+  }
+  out[0] = cast_t<T>(a0.x);
+  out[1] = cast_t<T>(a0.y);
+  out[2] = cast_t<T>(a1.x);
+  out[3] = cast_t<T>(a1.y);
+
+
+}
+
+constexpr int kXch = 5;  // channels exchanged downwards: 3, 9, 10, 16 (plane c), 17 (plane c-1)
+constexpr int kWtWords = 172;  // 19 * 8 weights + 19 biases, rounded up to 16 B
+
+template <typename T, bool DEC>
+__global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  static_assert(VX == 4 || VX == 8, "u16 / u8");
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+  // LDS: weights (channel-major [19][8] + bias [19]), then the exchange rows [wave][kXch][Ex]
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  float* Wt = (float*)smem;
+  uint32_t* xrow = smem + kWtWords;
+  for (int t = threadIdx.x; t < 19 * 9; t += blockDim.x) {
+    if (t < 152) Wt[(t % 19) * 8 + t / 19] = a.W[t];  // W[n][k] -> Wt[k][n]
+    else Wt[152 + (t - 152)] = a.b[t - 152];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wv_ = threadIdx.x >> 6;
+  const int tx = lane % a.txn;
+  const int r = lane / a.txn;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int nplanes = a.zend - a.zbegin;
+  const int c = a.zbegin + blk % nplanes;
+  const int64_t b = blk / nplanes;
+  const int Y0 = wv_ * a.rows;
+  const bool wave_live = Y0 < a.Ey;
+  const int Y = Y0 + r;
+  const bool live = wave_live && Y < a.Ey;
+  const int Yc = live ? Y : a.Ey - 1;
+  const bool first = r == 0;
+  const bool last = r == a.rows - 1 || Y == a.Ey - 1;
+  const bool vy1 = Y < a.Lcy;
+  const bool vy0 = Y >= 1;
+  const bool need_dn = live && last && vy1;
+  const int ydn = lsrc(Yc + 1, a.Ly, a.Ey);
+  const bool xlast = tx == a.txn - 1;
+  const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+
+  const int hplane = a.H * a.W_;
+  const int lplane = a.Ey * a.Ex;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
+  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
+  const int hx = 2 * X;
+  const int ho_own = 2 * Yc * a.W_ + hx, ho_dn = 2 * ydn * a.W_ + hx;
+  const int lo_own = Yc * a.Ex + X, lo_dn = ydn * a.Ex + X;
+
+  const T* mbase[7];
+  int mplane[7];
+  bool mok_y[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    int par[3];
+    map_parity(3, k, par);
+    const int ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
+    mplane[k] = ey * a.Ex;
+    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + Yc * a.Ex + X;
+    mok_y[k] = live && (!par[1] || vy1);
+  }
+
+  // ---- all loads up front: node planes c-1, c, c+1 (own row + the last row's halo row) ----
+  V own[3] = {}, dn[3] = {};
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int q = c - 1 + t;
+    if (q < 0) continue;
+    const int sz = lsrc(q, a.Lz, a.Ez);
+    if constexpr (DEC) {
+      const T* p = lin + sz * lplane;
+      if (live) own[t] = ld8c(p + lo_own);
+      if (need_dn) dn[t] = ld8c(p + lo_dn);
+    } else {
+      const T* p = hin + 2 * sz * hplane;
+      if (live) own[t] = ld16c(p + ho_own);
+      if (need_dn) dn[t] = ld16c(p + ho_dn);
+    }
+  }
+  uint4 e1 = make_uint4(0, 0, 0, 0), o0 = e1, o1 = e1;
+  uint2 mv[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
+  if constexpr (DEC) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int par[3];
+      map_parity(3, k, par);
+      if (mok_y[k] && (!par[0] || vz1)) mv[k] = ld8(mbase[k] + c * mplane[k]);
+    }
+  } else {
+    const T* p = hin + 2 * c * hplane;
+    if (live && vy1) e1 = ld16(p + ho_own + a.W_);
+    if (live && vz1) o0 = ld16(p + hplane + ho_own);
+    if (live && vz1 && vy1) o1 = ld16(p + hplane + ho_own + a.W_);
+  }
+
+  // ---- node values: own row Y, row Y+1 (shuffle / halo), each with node x+VX ----
+  float nY[3][VX + 1], nY1[3][VX + 1];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    uint32_t n[VX], nd[VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      if constexpr (DEC) {
+        n[i] = el8<T>(own[t], i);
+        nd[i] = el8<T>(dn[t], i);
+      } else {
+        n[i] = el16<T>(own[t], 2 * i);
+        nd[i] = el16<T>(dn[t], 2 * i);
+      }
+    }
+    uint32_t nx = shdn(n[0], 1), ndx = shdn(nd[0], 1);
+    if (xlast) {  // node Ex: mirror of node Ex-1 (even pad); no cell there otherwise
+      nx = n[VX - 1];
+      ndx = nd[VX - 1];
+    }
+    const uint32_t bx = shdn(nx, a.txn);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t below = shdn(n[i], a.txn);
+      nY[t][i] = (float)n[i];
+      nY1[t][i] = (float)(last ? nd[i] : below);
+    }
+    nY[t][VX] = (float)nx;
+    nY1[t][VX] = (float)(last ? ndx : bx);
+  }
+
+  // ---- channels: evaluated map group by map group so only a few are live at a time ----
+  // feat(PLANE, ...) gathers the 8 features of cells X+4g .. X+4g+3 of cell plane c-1+PLANE
+  auto feats = [&](int pl, int g, float (&f)[8][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * g + j;
+#pragma unroll
+      for (int dz = 0; dz < 2; ++dz) {
+        f[dz * 4 + 0][j] = nY[pl + dz][i];
+        f[dz * 4 + 1][j] = nY[pl + dz][i + 1];
+        f[dz * 4 + 2][j] = nY1[pl + dz][i];
+        f[dz * 4 + 3][j] = nY1[pl + dz][i + 1];
+      }
+    }
+  };
+  constexpr int G = VX / 4;
+  // CH(out, PLANE, K): channel K of this lane's VX cells of plane c-1+PLANE into out[1..VX]
+#define KMP_CH(OUT, PLANE, K)                                             \
+  _Pragma("unroll") for (int g = 0; g < G; ++g) {                         \
+    float f[8][4];                                                        \
+    uint32_t o[4];                                                        \
+    feats(PLANE, g, f);                                                   \
+    channel<T, K>(f, Wt, o);                                              \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j]; \
+  }
+
+  // 1. the channels row Y+1 reads from row Y: 3, 9, 10, 16 (plane c), 17 (plane c-1)
+  uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
+  {
+    uint32_t P3[VX + 1], P9[VX + 1], P10[VX + 1], P16[VX + 1], Q17[VX + 1];
+    KMP_CH(P3, 1, 3) KMP_CH(P9, 1, 9) KMP_CH(P10, 1, 10) KMP_CH(P16, 1, 16) KMP_CH(Q17, 0, 17)
+    if (wave_live && r == a.rows - 1) {  // a wave's full last row publishes its cells for the wave below
+      uint32_t* row = xrow + (size_t)wv_ * kXch * a.Ex;
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        row[0 * a.Ex + X + i] = P3[i + 1];
+        row[1 * a.Ex + X + i] = P9[i + 1];
+        row[2 * a.Ex + X + i] = P10[i + 1];
+        row[3 * a.Ex + X + i] = P16[i + 1];
+        row[4 * a.Ex + X + i] = Q17[i + 1];
+      }
+    }
+#pragma unroll
+    for (int i = 1; i <= VX; ++i) {
+      A3[i] = shup(P3[i], a.txn);
+      A9[i] = shup(P9[i], a.txn);
+      A10[i] = shup(P10[i], a.txn);
+      A16[i] = shup(P16[i], a.txn);
+      QA17[i] = shup(Q17[i], a.txn);
+    }
+  }
+  __syncthreads();
+  if (first && wv_ >= 1) {
+    const uint32_t* row = xrow + (size_t)(wv_ - 1) * kXch * a.Ex;
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      A3[i + 1] = row[0 * a.Ex + X + i];
+      A9[i + 1] = row[1 * a.Ex + X + i];
+      A10[i + 1] = row[2 * a.Ex + X + i];
+      A16[i + 1] = row[3 * a.Ex + X + i];
+      QA17[i + 1] = row[4 * a.Ex + X + i];
+    }
+  }
+  A9[0] = shup(A9[VX], 1);  // cell (Y-1, X-1): the lane to the left
+
+  bool vx[VX + 1];
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+  const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+  auto m = [&](const uint32_t (&v)[VX + 1], int q, bool zok, bool yok) { return (zok && yok && vx[q]) ? v[q] : 0u; };
+  auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };  // cell X-1 (all lanes)
+  auto put8 = [&](int k, const uint32_t (&res)[VX]) {  // encode: one map row
+    int par[3];
+    map_parity(3, k, par);
+    if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res));
+  };
+  const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own[1];
+  T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
+  uint32_t ownv[VX];
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own[1], i);
+    else ownv[i] = el16<T>(e0, 2 * i);
+  }
+  // decoded value (DEC) or residual (encode) of map k from its prediction; encode reads the
+  // ground truth element ``gt`` of the stream rows
+  auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      if constexpr (DEC) outv[i] = (pred[i] + el8<T>(mv[k], i)) & MASK;
+      else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+    }
+  };
+
+  // 2. X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); shares highres row
+  //    2Y of plane 2c with the lowres
+  {
+    uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
+    KMP_CH(P15, 1, 15) KMP_CH(Q18, 0, 18)
+    if (!live) return;
+#pragma unroll
+    for (int i = 0; i < VX; ++i)
+      pred[i] = (m(P15, i + 1, vz1, vy1) + m(A16, i + 1, vz1, vy0) + m(QA17, i + 1, vz0, vy0) +
+                 m(Q18, i + 1, vz0, vy1)) >> ((nz * ny) >> 1);
+    code(6, pred, e0, 1, outv);
+    if constexpr (DEC) {
+      st16(h0, pack16<T, VX>(ownv, outv));  // plane 2c, row 2Y: lowres | X
+    } else {
+      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(ownv));
+      put8(6, outv);
+    }
+  }
+  // 3. Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
+  {
+    uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
+    uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
+    KMP_CH(P11, 1, 11) KMP_CH(P12, 1, 12) KMP_CH(Q13, 0, 13) KMP_CH(Q14, 0, 14) KMP_CH(P4, 1, 4) KMP_CH(Q5, 0, 5)
+    left(P12);
+    left(Q13);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pY[i] = (m(P11, i + 1, vz1, vy1) + m(P12, i, vz1, vy1) + m(Q13, i, vz0, vy1) + m(Q14, i + 1, vz0, vy1)) >>
+              ((nz * nx) >> 1);
+      pF[i] = (m(P4, i + 1, vz1, vy1) + m(Q5, i + 1, vz0, vy1)) >> (nz >> 1);
+    }
+    code(5, pY, e1, 0, oY);
+    code(2, pF, e1, 1, oF);
+    if constexpr (DEC) {
+      if (vy1) st16(h0 + a.W_, pack16<T, VX>(oY, oF));  // plane 2c, row 2Y+1: Y | FB
+    } else {
+      put8(5, oY);
+      put8(2, oF);
+    }
+  }
+  // 4. Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
+  {
+    uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
+    uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
+    KMP_CH(P7, 1, 7) KMP_CH(P8, 1, 8) KMP_CH(P2, 1, 2)
+    left(P8);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pZ[i] = (m(P7, i + 1, vz1, vy1) + m(P8, i, vz1, vy1) + m(A9, i, vz1, vy0) + m(A10, i + 1, vz1, vy0)) >>
+              ((ny * nx) >> 1);
+      pU[i] = (m(P2, i + 1, vz1, vy1) + m(A3, i + 1, vz1, vy0)) >> (ny >> 1);
+    }
+    code(4, pZ, o0, 0, oZ);
+    code(1, pU, o0, 1, oU);
+    if constexpr (DEC) {
+      if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));  // plane 2c+1, row 2Y: Z | UD
+    } else {
+      put8(4, oZ);
+      put8(1, oU);
+    }
+  }
+  // 5. LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
+  {
+    uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
+    uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
+    KMP_CH(P0, 1, 0) KMP_CH(P1, 1, 1) KMP_CH(P6, 1, 6)
+    left(P1);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pL[i] = (m(P0, i + 1, vz1, vy1) + m(P1, i, vz1, vy1)) >> (nx >> 1);
+      pC[i] = m(P6, i + 1, vz1, vy1);
+    }
+    code(0, pL, o1, 0, oL);
+    code(3, pC, o1, 1, oC);
+    if constexpr (DEC) {
+      if (vz1 && vy1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));  // plane 2c+1, row 2Y+1: LR | C
+    } else {
+      put8(0, oL);
+      put8(3, oC);
+    }
+  }
+#undef KMP_CH
+}
+
+}  // namespace l3
+
+static int l3_env(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+template <typename T>
+static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
+                              const kmp_region* region, l3::L3& a, dim3& grid, dim3& block, size_t& lds) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
+  if (l3_env("KMP_DISABLE_FAST", 0) || l3_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (C != 1 || pred->kind != KMP_PRED_LINEAR || pred->padding != 0) return false;
+  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
+  const int64_t txn = g.E[2] / VX;
+  if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
+  const int64_t rows = 64 / txn;
+  const int64_t waves = ceil_div(g.E[1], rows);
+  if (waves > 4) return false;  // the workgroup covers the whole plane (row exchange through LDS)
+  int64_t zb = 0, ze = g.E[0];
+  if (region) {
+    if (region->begin[1] > 0 || region->begin[2] > 0 || region->end[1] < g.E[1] || region->end[2] < g.E[2]) return false;
+    zb = region->begin[0] < 0 ? 0 : region->begin[0];
+    ze = region->end[0] > g.E[0] ? g.E[0] : region->end[0];
+    if (ze <= zb) return false;
+  }
+  a.D = (int)g.n[0]; a.H = (int)g.n[1]; a.W_ = (int)g.n[2];
+  a.Lz = (int)g.L[0]; a.Ly = (int)g.L[1]; a.Lx = (int)g.L[2];
+  a.Ez = (int)g.E[0]; a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
+  a.Lcz = (int)g.Lc[0]; a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
+  a.zbegin = (int)zb; a.zend = (int)ze;
+  a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)waves;
+  const int64_t nblk = B * (ze - zb);
+  a.xcd_per = (l3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  lds = (size_t)(l3::kWtWords + waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
+  grid = dim3((unsigned)nblk);
+  block = dim3((unsigned)(64 * waves));
+  return nblk < ((int64_t)1 << 31);
+}
+
+template <typename T>
+int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                        const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    l3::L3 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!linear3d_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k)
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+    a.hi_in = hi;
+    a.lo_out = lowres;
+    a.maps = maps;
+    a.W = pred->weights;
+    a.b = pred->bias;
+    l3::linear3d_kernel<T, false><<<grid, block, lds, stream>>>(a);
+    return check_launch("linear3d_encode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                        const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
+    l3::L3 a{};
+    dim3 grid, block;
+    size_t lds = 0;
+    if (!linear3d_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k) {
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      a.maps.p[k] = (void*)maps.p[k];
+    }
+    a.hi_out = hi;
+    a.lo_in = lowres;
+    a.W = pred->weights;
+    a.b = pred->bias;
+    l3::linear3d_kernel<T, true><<<grid, block, lds, stream>>>(a);
+    return check_launch("linear3d_decode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+#define KMP_L3_INST(T)                                                                                    \
+  template int try_linear3d_encode<T>(const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,   \
+                                      const MapPtrs&, const kmp_region*, hipStream_t);                    \
+  template int try_linear3d_decode<T>(const T*, const CMapPtrs&, const Geo&, int64_t, int64_t,            \
+                                      const kmp_predictor*, T*, const kmp_region*, hipStream_t);
+KMP_L3_INST(uint8_t)
+KMP_L3_INST(uint16_t)
+KMP_L3_INST(int32_t)
+KMP_L3_INST(uint32_t)
+
+}  // namespace kmp
