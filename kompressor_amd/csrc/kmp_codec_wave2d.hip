@@ -35,7 +35,7 @@ struct W2 {
   int32_t ybeg, yend;            // output rows written (a chunked-driver region; all rows otherwise)
 };
 
-template <typename T, bool DEC>
+template <typename T, bool DEC, bool ONE>
 __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -62,8 +62,12 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   const bool last = r == a.rows - 1 || Y == a.Ey - 1;
   const bool vy1 = Y < a.Lcy;  // cell row Y (== highres row 2Y+1) exists
   const bool vy0 = Y >= 1;
-  const bool need_halo = live && ((first && Y0 >= 1) || (last && vy1));
-  const int yh = first ? (Y0 >= 1 ? Y0 - 1 : 0) : lsrc(Yc + 1, a.Ly, a.Ey);
+  // one halo row per lane (its wave's first row: Y0-1, last row: Y+1); a one-row wave (ONE, 64
+  // lanes per output row) needs both: ``halo`` above and ``hdn`` below
+  const bool need_halo = live && (ONE ? (Y0 >= 1) : ((first && Y0 >= 1) || (last && vy1)));
+  const bool need_dn = ONE && live && vy1;
+  const int yh = (ONE || first) ? (Y0 >= 1 ? Y0 - 1 : 0) : lsrc(Yc + 1, a.Ly, a.Ey);
+  const int ydn = lsrc(Yc + 1, a.Ly, a.Ey);
   const bool xlast = tx == a.txn - 1;
 
   const int64_t himg = (int64_t)a.H * a.W;
@@ -75,47 +79,57 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   const int64_t m_ud = (b * a.Ey + Yc) * a.Ex + X;   // UD map and lowres: [B, Ey, Ex]
 
   // ---- every load up front ----
-  V own{}, halo{};
+  V own{}, halo{}, hdn{};
   uint4 o0 = make_uint4(0, 0, 0, 0);
   uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
   if constexpr (DEC) {
     if (live) own = ld8c(lin + Yc * a.Ex + X);
     if (need_halo) halo = ld8c(lin + yh * a.Ex + X);
+    if (need_dn) hdn = ld8c(lin + ydn * a.Ex + X);
     if (live && vy1) mv[0] = ld8((const T*)a.maps.p[0] + m_lr);
     if (live) mv[1] = ld8((const T*)a.maps.p[1] + m_ud);
     if (live && vy1) mv[2] = ld8((const T*)a.maps.p[2] + m_lr);
   } else {
     if (live) own = ld16c(hin + 2 * Yc * a.W + hx);  // node row: re-read as a neighbour's halo
     if (need_halo) halo = ld16c(hin + 2 * yh * a.W + hx);
+    if (need_dn) hdn = ld16c(hin + 2 * ydn * a.W + hx);
     if (live && vy1) o0 = ld16(hin + (2 * Yc + 1) * a.W + hx);
   }
 
   // ---- 2x2 node sums: row Y, and on the wave's first row also row Y-1 ----
-  uint32_t n[VX], nh[VX];
+  uint32_t n[VX], nh[VX], nd[VX];
 #pragma unroll
   for (int i = 0; i < VX; ++i) {
     if constexpr (DEC) {
       n[i] = el8<T>(own, i);
       nh[i] = el8<T>(halo, i);
+      nd[i] = el8<T>(hdn, i);
     } else {
       n[i] = el16<T>(own, 2 * i);
       nh[i] = el16<T>(halo, 2 * i);
+      nd[i] = el16<T>(hdn, 2 * i);
     }
   }
-  uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1);
+  uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1), ndx1 = ONE ? shdn(nd[0], 1) : 0u;
   if (xlast) {  // node X+VX = Ex: the mirrored node Ex-1 (even pad), or no cell at all (odd)
     nx1 = n[VX - 1];
     nhx1 = nh[VX - 1];
+    ndx1 = nd[VX - 1];
   }
   uint32_t M1[VX + 1], M0[VX + 1];  // cell rows Y / Y-1, cols X-1 .. X+VX-1
 #pragma unroll
   for (int i = 0; i < VX; ++i) {
     const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
     const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
-    const uint32_t below = shdn(h, a.txn);
-    M1[i + 1] = (h + (last ? hh : below)) >> 2;
-    const uint32_t above = shup(M1[i + 1], a.txn);
-    M0[i + 1] = first ? (hh + h) >> 2 : above;
+    if constexpr (ONE) {
+      M1[i + 1] = (h + nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1)) >> 2;
+      M0[i + 1] = (hh + h) >> 2;
+    } else {
+      const uint32_t below = shdn(h, a.txn);
+      M1[i + 1] = (h + (last ? hh : below)) >> 2;
+      const uint32_t above = shup(M1[i + 1], a.txn);
+      M0[i + 1] = first ? (hh + h) >> 2 : above;
+    }
   }
   M1[0] = shup(M1[VX], 1);
   M0[0] = shup(M0[VX], 1);
@@ -187,9 +201,9 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;  // 32-bit offsets inside an image
   const int64_t txn = g.E[2] / VX;
-  if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
+  if (txn * VX != g.E[2] || txn < 1 || txn > 64 || (txn & (txn - 1)) != 0) return false;
   const int64_t rows = 64 / txn;
-  if (g.E[1] % rows == 1) return false;  // a one-row wave would need both halo rows
+  if (rows > 1 && g.E[1] % rows == 1) return false;  // a one-row wave in a multi-row layout
   const int64_t waves = ceil_div(g.E[1], rows);
   const int64_t nwv = waves < 4 ? waves : 4;
   const int64_t ngrp = ceil_div(waves, nwv);
@@ -220,7 +234,8 @@ int try_wave2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
-    w2::wave2d_kernel<T, false><<<grid, block, 0, stream>>>(a);
+    if (a.rows == 1) w2::wave2d_kernel<T, false, true><<<grid, block, 0, stream>>>(a);
+    else w2::wave2d_kernel<T, false, false><<<grid, block, 0, stream>>>(a);
     return check_launch("wave2d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -240,7 +255,8 @@ int try_wave2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64
     }
     a.hi_out = hi;
     a.lo_in = lowres;
-    w2::wave2d_kernel<T, true><<<grid, block, 0, stream>>>(a);
+    if (a.rows == 1) w2::wave2d_kernel<T, true, true><<<grid, block, 0, stream>>>(a);
+    else w2::wave2d_kernel<T, true, false><<<grid, block, 0, stream>>>(a);
     return check_launch("wave2d_decode");
   }
   return KMP_ERR_UNSUPPORTED;

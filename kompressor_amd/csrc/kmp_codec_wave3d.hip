@@ -45,11 +45,12 @@ struct W3 {
   int32_t nt_nodes; // plane kernel: 1 = non-temporal node-row loads, 0 = default policy (L2-shared halo)
 };
 
-// rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row
+// rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row;
+// one-row waves (64 lanes per output row) need both: ``halo`` above, ``dn`` below
 template <bool DEC>
 struct NodeRows {
   using V = typename std::conditional<DEC, uint2, uint4>::type;
-  V own, halo;
+  V own, halo, dn;
 };
 // encode: the non-node rows of output plane q (plane 2q row 2Y+1, plane 2q+1 rows 2Y, 2Y+1)
 // decode: the 7 residual rows of output plane q
@@ -60,7 +61,7 @@ struct OutRows {
 };
 
 // WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
-template <typename T, bool DEC, int PL, int WPE>
+template <typename T, bool DEC, int PL, int WPE, bool ONE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -140,7 +141,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       } else {
         if (live) N[t].own = ld8c(p + lo_own);
       }
-      if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
+      if constexpr (ONE) {
+        if (need_up) N[t].halo = ld8c(p + lo_up);
+        if (need_dn) N[t].dn = ld8c(p + lo_dn);
+      } else {
+        if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
+      }
     } else {
       const T* p = hin + 2 * sz * hplane;
       if (a.nt_nodes) {
@@ -148,7 +154,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       } else {
         if (live) N[t].own = ld16c(p + ho_own);
       }
-      if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
+      if constexpr (ONE) {
+        if (need_up) N[t].halo = ld16c(p + ho_up);
+        if (need_dn) N[t].dn = ld16c(p + ho_dn);
+      } else {
+        if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
+      }
     }
   }
 #pragma unroll
@@ -177,26 +188,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
   for (int t = 0; t < PL + 2; ++t) {
     // own node row, and the halo row (row Y0-1 on the wave's first row, Y+1 on its last row)
-    uint32_t n[VX], nh[VX];
+    uint32_t n[VX], nh[VX], nd[VX];
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       if constexpr (DEC) {
-        n[i] = el8<T>(N[t].own, i); nh[i] = el8<T>(N[t].halo, i);
+        n[i] = el8<T>(N[t].own, i); nh[i] = el8<T>(N[t].halo, i); nd[i] = el8<T>(N[t].dn, i);
       } else {
-        n[i] = el16<T>(N[t].own, 2 * i); nh[i] = el16<T>(N[t].halo, 2 * i);
+        n[i] = el16<T>(N[t].own, 2 * i); nh[i] = el16<T>(N[t].halo, 2 * i); nd[i] = el16<T>(N[t].dn, 2 * i);
       }
     }
-    uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1);
+    uint32_t nx1 = shdn(n[0], 1), nhx1 = shdn(nh[0], 1), ndx1 = ONE ? shdn(nd[0], 1) : 0u;
     if (xlast) {
       nx1 = n[VX - 1];
       nhx1 = nh[VX - 1];
+      ndx1 = nd[VX - 1];
     }
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
       const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
-      const uint32_t below = shdn(h, a.txn);
-      S[t][i] = h + (last ? hh : below);
+      if constexpr (ONE) {  // every lane is its wave's first and last row
+        const uint32_t hd = nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1);
+        S[t][i] = h + hd;
+      } else {
+        const uint32_t below = shdn(h, a.txn);
+        S[t][i] = h + (last ? hh : below);
+      }
       Su[t][i] = hh + h;
     }
   }
@@ -313,9 +330,9 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;  // 32-bit offsets inside a tile
   const int64_t txn = g.E[2] / VX;
-  if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
+  if (txn * VX != g.E[2] || txn < 1 || txn > 64 || (txn & (txn - 1)) != 0) return false;
   const int64_t rows = 64 / txn;
-  if (g.E[1] % rows == 1) return false;  // a one-row wave would need both halo rows
+  if (rows > 1 && g.E[1] % rows == 1) return false;  // a one-row wave in a multi-row layout
   const int64_t waves = ceil_div(g.E[1], rows);
   const int64_t nwv = waves < 4 ? waves : 4;
   const int64_t nyg = ceil_div(waves, nwv);
@@ -349,8 +366,14 @@ template <typename T, bool DEC>
 static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
   // PL = 2 at 3 waves / SIMD is the measured optimum at C3 (profiles/round1/kprof_wave3d.log):
   // PL = 1 re-reads twice the z halo per output plane; forcing 4 waves / SIMD spills
-  if (pl == 1) w3::wave3d_plane_kernel<T, DEC, 1, 4><<<grid, block, 0, stream>>>(a);
-  else w3::wave3d_plane_kernel<T, DEC, 2, 3><<<grid, block, 0, stream>>>(a);
+  if (a.rows == 1) {  // 64 lanes per output row (wide volumes): both halo rows per lane
+    if (pl == 1) w3::wave3d_plane_kernel<T, DEC, 1, 4, true><<<grid, block, 0, stream>>>(a);
+    else w3::wave3d_plane_kernel<T, DEC, 2, 3, true><<<grid, block, 0, stream>>>(a);
+  } else if (pl == 1) {
+    w3::wave3d_plane_kernel<T, DEC, 1, 4, false><<<grid, block, 0, stream>>>(a);
+  } else {
+    w3::wave3d_plane_kernel<T, DEC, 2, 3, false><<<grid, block, 0, stream>>>(a);
+  }
 }
 
 template <typename T>

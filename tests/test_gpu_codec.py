@@ -208,3 +208,30 @@ def test_categorical_coder_vs_oracle(kom):
         got = kom.utils.decode_categorical(logits, x)
         want = oracle.common.decode_categorical(logits, x)
         assert np.array_equal(got, want), L
+
+
+@pytest.mark.parametrize('shape,dtype,p', [
+    ((1, 6, 8, 512, 1), np.uint16, 0),    # 64 lanes per output row: one-row waves (both halos)
+    ((2, 7, 5, 512, 1), np.uint16, 0),    # odd depth / height
+    ((1, 5, 6, 1024, 1), np.uint8, 0),
+    ((1, 9, 9, 512, 1), np.uint16, 1),    # p = 1 on a wide row (fast3d / generic)
+    ((2, 9, 1024, 1), np.uint8, 0),       # images, one-row waves
+    ((3, 10, 512, 1), np.uint16, 0),
+    ((2, 11, 512, 1), np.uint16, 0),
+])
+def test_wide_rows_match_oracle(kom, shape, dtype, p):
+    """Wide volumes / images (a whole 512^3 volume as ONE array has 256 outputs per row)."""
+    import oracle
+    from oracle import predictors as OP
+    ndim = len(shape) - 2
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    enc, dec, oenc = (ns.encode_values_uint16, ns.decode_values_uint16, ons.encode_values_uint16) \
+        if dtype == np.uint16 else (ns.encode_values_uint8, ns.decode_values_uint8, ons.encode_values_uint8)
+    x = np.random.default_rng(5).integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, ndim), oenc, x, padding=p)
+    pred = kom.MeanPredictor(p, ndim)
+    lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for a, b in zip(maps, want_maps):
+        assert np.array_equal(a, b)
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)

@@ -94,7 +94,7 @@ def main():
         t = cpu_time(rnd)
         return sample.nbytes * 2 * 2 / t / 1e9, f'{sample.shape[0]} tiles, oracle encode+decode, 1 thread'
 
-    def codec_rows(tag, ns, ons, x, xh, pred, opf, enc, dec, oenc, odec, padding, raw, ndim):
+    def codec_rows(tag, ns, ons, x, xh, pred, opf, enc, dec, oenc, odec, padding, raw, ndim, with_cpu=True):
         if want and tag not in want:
             return
         coder = _nd.NATURAL_CODER[x.dtype]
@@ -107,7 +107,7 @@ def main():
         torch.cuda.synchronize()
         assert torch.equal(rec, x), tag
         te, td = gpu_time(fe, args.reps), gpu_time(fd, args.reps)
-        cpu = cpu_codec(ons, opf, oenc, odec, xh[:2], padding)
+        cpu = cpu_codec(ons, opf, oenc, odec, xh[:2], padding) if with_cpu else None
         emit(tag + ':encode', f'fused encode {pred!r}', 2 * raw, te, cpu)
         emit(tag + ':decode', f'fused decode {pred!r}', 2 * raw, td)
 
@@ -127,6 +127,13 @@ def main():
         codec_rows(f'volume_linear_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3),
                    OP.linear_predictions_fn(p, w, b, 3), V.encode_values_uint16, V.decode_values_uint16,
                    OV.encode_values_uint16, OV.decode_values_uint16, p, raw_v, 3)
+
+    # ONE 512^3 volume as a single array (global-volume mode on one GPU: 256 outputs per row)
+    if not want or 'volume_global' in want:
+        g = vol.view(8, 8, 8, 64, 64, 64).permute(0, 3, 1, 4, 2, 5).reshape(1, 512, 512, 512, 1)
+        codec_rows('volume_global', V, OV, g, None, kom.MeanPredictor(0, 3), None, V.encode_values_uint16,
+                   V.decode_values_uint16, None, None, 0, raw_v, 3, with_cpu=False)
+        del g
 
     # chunked drivers (encode_decode_chunk.py:33-117) at C3, chunk 32 (the reference default)
     if not want or 'volume_chunks' in want:
