@@ -47,13 +47,18 @@ def build(verbose=True, jobs=None):
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+    stamp = os.path.join(BUILD, 'objects.txt')  # relink when the set of sources changes too
+    listing = '\n'.join(sorted(objs))
+    same_set = os.path.exists(stamp) and open(stamp).read() == listing
+    if same_set and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
     cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB + '.tmp']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(LIB + '.tmp', LIB)
+    with open(stamp, 'w') as f:
+        f.write(listing)
     return LIB
 
 
