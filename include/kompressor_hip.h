@@ -74,6 +74,12 @@ const char* kmp_last_error(void);
 /* 1 if the kernels were built for the device's ISA (gfx950) and a device is visible. */
 int kmp_device_ok(void);
 
+/* Device address of pinned (page-locked, device-mapped) host memory, for zero-copy streaming:
+   the fused kernels then read the input from / write the outputs to host memory over the host
+   link directly (kompressor_amd.stream, the reference's host-resident arrays,
+   volume/encode_decode.py:30-85).  KMP_ERR_UNSUPPORTED if ``host`` is not such memory. */
+int kmp_host_device_pointer(void* host, void** device);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Fused encode / decode (one pass over HBM each).                                           */
 /* ---------------------------------------------------------------------------------------- */

@@ -54,6 +54,7 @@ _PROTOS = {
     'kmp_version': (ctypes.c_char_p, []),
     'kmp_last_error': (ctypes.c_char_p, []),
     'kmp_device_ok': (ctypes.c_int, []),
+    'kmp_host_device_pointer': (ctypes.c_int, [_vp, _vpp]),
     'kmp_volume_encode': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor), _i32,
                                          _vp, _vpp, _i32p, ctypes.POINTER(Region), _vp, ctypes.c_size_t, _vp]),
     'kmp_volume_decode': (ctypes.c_int, [_i32, _vp, _vpp, _i64, _i64, _i64, _i64, _i64, _i32p,

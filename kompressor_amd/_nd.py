@@ -370,6 +370,33 @@ def encoded_shapes(shape, nsp):
     return lo, maps, dims
 
 
+_HOST_PTRS = {}
+
+
+def _ptr(t):
+    """Device address of ``t``: its data pointer for a device tensor; for a pinned host tensor the
+    device mapping of the page-locked buffer (zero-copy: the kernel reads / writes host memory
+    over the host link directly, ``kmp_host_device_pointer``)."""
+    if t.is_cuda:
+        return t.data_ptr()
+    if not t.is_pinned():
+        raise TypeError('fused kernels take device tensors or pinned host tensors')
+    base = t.untyped_storage().data_ptr()
+    dbase = _HOST_PTRS.get(base)
+    if dbase is None:
+        out = ctypes.c_void_p()
+        check(lib.kmp_host_device_pointer(ctypes.c_void_p(base), ctypes.byref(out)), 'host_device_pointer')
+        dbase = _HOST_PTRS[base] = out.value
+    return dbase + (t.data_ptr() - base)
+
+
+def _ptrs(tensors):
+    arr = (ctypes.c_void_p * 7)()
+    for i, t in enumerate(tensors):
+        arr[i] = _ptr(t)
+    return arr
+
+
 def workspace_bytes(h, predictor, nsp):
     """Device workspace the fused calls may need for highres ``h`` (0 on the one-pass path)."""
     B, sp, C = h.shape[0], _sp(h.shape, nsp), _C(h.shape, nsp)
@@ -388,8 +415,8 @@ def fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=None, works
     ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need)
     dims = (ctypes.c_int32 * 3)()
     reg = _region(nsp, region)
-    args = (dev.dtype_code(h), h.data_ptr(), B, *sp, C, ctypes.byref(pstruct), coder, lowres.data_ptr(),
-            _lib.ptrs(maps), dims, ctypes.byref(reg) if reg is not None else None, ws.data_ptr(), ws.numel(),
+    args = (dev.dtype_code(h), _ptr(h), B, *sp, C, ctypes.byref(pstruct), coder, _ptr(lowres),
+            _ptrs(maps), dims, ctypes.byref(reg) if reg is not None else None, ws.data_ptr(), ws.numel(),
             dev.stream())
     fn = lib.kmp_volume_encode if nsp == 3 else lib.kmp_image_encode
     check(fn(*args), 'fused encode')
@@ -407,8 +434,8 @@ def fused_decode_into(lowres, maps, dims, predictor, coder, out, nsp, region=Non
     ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need)
     reg = _region(nsp, region)
     dims_c = _lib.i32xn(dims)
-    args = (dev.dtype_code(lowres), lowres.data_ptr(), _lib.ptrs(maps), B, *E, C, dims_c, ctypes.byref(pstruct),
-            coder, out.data_ptr(), ctypes.byref(reg) if reg is not None else None, ws.data_ptr(), ws.numel(),
+    args = (dev.dtype_code(lowres), _ptr(lowres), _ptrs(maps), B, *E, C, dims_c, ctypes.byref(pstruct),
+            coder, _ptr(out), ctypes.byref(reg) if reg is not None else None, ws.data_ptr(), ws.numel(),
             dev.stream())
     fn = lib.kmp_volume_decode if nsp == 3 else lib.kmp_image_decode
     check(fn(*args), 'fused decode')

@@ -363,6 +363,16 @@ int kmp_device_ok(void) {
   return 1;
 }
 
+int kmp_host_device_pointer(void* host, void** device) {
+  KMP_REQUIRE(host && device, "null pointer");
+  hipError_t e = hipHostGetDevicePointer(device, host, 0);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(KMP_ERR_UNSUPPORTED, std::string("not device-mapped host memory: ") + hipGetErrorString(e));
+  }
+  return KMP_OK;
+}
+
 int kmp_lowres_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3],
                             int64_t C, void* out, kmp_stream_t stream) {
   if (int s = check_common(nsp, B, shape, C)) return s;

@@ -13,6 +13,14 @@ issued ahead of it (stream order), while the other slots' copies and kernels ove
 host->device and device->host DMA engines and the CUs run concurrently).  Host buffers must be
 pinned (``torch.empty(..., pin_memory=True)``) for the copies to be asynchronous DMA.
 
+For 8/16-bit samples the default is **zero-copy** instead: pinned host memory is mapped into the
+GPU's address space (``kmp_host_device_pointer``), so ONE fused launch reads the host input and
+writes the host outputs over the link itself -- reads and writes interleave, using both link
+directions at once, with no staging buffers and no per-map DMA descriptors (8 outputs per chunk
+made the copy pipeline descriptor-bound: 16.4 GB/s vs 20.1 GB/s end to end at C3 on MI355X,
+``profiles/round1/h2d_probe.log``).  32-bit samples keep the copy pipeline: their generic
+two-pass kernels would read the input across the link twice.
+
 float32 data (config C5) is coded losslessly by bit-casting to uint32 and using the mod-2^32
 coder (``encode_values_uint32``), a build extension: the reference has no lossless float coder
 (``encode_values_raw`` truncates through ``int32``, ``utils.py:28-30``).
@@ -42,9 +50,10 @@ class TileStream:
     move per copy.
     """
 
-    def __init__(self, predictor, tile_shape, dtype, chunk, slots=3, ndim=3):
+    def __init__(self, predictor, tile_shape, dtype, chunk, slots=3, ndim=3, zero_copy=None):
         dev.require_gpu()
         self.ndim = ndim
+        self.zero_copy = (dtype in (torch.uint8, torch.uint16)) if zero_copy is None else bool(zero_copy)
         self.predictor = predictor
         self.chunk = int(chunk)
         self.slots = int(slots)
@@ -85,6 +94,11 @@ class TileStream:
         cur = torch.cuda.current_stream()
         for s in self._streams:
             s.wait_stream(cur)
+        if self.zero_copy and src.is_pinned() and host_lowres.is_pinned() and all(m.is_pinned() for m in host_maps):
+            with torch.cuda.stream(self._streams[0]):
+                _nd.fused_encode_into(src, self.predictor, self.coder, host_lowres, list(host_maps), self.ndim,
+                                      workspace=self._ws[0] if n <= self.chunk else None)
+            return host_lowres, host_maps
         for slot, b, e in self._chunks(n):
             k = e - b
             with torch.cuda.stream(self._streams[slot]):
@@ -104,6 +118,11 @@ class TileStream:
         cur = torch.cuda.current_stream()
         for s in self._streams:
             s.wait_stream(cur)
+        if self.zero_copy and dst.is_pinned() and host_lowres.is_pinned() and all(m.is_pinned() for m in host_maps):
+            with torch.cuda.stream(self._streams[0]):
+                _nd.fused_decode_into(host_lowres, list(host_maps), self.dims, self.predictor, self.coder, dst,
+                                      self.ndim, workspace=self._ws[0] if n <= self.chunk else None)
+            return host_out
         for slot, b, e in self._chunks(n):
             k = e - b
             with torch.cuda.stream(self._streams[slot]):

@@ -15,12 +15,13 @@ def _pinned_from(a):
     return t
 
 
+@pytest.mark.parametrize('zero_copy', [False, True])
 @pytest.mark.parametrize('ndim,shape,dtype,chunk,slots', [
     (3, (10, 16, 16, 16, 1), np.uint16, 3, 2),     # ragged last chunk
     (3, (8, 64, 64, 64, 1), np.uint16, 2, 3),      # metric tile
     (2, (9, 64, 32, 1), np.uint8, 4, 3),
 ])
-def test_stream_equals_device_resident(kom, ndim, shape, dtype, chunk, slots):
+def test_stream_equals_device_resident(kom, ndim, shape, dtype, chunk, slots, zero_copy):
     rng = np.random.default_rng(11)
     host = rng.integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
     ns = kom.volume if ndim == 3 else kom.image
@@ -28,7 +29,8 @@ def test_stream_equals_device_resident(kom, ndim, shape, dtype, chunk, slots):
     enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if dtype == np.uint16 else \
                (ns.encode_values_uint8, ns.decode_values_uint8)
     ref_lo, (ref_maps, dims) = ns.encode(pred, enc, torch.from_numpy(host).cuda())
-    ts = kom.stream.TileStream(pred, shape[1:], torch.from_numpy(host[:0]).dtype, chunk, slots, ndim)
+    ts = kom.stream.TileStream(pred, shape[1:], torch.from_numpy(host[:0]).dtype, chunk, slots, ndim,
+                               zero_copy=zero_copy)
     src = _pinned_from(host)
     lo, maps = ts.alloc_encoded(shape[0])
     ts.encode(src, lo, maps)
