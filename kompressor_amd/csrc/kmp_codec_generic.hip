@@ -55,12 +55,11 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restric
   const int kz = nsp == 3 ? k : 1;
   const float inv_n = (float)(kz * k * k);
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = t;
-    const int64_t c = r % C; r /= C;
-    const int64_t cx = cf.begin[2] + r % cf.ext[2]; r /= cf.ext[2];
-    const int64_t cy = cf.begin[1] + r % cf.ext[1]; r /= cf.ext[1];
-    const int64_t cz = cf.begin[0] + r % cf.ext[0]; r /= cf.ext[0];
-    const int64_t b = r;
+    int64_t b, cz, cy, cx, c;
+    unflat5(t, cf.ext[0], cf.ext[1], cf.ext[2], C, b, cz, cy, cx, c);
+    cz += cf.begin[0];
+    cy += cf.begin[1];
+    cx += cf.begin[2];
     const int pz = nsp == 3 ? p : 0;
     float sum = 0.0f;
     for (int dz = 0; dz < kz; ++dz)
@@ -79,12 +78,11 @@ __global__ void __launch_bounds__(kGThreads) encode_generic_kernel(const T* __re
   using TO = typename coder_out<CODER>::type;
   const int nmaps = nsp == 3 ? 7 : 3;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = t;
-    const int64_t c = r % C; r /= C;
-    const int64_t ox = f.begin[2] + r % f.ext[2]; r /= f.ext[2];
-    const int64_t oy = f.begin[1] + r % f.ext[1]; r /= f.ext[1];
-    const int64_t oz = f.begin[0] + r % f.ext[0]; r /= f.ext[0];
-    const int64_t b = r;
+    int64_t b, oz, oy, ox, c;
+    unflat5(t, f.ext[0], f.ext[1], f.ext[2], C, b, oz, oy, ox, c);
+    oz += f.begin[0];
+    oy += f.begin[1];
+    ox += f.begin[2];
     auto hv = [&](int pz, int py, int px) -> T {
       return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
     };
@@ -113,12 +111,11 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
   using TO = typename coder_out<CODER>::type;
   const int nmaps = nsp == 3 ? 7 : 3;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = t;
-    const int64_t c = r % C; r /= C;
-    const int64_t ox = f.begin[2] + r % f.ext[2]; r /= f.ext[2];
-    const int64_t oy = f.begin[1] + r % f.ext[1]; r /= f.ext[1];
-    const int64_t oz = f.begin[0] + r % f.ext[0]; r /= f.ext[0];
-    const int64_t b = r;
+    int64_t b, oz, oy, ox, c;
+    unflat5(t, f.ext[0], f.ext[1], f.ext[2], C, b, oz, oy, ox, c);
+    oz += f.begin[0];
+    oy += f.begin[1];
+    ox += f.begin[2];
     auto hout = [&](int pz, int py, int px) -> T& {
       return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
     };

@@ -109,6 +109,8 @@ __host__ __device__ __forceinline__ typename coder_out<CODER>::type code_decode(
 
 // numpy/jnp mode='symmetric' source index for any integer i (periodic mirror, period 2n).
 __host__ __device__ __forceinline__ int64_t sym_index(int64_t i, int64_t n) {
+  if (i >= 0 && i < n) return i;  // interior: no (emulated 64-bit) modulo
+  if (i >= -n && i < 2 * n) return i < 0 ? -1 - i : 2 * n - 1 - i;  // one reflection
   int64_t m = i % (2 * n);
   if (m < 0) m += 2 * n;
   return m < n ? m : 2 * n - 1 - m;
@@ -185,5 +187,32 @@ struct CMapPtrs {
 };
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Flat index t over [B, e0, e1, e2, C] (C fastest).  The grid-stride kernels decompose one index
+// per element: 64-bit division is a long emulated sequence on gfx950, so indices below 2^32 (every
+// array axis and, in practice, every flat index fits) take 32-bit divisions; C == 1 skips one.
+__device__ __forceinline__ void unflat5(int64_t t, int64_t e0, int64_t e1, int64_t e2, int64_t C, int64_t& b,
+                                        int64_t& i0, int64_t& i1, int64_t& i2, int64_t& c) {
+  if ((uint64_t)t < 0x100000000ull) {
+    uint32_t u = (uint32_t)t;
+    const uint32_t uC = (uint32_t)C, u2 = (uint32_t)e2, u1 = (uint32_t)e1, u0 = (uint32_t)e0;
+    if (uC == 1) {
+      c = 0;
+    } else {
+      c = u % uC;
+      u /= uC;
+    }
+    i2 = u % u2; u /= u2;
+    i1 = u % u1; u /= u1;
+    i0 = u % u0;
+    b = u / u0;
+  } else {
+    c = t % C; t /= C;
+    i2 = t % e2; t /= e2;
+    i1 = t % e1; t /= e1;
+    i0 = t % e0;
+    b = t / e0;
+  }
+}
 
 }  // namespace kmp

@@ -68,12 +68,11 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
     // decode this lane's A row (cell)
     const int64_t row = tile * 32 + (lane & 31);
     const bool row_ok = row < rows;
-    int64_t r = row_ok ? row : 0;
-    const int64_t c = r % C; r /= C;
-    const int64_t x = s.cbeg[2] + r % s.cext[2]; r /= s.cext[2];
-    const int64_t y = s.cbeg[1] + r % s.cext[1]; r /= s.cext[1];
-    const int64_t z = s.cbeg[0] + r % s.cext[0]; r /= s.cext[0];
-    const int64_t b = r;
+    int64_t b, z, y, x, c;
+    unflat5(row_ok ? row : 0, s.cext[0], s.cext[1], s.cext[2], C, b, z, y, x, c);
+    z += s.cbeg[0];
+    y += s.cbeg[1];
+    x += s.cbeg[2];
     f32x16 acc;
     const float bj = j < K ? bias[j] : 0.0f;
 #pragma unroll
@@ -89,12 +88,11 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
     for (int q = 0; q < 16; ++q) {
       const int64_t orow = tile * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
       if (orow >= rows) continue;
-      int64_t rr = orow;
-      const int64_t oc = rr % C; rr /= C;
-      const int64_t ox = s.cbeg[2] + rr % s.cext[2]; rr /= s.cext[2];
-      const int64_t oy = s.cbeg[1] + rr % s.cext[1]; rr /= s.cext[1];
-      const int64_t oz = s.cbeg[0] + rr % s.cext[0]; rr /= s.cext[0];
-      const int64_t ob = rr;
+      int64_t ob, oz, oy, ox, oc;
+      unflat5(orow, s.cext[0], s.cext[1], s.cext[2], C, ob, oz, oy, ox, oc);
+      oz += s.cbeg[0];
+      oy += s.cbeg[1];
+      ox += s.cbeg[2];
       const int64_t cell = ((ob * s.Lc[0] + oz) * s.Lc[1] + oy) * s.Lc[2] + ox;
       const int64_t o = (cell * K + j) * C + oc;
       out[o] = cast_f32<T>(acc[q]);

@@ -39,11 +39,7 @@ struct Idx5 {
 };
 __device__ __forceinline__ Idx5 unflatten5(int64_t t, int64_t e0, int64_t e1, int64_t e2, int64_t C) {
   Idx5 r;
-  r.c = t % C; t /= C;
-  r.i2 = t % e2; t /= e2;
-  r.i1 = t % e1; t /= e1;
-  r.i0 = t % e0; t /= e0;
-  r.b = t;
+  unflat5(t, e0, e1, e2, C, r.b, r.i0, r.i1, r.i2, r.c);
   return r;
 }
 
