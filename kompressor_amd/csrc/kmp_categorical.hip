@@ -93,6 +93,90 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_kernel(const float
   }
 }
 
+
+// ---- decode by a wave-wide bitonic sort (L <= 64 * E) ----------------------------------------
+// The descending rank of class i is #{j : key_j > key_i or (key_j == key_i and j > i)}, i.e. the
+// position of the combined 64-bit key (key_i << 32 | i) in DESCENDING order of all combined keys.
+// key is the float mapped to an order-preserving uint32 (-0 -> +0, every NaN -> 0xffffffff: NaN
+// after every number, NaNs equal -- the cat_less / cat_equal order).  The wave sorts its E
+// combined keys per lane (blocked layout, element p = lane * E + e) with a bitonic network --
+// in-register compare-exchange for partner distances < E, xor shuffles above -- and reads the
+// class at position k.  O(L log^2 L) per element instead of the counting kernel's O(L^2).
+__device__ __forceinline__ uint32_t order_key(float f) {
+  if (f != f) return 0xffffffffu;
+  uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <typename T, int E>
+__global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_sort_kernel(const float* __restrict__ logits,
+                                                                                int64_t n, int64_t L,
+                                                                                const T* __restrict__ x,
+                                                                                T* __restrict__ out) {
+  constexpr int NE = 64 * E;
+  __shared__ uint32_t pos_idx[kCatWaves][NE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t el = (int64_t)blockIdx.x * kCatWaves + w; el < n; el += (int64_t)gridDim.x * kCatWaves) {
+    const float* row = logits + el * L;
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      v[e] = i < L ? (((uint64_t)order_key(row[i]) << 32) | (uint32_t)i) : 0ull;  // padding sorts last
+    }
+    // bitonic network, descending overall
+#pragma unroll
+    for (int k = 2; k <= NE; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j < E) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int pe = e ^ j;
+            if (pe > e) {
+              const int p = lane * E + e;
+              const bool desc = (p & k) == 0;  // this block sorts descending
+              const uint64_t a = v[e], b = v[pe];
+              const bool sw = desc ? (a < b) : (a > b);
+              v[e] = sw ? b : a;
+              v[pe] = sw ? a : b;
+            }
+          }
+        } else {
+          const int m = j / E;  // partner lane distance
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int p = lane * E + e;
+            const uint64_t o = shfl_xor64(v[e], m);
+            const bool lower = (p & j) == 0;  // p < partner
+            const bool desc = (p & k) == 0;
+            // keep the larger of the pair at the lower position in a descending block
+            const bool keep_max = (lower == desc);
+            v[e] = keep_max ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) pos_idx[w][lane * E + e] = (uint32_t)v[e];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane == 0) {
+      int64_t k = (int64_t)(std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el]);
+      k = k < 0 ? 0 : (k >= L ? L - 1 : k);
+      out[el] = (T)pos_idx[w][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
 }  // namespace kmp
 
 using namespace kmp;
@@ -110,6 +194,18 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
     if (direction == KMP_ENCODE)
       categorical_kernel<T, KMP_ENCODE><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L, (const T*)x,
                                                                                           (T*)out);
+    else if (L <= 64)
+      categorical_decode_sort_kernel<T, 1><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+                                                                                             (const T*)x, (T*)out);
+    else if (L <= 128)
+      categorical_decode_sort_kernel<T, 2><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+                                                                                             (const T*)x, (T*)out);
+    else if (L <= 256)
+      categorical_decode_sort_kernel<T, 4><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+                                                                                             (const T*)x, (T*)out);
+    else if (L <= 512)
+      categorical_decode_sort_kernel<T, 8><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+                                                                                             (const T*)x, (T*)out);
     else
       categorical_kernel<T, KMP_DECODE><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L, (const T*)x,
                                                                                           (T*)out);

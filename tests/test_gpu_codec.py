@@ -196,11 +196,14 @@ def test_categorical_matches_golden(kom, name, chunk):
 def test_categorical_coder_vs_oracle(kom):
     import oracle
     rng = np.random.default_rng(7)
-    for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32)):
+    for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32),
+                  (64, np.uint8), (128, np.uint16), (512, np.uint16)):
         logits = rng.standard_normal((513, L)).astype(np.float32)
         logits[::7, 3] = logits[::7, 1]  # ties
         if L > 4:
             logits[5, :] = 0.5          # an all-tie row
+            logits[6, :4] = [np.nan, -0.0, 0.0, np.nan]      # NaN after every number, -0 == +0
+            logits[7, :4] = [np.inf, -np.inf, np.nan, np.inf]
         x = rng.integers(0, min(L + 3, np.iinfo(dt).max), size=513).astype(dt)
         got = kom.utils.encode_categorical(logits, x)
         want = oracle.common.encode_categorical(logits, x)
