@@ -518,6 +518,42 @@ def decode(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
 
 
 # =============================================================================================
+# Multi-level pyramid: the reference's single level applied recursively
+# =============================================================================================
+
+def _per_level(fn, levels, what):
+    if isinstance(fn, (list, tuple)):
+        _require(len(fn) == levels, f'{what}: one per level ({levels}) expected, got {len(fn)}')
+        return list(fn)
+    return [fn] * levels
+
+
+def encode_pyramid(predictions_fn, encode_fn, highres, levels, padding, nsp):
+    """``levels`` applications of ``encode`` (volume/encode_decode.py:30-56), each on the previous
+    level's lowres.  ``predictions_fn`` / ``encode_fn`` may be one callable or one per level
+    (finest first).  Returns ``(lowres, [(maps, dims), ...])`` finest level first."""
+    _require(isinstance(levels, int) and not isinstance(levels, bool) and levels >= 1, 'levels must be an int >= 1')
+    preds, encs = _per_level(predictions_fn, levels, 'predictions_fn'), _per_level(encode_fn, levels, 'encode_fn')
+    x, out = highres, []
+    for lvl in range(levels):
+        x, enc = encode(preds[lvl], encs[lvl], x, padding, nsp)
+        out.append(enc)
+    return x, out
+
+
+def decode_pyramid(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
+    """Inverse of :func:`encode_pyramid`: decode the coarsest level first."""
+    encoded = list(encoded)
+    levels = len(encoded)
+    _require(levels >= 1, 'encoded must hold at least one level')
+    preds, decs = _per_level(predictions_fn, levels, 'predictions_fn'), _per_level(decode_fn, levels, 'decode_fn')
+    x = lowres
+    for lvl in reversed(range(levels)):
+        x = decode(preds[lvl], decs[lvl], x, encoded[lvl], padding, nsp)
+    return x
+
+
+# =============================================================================================
 # Chunked drivers -- volume/encode_decode_chunk.py:33-117, image/encode_decode_chunk.py:33-115
 # =============================================================================================
 

@@ -17,6 +17,6 @@ from .losses import \
     mean_squared_error, mean_abs_error, \
     mean_charbonnier_error, mean_total_variation  # noqa: F401
 
-from .encode_decode import encode, decode  # noqa: F401
+from .encode_decode import encode, decode, encode_pyramid, decode_pyramid  # noqa: F401
 from .encode_decode_chunk import encode_chunks, decode_chunks  # noqa: F401
 from . import utils, losses  # noqa: F401

@@ -19,3 +19,14 @@ def encode(predictions_fn, encode_fn, highres, padding=0):
 def decode(predictions_fn, decode_fn, lowres, encoded, padding=0):
     """image/encode_decode.py:59-85 -- returns the losslessly reconstructed highres."""
     return _nd.decode(predictions_fn, decode_fn, lowres, encoded, padding, _N)
+
+
+def encode_pyramid(predictions_fn, encode_fn, highres, levels, padding=0):
+    """Multi-level pyramid (build extension): ``encode`` applied ``levels``
+    times, each on the previous lowres.  Returns ``(lowres, [(maps, dims), ...])``, finest first."""
+    return _nd.encode_pyramid(predictions_fn, encode_fn, highres, levels, padding, _N)
+
+
+def decode_pyramid(predictions_fn, decode_fn, lowres, encoded, padding=0):
+    """Inverse of :func:`encode_pyramid`."""
+    return _nd.decode_pyramid(predictions_fn, decode_fn, lowres, encoded, padding, _N)

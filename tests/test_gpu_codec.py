@@ -238,3 +238,30 @@ def test_wide_rows_match_oracle(kom, shape, dtype, p):
     for a, b in zip(maps, want_maps):
         assert np.array_equal(a, b)
     assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
+
+
+@pytest.mark.parametrize('ndim,shape,dtype,levels,p', [
+    (3, (2, 33, 40, 36, 1), np.uint16, 3, 0),
+    (3, (1, 64, 64, 64, 1), np.uint16, 2, 1),
+    (2, (3, 130, 96, 1), np.uint8, 4, 0),
+])
+def test_pyramid_matches_oracle_composition(kom, ndim, shape, dtype, levels, p):
+    """Multi-level pyramid (f-4): each level equals the oracle's encode of the previous lowres."""
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    enc, dec, oenc = (ns.encode_values_uint16, ns.decode_values_uint16, ons.encode_values_uint16) \
+        if dtype == np.uint16 else (ns.encode_values_uint8, ns.decode_values_uint8, ons.encode_values_uint8)
+    x = np.random.default_rng(8).integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    pred = kom.MeanPredictor(p, ndim)
+    lo, levels_out = ns.encode_pyramid(pred, enc, x, levels, padding=p)
+    assert len(levels_out) == levels
+    cur = x
+    for maps, dims in levels_out:
+        want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, ndim), oenc, cur, padding=p)
+        assert tuple(dims) == tuple(want_dims)
+        for a, b in zip(maps, want_maps):
+            assert np.array_equal(a, b)
+        cur = want_lo
+    assert np.array_equal(lo, cur)
+    assert np.array_equal(ns.decode_pyramid(pred, dec, lo, levels_out, padding=p), x)

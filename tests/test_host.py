@@ -164,3 +164,14 @@ def test_fused_chunk_regions_merge_and_cover():
     # a filtered chunk list leaves outputs unreached -> not covered
     regs, cov = fused_chunk_regions(chunks[:-1], E, 3)
     assert not cov
+
+
+def test_pyramid_validates_levels():
+    import kompressor_amd as kom
+    for bad in (0, -1, 1.5, True):
+        with pytest.raises(AssertionError):
+            kom.volume.encode_pyramid(kom.MeanPredictor(0, 3), kom.volume.encode_values_uint16,
+                                      np.zeros((1, 9, 9, 9, 1), np.uint16), bad)
+    with pytest.raises(AssertionError):
+        kom.volume.encode_pyramid([kom.MeanPredictor(0, 3)], kom.volume.encode_values_uint16,
+                                  np.zeros((1, 9, 9, 9, 1), np.uint16), 2)

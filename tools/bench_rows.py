@@ -128,6 +128,14 @@ def main():
                    OP.linear_predictions_fn(p, w, b, 3), V.encode_values_uint16, V.decode_values_uint16,
                    OV.encode_values_uint16, OV.decode_values_uint16, p, raw_v, 3)
 
+    for p in (0,):
+        n = (2 * p + 2) ** 2
+        w = (1.0 / n + rng.standard_normal((n, 5)) * (0.3 / n)).astype(np.float32)
+        b = np.zeros(5, np.float32)
+        codec_rows(f'image_linear_p{p}', I, OI, img, img_h, kom.LinearPredictor(w, b, p, 2),
+                   OP.linear_predictions_fn(p, w, b, 2), I.encode_values_uint8, I.decode_values_uint8,
+                   OI.encode_values_uint8, OI.decode_values_uint8, p, raw_i, 2)
+
     # ONE 512^3 volume as a single array (global-volume mode on one GPU: 256 outputs per row)
     if not want or 'volume_global' in want:
         g = vol.view(8, 8, 8, 64, 64, 64).permute(0, 3, 1, 4, 2, 5).reshape(1, 512, 512, 512, 1)
