@@ -33,9 +33,20 @@ struct W2 {
   int32_t txn, rows, nwv, ngrp;  // lanes per row, rows per wave, waves per workgroup, workgroups per image
   int32_t xcd_per;               // > 0: image-per-XCD block order (workgroups per image)
   int32_t ybeg, yend;            // output rows written (a chunked-driver region; all rows otherwise)
+  const float* wt;               // LIN: LinearPredictor weights [4, 5] row-major and bias [5]
+  const float* bias;
 };
 
-template <typename T, bool DEC, bool ONE>
+template <typename T>
+__device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: trunc, saturate, NaN -> 0
+  constexpr float hi = sizeof(T) == 2 ? 65535.0f : 255.0f;
+  return (uint32_t)fminf(fmaxf(v, 0.0f), hi);
+}
+
+// LIN: the LinearPredictor with p = 0 instead of the mean (image/utils.py:58-86 on its 5
+// per-cell channels): pred[cell, k] = fma chain over the 4 nodes (n = dy*2 + dx) from b[k], cast
+// to T; LR = ch0 (x) + ch1 (x-1), UD = ch2 (y) + ch3 (y-1), C = ch4, with the same counts / shifts.
+template <typename T, bool DEC, bool ONE, bool LIN>
 __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -116,41 +127,94 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
     nhx1 = nh[VX - 1];
     ndx1 = nd[VX - 1];
   }
-  uint32_t M1[VX + 1], M0[VX + 1];  // cell rows Y / Y-1, cols X-1 .. X+VX-1
+  uint32_t M1[VX + 1], M0[VX + 1];  // mean: cell rows Y / Y-1, cols X-1 .. X+VX-1
+  uint32_t P0[VX + 1], P1[VX + 1], P2[VX + 1], A3[VX + 1], P4[VX + 1];  // LIN channels (q = cell X-1+q)
+  if constexpr (!LIN) {
 #pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
-    const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
-    if constexpr (ONE) {
-      M1[i + 1] = (h + nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1)) >> 2;
-      M0[i + 1] = (hh + h) >> 2;
-    } else {
-      const uint32_t below = shdn(h, a.txn);
-      M1[i + 1] = (h + (last ? hh : below)) >> 2;
-      const uint32_t above = shup(M1[i + 1], a.txn);
-      M0[i + 1] = first ? (hh + h) >> 2 : above;
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t h = n[i] + (i + 1 < VX ? n[i + 1] : nx1);
+      const uint32_t hh = nh[i] + (i + 1 < VX ? nh[i + 1] : nhx1);
+      if constexpr (ONE) {
+        M1[i + 1] = (h + nd[i] + (i + 1 < VX ? nd[i + 1] : ndx1)) >> 2;
+        M0[i + 1] = (hh + h) >> 2;
+      } else {
+        const uint32_t below = shdn(h, a.txn);
+        M1[i + 1] = (h + (last ? hh : below)) >> 2;
+        const uint32_t above = shup(M1[i + 1], a.txn);
+        M0[i + 1] = first ? (hh + h) >> 2 : above;
+      }
     }
+    M1[0] = shup(M1[VX], 1);
+    M0[0] = shup(M0[VX], 1);
+  } else {
+    // node rows Y (n), Y+1 (nb) and Y-1 (nu: this lane's halo when it is the wave's first row)
+    float fn[VX + 1], fb[VX + 1], fu[VX + 1];
+    const uint32_t bx1 = shdn(nx1, a.txn);
+#pragma unroll
+    for (int i = 0; i <= VX; ++i) {
+      const uint32_t own_i = i < VX ? n[i] : nx1;
+      const uint32_t below_i = i < VX ? shdn(n[i], a.txn) : bx1;
+      const uint32_t halo_dn = ONE ? (i < VX ? nd[i] : ndx1) : (i < VX ? nh[i] : nhx1);
+      fn[i] = (float)own_i;
+      fb[i] = (float)((ONE || last) ? halo_dn : below_i);
+      fu[i] = (float)(i < VX ? nh[i] : nhx1);
+    }
+    auto chan = [&](int k, const float (&r0)[VX + 1], const float (&r1)[VX + 1], uint32_t (&o)[VX + 1]) {
+      const float w0 = a.wt[0 * 5 + k], w1 = a.wt[1 * 5 + k], w2 = a.wt[2 * 5 + k], w3 = a.wt[3 * 5 + k];
+      const float bk = a.bias[k];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        float acc = bk;
+        acc = __builtin_fmaf(r0[i], w0, acc);
+        acc = __builtin_fmaf(r0[i + 1], w1, acc);
+        acc = __builtin_fmaf(r1[i], w2, acc);
+        acc = __builtin_fmaf(r1[i + 1], w3, acc);
+        o[i + 1] = cast_t<T>(acc);
+      }
+    };
+    uint32_t P3[VX + 1], U3[VX + 1];
+    chan(0, fn, fb, P0);
+    chan(1, fn, fb, P1);
+    chan(2, fn, fb, P2);
+    chan(3, fn, fb, P3);
+    chan(4, fn, fb, P4);
+    chan(3, fu, fn, U3);  // cell row Y-1 (used on the wave's first row)
+#pragma unroll
+    for (int i = 1; i <= VX; ++i) {
+      const uint32_t above = shup(P3[i], a.txn);
+      A3[i] = (ONE || first) ? U3[i] : above;
+    }
+    P1[0] = shup(P1[VX], 1);
   }
-  M1[0] = shup(M1[VX], 1);
-  M0[0] = shup(M0[VX], 1);
   if (!live || Y < a.ybeg || Y >= a.yend) return;
 
   bool vx[VX + 1];
 #pragma unroll
   for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) {
-    M1[q] = (vy1 && vx[q]) ? M1[q] : 0u;
-    M0[q] = (vy0 && vx[q]) ? M0[q] : 0u;
-  }
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
   uint32_t pred[3][VX];  // LR, UD, C
+  if constexpr (!LIN) {
 #pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-    pred[0][i] = (M1[i] + M1[i + 1]) >> (nx >> 1);      // LR: cells (Y, x-1), (Y, x)
-    pred[1][i] = (M0[i + 1] + M1[i + 1]) >> (ny >> 1);  // UD: cells (Y-1, x), (Y, x)
-    pred[2][i] = M1[i + 1];                             // C
+    for (int q = 0; q <= VX; ++q) {
+      M1[q] = (vy1 && vx[q]) ? M1[q] : 0u;
+      M0[q] = (vy0 && vx[q]) ? M0[q] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pred[0][i] = (M1[i] + M1[i + 1]) >> (nx >> 1);      // LR: cells (Y, x-1), (Y, x)
+      pred[1][i] = (M0[i + 1] + M1[i + 1]) >> (ny >> 1);  // UD: cells (Y-1, x), (Y, x)
+      pred[2][i] = M1[i + 1];                             // C
+    }
+  } else {
+    auto m = [&](const uint32_t (&v)[VX + 1], int q, bool yok) { return (yok && vx[q]) ? v[q] : 0u; };
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pred[0][i] = (m(P0, i + 1, vy1) + m(P1, i, vy1)) >> (nx >> 1);  // LR: ch0 (x), ch1 (x-1)
+      pred[1][i] = (m(P2, i + 1, vy1) + m(A3, i + 1, vy0)) >> (ny >> 1);  // UD: ch2 (y), ch3 (y-1)
+      pred[2][i] = m(P4, i + 1, vy1);                                  // C: ch4
+    }
   }
   if constexpr (!DEC) {
     uint32_t lov[VX], res[3][VX];
@@ -190,7 +254,9 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
   if (w2_env("KMP_DISABLE_WAVE", 0) || w2_env("KMP_DISABLE_FAST", 0)) return false;
-  if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0) return false;
+  if (C != 1 || pred->padding != 0) return false;
+  if (pred->kind != KMP_PRED_MEAN && !(pred->kind == KMP_PRED_LINEAR && pred->weights && pred->bias)) return false;
+  if (pred->kind == KMP_PRED_LINEAR && w2_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
   int64_t yb = 0, ye = g.E[1];
   if (region) {  // only row ranges (full width): the fused chunked drivers' merged slabs
     if (region->begin[2] > 0 || region->end[2] < g.E[2]) return false;
@@ -221,6 +287,17 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   return nblk < ((int64_t)1 << 31);
 }
 
+template <typename T, bool DEC>
+static void launch_wave2d(bool one, bool lin, dim3 grid, dim3 block, hipStream_t s, const w2::W2& a) {
+  if (one) {
+    if (lin) w2::wave2d_kernel<T, DEC, true, true><<<grid, block, 0, s>>>(a);
+    else w2::wave2d_kernel<T, DEC, true, false><<<grid, block, 0, s>>>(a);
+  } else {
+    if (lin) w2::wave2d_kernel<T, DEC, false, true><<<grid, block, 0, s>>>(a);
+    else w2::wave2d_kernel<T, DEC, false, false><<<grid, block, 0, s>>>(a);
+  }
+}
+
 template <typename T>
 int try_wave2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                       const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
@@ -234,8 +311,9 @@ int try_wave2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
-    if (a.rows == 1) w2::wave2d_kernel<T, false, true><<<grid, block, 0, stream>>>(a);
-    else w2::wave2d_kernel<T, false, false><<<grid, block, 0, stream>>>(a);
+    a.wt = pred->weights;
+    a.bias = pred->bias;
+    launch_wave2d<T, false>(a.rows == 1, pred->kind == KMP_PRED_LINEAR, grid, block, stream, a);
     return check_launch("wave2d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -255,8 +333,9 @@ int try_wave2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64
     }
     a.hi_out = hi;
     a.lo_in = lowres;
-    if (a.rows == 1) w2::wave2d_kernel<T, true, true><<<grid, block, 0, stream>>>(a);
-    else w2::wave2d_kernel<T, true, false><<<grid, block, 0, stream>>>(a);
+    a.wt = pred->weights;
+    a.bias = pred->bias;
+    launch_wave2d<T, true>(a.rows == 1, pred->kind == KMP_PRED_LINEAR, grid, block, stream, a);
     return check_launch("wave2d_decode");
   }
   return KMP_ERR_UNSUPPORTED;

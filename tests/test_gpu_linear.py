@@ -21,7 +21,10 @@ def _weights(ndim, padding, seed, dtype):
 
 CASES = [(3, 0, (2, 9, 10, 12, 1), np.uint16), (3, 1, (2, 8, 9, 7, 1), np.uint16), (3, 0, (1, 9, 8, 16, 2), np.uint8),
          (3, 0, (4, 64, 64, 64, 1), np.uint16), (2, 0, (3, 33, 20, 1), np.uint8), (2, 1, (2, 30, 31, 2), np.uint16),
-         (2, 2, (2, 17, 17, 1), np.uint8)]
+         (2, 2, (2, 17, 17, 1), np.uint8),
+         # fused 2D wave kernel (LinearPredictor p = 0): multi-row waves, odd height, one-row waves
+         (2, 0, (3, 64, 64, 1), np.uint16), (2, 0, (2, 37, 128, 1), np.uint8), (2, 0, (2, 9, 1024, 1), np.uint8),
+         (2, 0, (3, 10, 512, 1), np.uint16), (2, 0, (8, 30, 256, 1), np.uint16)]
 
 
 def _data(shape, dtype, seed):
