@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-round}
 mkdir -p $O
 step() { local name=$1; shift; timeout -k 10 "$@" > $O/$name.log 2>&1; local rc=$?; echo "[$name] rc=$rc"; return $rc; }
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q && \
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread && \
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" && \
 step bench 400 python bench.py && \
 step bench_image 300 python bench.py --workload image --no-cpu-baseline && \
