@@ -71,6 +71,9 @@ typedef struct {
 /* ---------------------------------------------------------------------------------------- */
 const char* kmp_version(void);
 const char* kmp_last_error(void);
+/* Name of the last kernel family this thread launched (e.g. "wave3d_encode", "fast3d_decode",
+   "generic_encode"): lets tests and callers see which code path served a call. */
+const char* kmp_last_launch(void);
 /* 1 if the kernels were built for the device's ISA (gfx950) and a device is visible. */
 int kmp_device_ok(void);
 

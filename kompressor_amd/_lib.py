@@ -53,6 +53,7 @@ class Region(ctypes.Structure):
 _PROTOS = {
     'kmp_version': (ctypes.c_char_p, []),
     'kmp_last_error': (ctypes.c_char_p, []),
+    'kmp_last_launch': (ctypes.c_char_p, []),
     'kmp_device_ok': (ctypes.c_int, []),
     'kmp_host_device_pointer': (ctypes.c_int, [_vp, _vpp]),
     'kmp_volume_encode': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor), _i32,

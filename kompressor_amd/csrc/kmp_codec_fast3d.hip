@@ -491,6 +491,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_wave3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
+    if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     F3 a{};
@@ -517,6 +519,8 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     int st = try_wave3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_wave3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {

@@ -12,6 +12,7 @@
 namespace kmp {
 
 static thread_local std::string g_last_error;
+static thread_local const char* g_last_launch = "";
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int status, const std::string& msg) {
@@ -19,6 +20,7 @@ int fail(int status, const std::string& msg) {
   return status;
 }
 int check_launch(const char* what) {
+  g_last_launch = what;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(KMP_ERR_LAUNCH, std::string(what) + ": " + hipGetErrorString(e));
   return KMP_OK;
@@ -340,6 +342,7 @@ extern "C" {
 
 const char* kmp_version(void) { return "kompressor_hip 0.1.0 (gfx950)"; }
 const char* kmp_last_error(void) { return g_last_error.c_str(); }
+const char* kmp_last_launch(void) { return g_last_launch; }
 
 int kmp_device_ok(void) {
   // The real requirement: this library's code object loads on the current device (gfx950).

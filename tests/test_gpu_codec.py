@@ -265,3 +265,45 @@ def test_pyramid_matches_oracle_composition(kom, ndim, shape, dtype, levels, p):
         cur = want_lo
     assert np.array_equal(lo, cur)
     assert np.array_equal(ns.decode_pyramid(pred, dec, lo, levels_out, padding=p), x)
+
+
+def _last_launch(kom):
+    return kom._lib.lib.kmp_last_launch().decode()
+
+
+@pytest.mark.parametrize('shape,dtype,p', [
+    ((8, 12, 14, 64, 1), np.uint16, 1),    # Ey = 7 < rows: idle rows read mirrored rows
+    ((8, 12, 14, 64, 1), np.uint16, 2),
+    ((2, 17, 34, 32, 1), np.uint16, 2),    # odd depth, 16 rows per wave, Ey = 17
+    ((3, 9, 40, 128, 1), np.uint16, 1),    # 16 lanes per row, 4 rows per wave
+    ((8, 10, 20, 64, 1), np.uint8, 2),     # u8: 8 outputs per lane
+    ((1, 6, 66, 16, 1), np.uint8, 1),      # one lane per row, 64 rows per wave, Ey = 33
+    ((2, 7, 5, 32, 1), np.uint16, 2),      # odd height, rows beyond the volume
+    ((1, 64, 64, 64, 1), np.uint16, 2),
+])
+@pytest.mark.parametrize('pl', [None, '1', '2'])
+def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
+    """The p = 1, 2 wave kernel (kmp_codec_wave3dp.hip) against the oracle, encode and decode, and
+    chunked (z-region) launches, at the default and both forced planes-per-workgroup; asserts the
+    kernel served the call."""
+    if pl is not None:
+        monkeypatch.setenv('KMP_W3P_PL', pl)
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = kom.volume, oracle.volume
+    enc, dec, oenc = (ns.encode_values_uint16, ns.decode_values_uint16, ons.encode_values_uint16) \
+        if dtype == np.uint16 else (ns.encode_values_uint8, ns.decode_values_uint8, ons.encode_values_uint8)
+    x = np.random.default_rng(11).integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, 3), oenc, x, padding=p)
+    pred = kom.MeanPredictor(p, 3)
+    lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
+    assert _last_launch(kom) == 'wave3dp_encode'
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
+    assert _last_launch(kom) == 'wave3dp_decode'
+    lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
+    assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
+    assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(5, 7, 9), padding=p), x)
