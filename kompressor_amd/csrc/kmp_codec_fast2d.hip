@@ -378,7 +378,9 @@ template <typename T>
 int try_fast2d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                       const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
   {  // p == 0: the barrier-free wave kernel (kmp_codec_wave2d.hip)
-    const int st = try_wave2d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
+    int st = try_wave2d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_wave2dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
@@ -402,7 +404,9 @@ template <typename T>
 int try_fast2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
                       const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
   {
-    const int st = try_wave2d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    int st = try_wave2d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_wave2dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {

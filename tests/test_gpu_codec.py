@@ -307,3 +307,37 @@ def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
     lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(5, 7, 9), padding=p), x)
+
+
+@pytest.mark.parametrize('shape,dtype,p', [
+    ((8, 256, 256, 1), np.uint8, 1),     # C2 geometry: 16 lanes per row, 4 rows per wave
+    ((8, 256, 256, 1), np.uint8, 2),     # rows (4) < 2p+2: a lane holds both halo rows
+    ((3, 33, 64, 1), np.uint8, 2),       # odd height, 16 rows per wave
+    ((2, 30, 32, 1), np.uint16, 1),
+    ((2, 31, 48, 1), np.uint16, 2),      # 6 lanes per row is not a power of two: the LDS kernel
+    ((1, 20, 256, 1), np.uint16, 1),     # 2 rows per wave
+    ((2, 9, 16, 1), np.uint8, 2),        # one lane per row, Ey = 5 < rows
+])
+def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
+    """The p = 1, 2 image wave kernel (kmp_codec_wave2dp.hip) against the oracle, whole-image and
+    row-region (chunked) launches; asserts which kernel served the call."""
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = kom.image, oracle.image
+    enc, dec, oenc = (ns.encode_values_uint16, ns.decode_values_uint16, ons.encode_values_uint16) \
+        if dtype == np.uint16 else (ns.encode_values_uint8, ns.decode_values_uint8, ons.encode_values_uint8)
+    x = np.random.default_rng(12).integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, 2), oenc, x, padding=p)
+    pred = kom.MeanPredictor(p, 2)
+    lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
+    wave = (shape[2] // 2 // (8 // np.dtype(dtype).itemsize)) in (1, 2, 4, 8, 16, 32, 64)
+    assert _last_launch(kom) == ('wave2dp_encode' if wave else 'fast2d_encode')
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
+    assert _last_launch(kom) == ('wave2dp_decode' if wave else 'fast2d_decode')
+    lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
+    assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
+    assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(7, 9), padding=p), x)
