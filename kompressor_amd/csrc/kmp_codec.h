@@ -59,10 +59,19 @@ template <typename T>
 int try_wave2dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
                        const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream);
 template <typename T>
+int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                         const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+template <typename T>
+int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                         const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+template <typename T>
 int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
-                    const MapPtrs& maps, const kmp_region* region, hipStream_t stream);
+                    const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes, hipStream_t stream);
 template <typename T>
 int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
-                    const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream);
+                    const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
+                    hipStream_t stream);
 
 }  // namespace kmp

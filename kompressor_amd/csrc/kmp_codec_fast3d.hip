@@ -484,7 +484,7 @@ static void launch_fast3d(int P, dim3 grid, dim3 block, size_t lds, hipStream_t 
 
 template <typename T>
 int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
-                    const MapPtrs& maps, const kmp_region* region, hipStream_t stream) {
+                    const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (nsp != 3) return try_fast2d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
   {  // p == 0: the barrier-free wave kernel (kmp_codec_wave3d.hip) / fused linear (kmp_codec_linear3d.hip)
     int st = try_wave3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
@@ -492,6 +492,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     st = try_linear3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
@@ -513,7 +515,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
 
 template <typename T>
 int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
-                    const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream) {
+                    const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
+                    hipStream_t stream) {
   if (nsp != 3) return try_fast2d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
   {
     int st = try_wave3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
@@ -521,6 +524,8 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
@@ -543,9 +548,9 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
 
 #define KMP_INST(T)                                                                                              \
   template int try_fast_encode<T>(int, const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,         \
-                                  const MapPtrs&, const kmp_region*, hipStream_t);                               \
+                                  const MapPtrs&, const kmp_region*, void*, size_t, hipStream_t);                \
   template int try_fast_decode<T>(int, const T*, const CMapPtrs&, const Geo&, int64_t, int64_t,                  \
-                                  const kmp_predictor*, T*, const kmp_region*, hipStream_t);
+                                  const kmp_predictor*, T*, const kmp_region*, void*, size_t, hipStream_t);
 KMP_INST(uint8_t)
 KMP_INST(uint16_t)
 KMP_INST(int32_t)

@@ -140,8 +140,15 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
 // Host side of the generic path
 // ------------------------------------------------------------------------------------------
 int64_t generic_workspace_bytes(int dtype, int nsp, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred) {
-  const int K = (pred && pred->kind == KMP_PRED_LINEAR) ? (nsp == 3 ? 19 : 5) : 1;
-  return B * g.Lc[0] * g.Lc[1] * g.Lc[2] * K * C * dtype_size(dtype);
+  const bool lin = pred && pred->kind == KMP_PRED_LINEAR;
+  const int K = lin ? (nsp == 3 ? 19 : 5) : 1;
+  int64_t need = B * g.Lc[0] * g.Lc[1] * g.Lc[2] * K * C * dtype_size(dtype);
+  if (lin && B > 0) {  // the fused LinearPredictor kernels keep a reordered copy of W [N, K] there
+    const int64_t nb = 2 * pred->padding + 2, N = nsp == 3 ? nb * nb * nb : nb * nb;
+    const int64_t wbytes = N * K * (int64_t)sizeof(float);
+    need = need > wbytes ? need : wbytes;
+  }
+  return need;
 }
 
 static Frame make_frame(int nsp, const Geo& g, const kmp_region* region) {
@@ -268,7 +275,8 @@ int codec_encode(int nsp, int dtype, const void* highres, int64_t B, const int64
   return dispatch_natural(dtype, coder, [&](auto tag, auto coder_c) {
     using T = decltype(tag);
     constexpr int CODER = decltype(coder_c)::value;
-    int st = try_fast_encode<T>(nsp, (const T*)highres, g, B, C, pred, (T*)lowres_out, maps, region, stream);
+    int st = try_fast_encode<T>(nsp, (const T*)highres, g, B, C, pred, (T*)lowres_out, maps, region, ws, ws_bytes,
+                                stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     return encode_generic_t<T, CODER>((const T*)highres, g, nsp, B, C, pred, (T*)lowres_out, maps, region, ws,
                                       ws_bytes, stream);
@@ -295,7 +303,8 @@ int codec_decode(int nsp, int dtype, const void* lowres, const void* const* maps
   return dispatch_natural(dtype, coder, [&](auto tag, auto coder_c) {
     using T = decltype(tag);
     constexpr int CODER = decltype(coder_c)::value;
-    int st = try_fast_decode<T>(nsp, (const T*)lowres, maps, g, B, C, pred, (T*)highres_out, region, stream);
+    int st = try_fast_decode<T>(nsp, (const T*)lowres, maps, g, B, C, pred, (T*)highres_out, region, ws, ws_bytes,
+                                stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     return decode_generic_t<T, CODER>((const T*)lowres, maps, g, nsp, B, C, pred, (T*)highres_out, region, ws,
                                       ws_bytes, stream);

@@ -76,6 +76,23 @@ __device__ __forceinline__ int lsrc(int r, int L, int E) {
   return m2 < E ? m2 : 2 * E - 1 - m2;
 }
 
+// lsrc for indices within one reflection of the axis (-L <= r < 2L): no integer division
+__device__ __forceinline__ int lsrc1(int r, int L, int E) {
+  int m = r < 0 ? -1 - r : r;
+  m = m >= L ? 2 * L - 1 - m : m;
+  return m >= E ? 2 * E - 1 - m : m;
+}
+
+// astype(uint8 / uint16) of an f32 (XLA: truncate toward zero, saturate, NaN -> 0):
+// v_cvt_u32_f32 truncates and saturates to [0, 2^32-1] with NaN -> 0, then clamp to the dtype
+template <typename T>
+__device__ __forceinline__ uint32_t cvt_sat(float v) {
+  uint32_t u;
+  asm volatile("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(v));
+  constexpr uint32_t hi = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  return u < hi ? u : hi;
+}
+
 __device__ __forceinline__ uint32_t shdn(uint32_t v, int d) { return (uint32_t)__shfl_down((int)v, d, 64); }
 __device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
 
