@@ -224,27 +224,40 @@ __device__ __forceinline__ T cell_mean_padded(const T* __restrict__ in, int64_t 
   return cast_f32<T>(s / (float)(kz * k * k));
 }
 
+// Two passes: (1) the per-cell means ARE the C map (volume/utils.py:117: channel 6 unscaled; 2D
+// channel 4), so they are written there once; (2) every other map aggregates up to 4 of them
+// (the f32 scatter-add / scale / truncate of volume/utils.py:83-155, kmp_aggregate.h).
 template <typename T>
-__global__ void __launch_bounds__(kThreads) mean_predict_maps_kernel(const T* __restrict__ in, int64_t B, Ext3 S,
-                                                                   int64_t C, int nsp, int p, MapPtrs outs,
-                                                                   int64_t total) {
+__global__ void __launch_bounds__(kThreads) cell_mean_map_kernel(const T* __restrict__ in, int64_t B, Ext3 S,
+                                                               int64_t C, int nsp, int p, Ext3 cells,
+                                                               T* __restrict__ out, int64_t total) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    Idx5 q = unflatten5(t, cells.e[0], cells.e[1], cells.e[2], C);
+    out[t] = cell_mean_padded<T>(in, q.b, q.i0, q.i1, q.i2, q.c, S, C, nsp, p);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T* __restrict__ cm, int64_t B,
+                                                                      Ext3 cells, int64_t C, int nsp, MapPtrs outs,
+                                                                      int64_t total) {
   const int nmaps = nsp == 3 ? 7 : 3;
-  const int64_t Lcz = nsp == 3 ? S.e[0] - 2 * p - 1 : 1, Lcy = S.e[1] - 2 * p - 1, Lcx = S.e[2] - 2 * p - 1;
+  const int64_t Lcz = cells.e[0], Lcy = cells.e[1], Lcx = cells.e[2];
   const int64_t f0 = nsp == 3 ? Lcz + 1 : 1, f1 = Lcy + 1, f2 = Lcx + 1;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     Idx5 q = unflatten5(t, f0, f1, f2, C);
     auto get = [&](int64_t z, int64_t y, int64_t x, int) -> T {
-      return cell_mean_padded<T>(in, q.b, z, y, x, q.c, S, C, nsp, p);
+      return cm[(((q.b * Lcz + z) * Lcy + y) * Lcx + x) * C + q.c];
     };
     for (int k = 0; k < nmaps; ++k) {
+      if (k == center_map(nsp)) continue;
       int par[3];
       map_parity(nsp, k, par);
       int64_t e[3];
       const int64_t idx[3] = {q.i0, q.i1, q.i2};
-      const int64_t lc[3] = {Lcz, Lcy, Lcx};
       bool ok = true;
       for (int a = 0; a < 3; ++a) {
-        e[a] = (a < 3 - nsp) ? 1 : (par[a] ? lc[a] : lc[a] + 1);
+        e[a] = (a < 3 - nsp) ? 1 : (par[a] ? cells.e[a] : cells.e[a] + 1);
         ok = ok && idx[a] < e[a];
       }
       if (!ok) continue;
@@ -494,16 +507,24 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     KMP_REQUIRE(out[k], "null map pointer");
     outs.p[k] = out[k];
   }
-  int64_t total = B * C;
-  for (int a = 3 - nsp; a < 3; ++a) {
+  int64_t total = B * C, ncell = B * C;
+  Ext3 cells{};
+  for (int a = 0; a < 3; ++a) {
+    if (a < 3 - nsp) { cells.e[a] = 1; continue; }
     KMP_REQUIRE(S.e[a] - 2 * padding - 1 >= 1, "window has no cells");
+    cells.e[a] = S.e[a] - 2 * padding - 1;
     total *= S.e[a] - 2 * padding;
+    ncell *= cells.e[a];
   }
   if (total == 0) return KMP_OK;
   return dispatch_int_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    mean_predict_maps_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
-        (const T*)padded_lowres, B, S, C, nsp, padding, outs, total);
+    T* cm = (T*)outs.p[center_map(nsp)];
+    cell_mean_map_kernel<T><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>((const T*)padded_lowres, B, S, C,
+                                                                                   nsp, padding, cells, cm, ncell);
+    if (int st = check_launch("mean_predict_maps")) return st;
+    maps_from_cell_means_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, B, cells, C, nsp, outs,
+                                                                                          total);
     return check_launch("mean_predict_maps");
   });
 }
