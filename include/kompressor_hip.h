@@ -198,6 +198,35 @@ int kmp_tiles(int32_t nsp, int32_t dtype, int32_t direction, const void* src, co
 int kmp_code(int32_t direction, int32_t coder, int32_t pred_dtype, const void* pred, int32_t x_dtype,
              const void* x, int64_t n, void* out, kmp_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Callback path: an opaque predictions_fn with a built-in coder (kmp_callback.hip).  The    */
+/* reference's steps on either side of the callback, fused; results identical to them.      */
+/* ---------------------------------------------------------------------------------------- */
+
+/* pad_neighborhood(lowres_from_highres(pad_highres(h)), p) (volume/encode_decode.py:36-48):
+   the window encode hands predictions_fn, [B, L+2p..., C], straight from the highres. */
+int kmp_window_from_highres(int32_t nsp, int32_t dtype, const void* highres, int64_t B, const int64_t shape[3],
+                            int64_t C, int32_t padding, void* window_out, kmp_stream_t stream);
+
+/* pad_neighborhood(pad_lowres(lowres, dims), p) (volume/encode_decode.py:70-76): the window
+   decode hands predictions_fn, from the trimmed lowres [B, E..., C]. */
+int kmp_window_from_lowres(int32_t nsp, int32_t dtype, const void* lowres, int64_t B, const int64_t shape[3],
+                           int64_t C, const int32_t dims[3], int32_t padding, void* window_out, kmp_stream_t stream);
+
+/* trim(lowres) and trim_maps([encode_fn(p, g) for p, g in zip(preds, maps_from_highres(
+   pad_highres(h)))]) (volume/encode_decode.py:49-56) with encode_fn the built-in coder of the
+   dtype: ``preds`` are predictions_fn's 7 (3) untrimmed maps in the sample dtype. */
+int kmp_encode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const void* highres, int64_t B,
+                                const int64_t shape[3], int64_t C, const void* const preds[7], void* lowres_out,
+                                void* const maps_out[7], kmp_stream_t stream);
+
+/* trim(highres_from_lowres_and_maps(pad_lowres(lowres), [decode_fn(p, e) for p, e in
+   zip(preds, pad_maps(maps))])) (volume/encode_decode.py:77-85), built-in decode_fn. */
+int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const void* lowres,
+                                const void* const maps[7], int64_t B, const int64_t shape[3], int64_t C,
+                                const int32_t dims[3], const void* const preds[7], void* highres_out,
+                                kmp_stream_t stream);
+
 /* Categorical rank coder utils.py:58-111: ``logits`` float32 [n, L]; x/out of ``dtype`` [n]. */
 int kmp_categorical(int32_t direction, const float* logits, int64_t n, int64_t L, int32_t dtype, const void* x,
                     void* out, kmp_stream_t stream);

@@ -82,6 +82,12 @@ _PROTOS = {
     'kmp_code': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i32, _vp, _i64, _vp, _vp]),
     'kmp_categorical': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     'kmp_tiles': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64p, _i64, _i64p, _vp, _vp]),
+    'kmp_window_from_highres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp]),
+    'kmp_window_from_lowres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32p, _i32, _vp, _vp]),
+    'kmp_encode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp, _vpp,
+                                                   _vp]),
+    'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
+                                                   _vp, _vp]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

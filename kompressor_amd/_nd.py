@@ -341,6 +341,50 @@ def fused_plan(predictions_fn, code_fn, padding, dtype, nsp, direction):
     return predictions_fn, kmp_code[0]
 
 
+def callback_coder(code_fn, dtype, direction):
+    """The built-in coder id when ``code_fn`` is the natural coder of ``dtype`` (the callback path
+    then runs the steps around an opaque predictions_fn as two fused launches), else None."""
+    if not fused_enabled():
+        return None
+    kc = getattr(code_fn, '_kmp_coder', None)
+    if kc is None or kc[1] != direction or NATURAL_CODER.get(dtype) != kc[0]:
+        return None
+    return kc[0]
+
+
+def d_window_from_highres(h, padding, nsp):
+    """pad_neighborhood(lowres_from_highres(pad_highres(h)), padding), one gather."""
+    sp = _sp(h.shape, nsp)
+    L = [(s + d + 1) // 2 for s, d in zip(sp, highres_dims(h.shape, nsp))]
+    out = dev.empty((h.shape[0], *[l + 2 * padding for l in L], *_ch(h.shape, nsp)), h.dtype)
+    if _empty_ok(h, out):
+        check(lib.kmp_window_from_highres(nsp, dev.dtype_code(h), h.data_ptr(), h.shape[0], _lib.i64x3(sp),
+                                          _C(h.shape, nsp), padding, out.data_ptr(), dev.stream()), 'window')
+    return out
+
+
+def d_window_from_lowres(lo, dims, padding, nsp):
+    """pad_neighborhood(pad_lowres(lo, dims), padding), one gather."""
+    E = _sp(lo.shape, nsp)
+    out = dev.empty((lo.shape[0], *[e + d + 2 * padding for e, d in zip(E, dims)], *_ch(lo.shape, nsp)), lo.dtype)
+    if _empty_ok(lo, out):
+        check(lib.kmp_window_from_lowres(nsp, dev.dtype_code(lo), lo.data_ptr(), lo.shape[0], _lib.i64x3(E),
+                                         _C(lo.shape, nsp), _lib.i32xn(dims), padding, out.data_ptr(), dev.stream()),
+              'window')
+    return out
+
+
+def _preds_fit(preds, dtype, B, L, ch, nsp):
+    """True when predictions_fn's maps can feed the fused coder kernels directly: contiguous
+    device tensors of the sample dtype in the untrimmed map shapes."""
+    for m, par in zip(preds, PARITY[nsp]):
+        want = (B, *[(l - 1 if p else l) for l, p in zip(L, par)], *ch)
+        if not (isinstance(m, torch.Tensor) and m.is_cuda and m.dtype == dtype and m.is_contiguous()
+                and tuple(m.shape) == want):
+            return False
+    return True
+
+
 def _workspace(nbytes):
     return dev.empty((max(int(nbytes), 1),), torch.uint8)
 
@@ -483,11 +527,28 @@ def encode(predictions_fn, encode_fn, highres, padding, nsp):
         fused_encode_into(h, predictor, coder, lowres, maps, nsp)
         encoded = tuple(maps)
     else:
+        coder = callback_coder(encode_fn, h.dtype, _lib.ENCODE)
+        L = [(s + d + 1) // 2 for s, d in zip(_sp(h.shape, nsp), dims)]
+        if coder is not None:
+            # the callback path with a built-in coder: window gather, predictions_fn, one coder launch
+            validate_lowres_shape((h.shape[0], *L, *_ch(h.shape, nsp)), nsp)
+            pred_maps = _callback_maps(predictions_fn(d_window_from_highres(h, padding, nsp)), nsp)
+            if _preds_fit(pred_maps, h.dtype, h.shape[0], L, _ch(h.shape, nsp), nsp):
+                lowres, encoded, dims = _alloc_encoded(h, coder, nsp)
+                check(lib.kmp_encode_with_predictions(nsp, dev.dtype_code(h), coder, h.data_ptr(), h.shape[0],
+                                                      _lib.i64x3(_sp(h.shape, nsp)), _C(h.shape, nsp),
+                                                      _lib.ptrs(pred_maps), lowres.data_ptr(), _lib.ptrs(encoded),
+                                                      dev.stream()), 'encode_with_predictions')
+                return (dev.from_device(lowres, kind),
+                        (tuple(dev.from_device(m, kind) for m in encoded), tuple(dims)))
+        else:
+            pred_maps = None
         hp, dims = d_pad_highres(h, nsp)
         lowres = d_lowres_from_highres(hp, nsp)
         validate_lowres_shape(lowres.shape, nsp)
         gt_maps = d_maps_from_highres(hp, nsp)
-        pred_maps = _callback_maps(predictions_fn(d_pad_neighborhood(lowres, padding, nsp)), nsp)
+        if pred_maps is None:
+            pred_maps = _callback_maps(predictions_fn(d_pad_neighborhood(lowres, padding, nsp)), nsp)
         encoded = [_dev(encode_fn(p, g)) for p, g in zip(pred_maps, gt_maps)]
         encoded = d_trim_maps(encoded, dims, nsp)
         lowres = d_trim(lowres, dims, nsp)
@@ -509,9 +570,25 @@ def decode(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
                          *_ch(lo.shape, nsp)), lo.dtype)
         fused_decode_into(lo, maps, dims, predictor, coder, out, nsp)
         return dev.from_device(out, kind)
+    coder = callback_coder(decode_fn, lo.dtype, _lib.DECODE)
+    pred_maps = None
+    if coder is not None and all(m.dtype == CODER_DTYPE[coder] and m.is_contiguous() for m in maps):
+        # the callback path with a built-in coder: window gather, predictions_fn, one coder launch
+        _check_encoded_maps(lo, maps, dims, nsp)
+        L = [e + d for e, d in zip(_sp(lo.shape, nsp), dims)]
+        pred_maps = _callback_maps(predictions_fn(d_window_from_lowres(lo, dims, padding, nsp)), nsp)
+        if _preds_fit(pred_maps, lo.dtype, lo.shape[0], L, _ch(lo.shape, nsp), nsp):
+            lo = lo.contiguous()
+            out = dev.empty((lo.shape[0], *[2 * l - 1 - d for l, d in zip(L, dims)], *_ch(lo.shape, nsp)), lo.dtype)
+            check(lib.kmp_decode_with_predictions(nsp, dev.dtype_code(lo), coder, lo.data_ptr(), _lib.ptrs(maps),
+                                                  lo.shape[0], _lib.i64x3(_sp(lo.shape, nsp)), _C(lo.shape, nsp),
+                                                  _lib.i32xn(dims), _lib.ptrs(pred_maps), out.data_ptr(),
+                                                  dev.stream()), 'decode_with_predictions')
+            return dev.from_device(out, kind)
     lo_p = d_pad_lowres(lo, dims, nsp)
     maps_p = d_pad_maps(maps, dims, nsp)
-    pred_maps = _callback_maps(predictions_fn(d_pad_neighborhood(lo_p, padding, nsp)), nsp)
+    if pred_maps is None:
+        pred_maps = _callback_maps(predictions_fn(d_pad_neighborhood(lo_p, padding, nsp)), nsp)
     decoded = [_dev(decode_fn(p, e)) for p, e in zip(pred_maps, maps_p)]
     hi = d_highres_from_lowres_and_maps(lo_p, decoded, nsp)
     return dev.from_device(d_trim(hi, dims, nsp), kind)

@@ -1,0 +1,303 @@
+// kmp_callback.hip -- the reference's step sequence around an OPAQUE predictions_fn, fused on
+// either side of the callback when the coder is a built-in one (utils.py:38-55 for the sample
+// dtype).  A user's predictor (a network, any callable) keeps its exact contract -- it is called
+// once with the reference's padded lowres window and returns the 7 (2D: 3) untrimmed prediction
+// maps -- while the reference's other steps collapse into two launches per direction:
+//
+//   encode (volume/encode_decode.py:30-56):
+//     kmp_window_from_highres      pad_neighborhood(lowres_from_highres(pad_highres(h)), p)
+//     predictions_fn(window)       (caller)
+//     kmp_encode_with_predictions  trim(lowres), trim_maps([encode_fn(p, g) for p, g in
+//                                  zip(preds, maps_from_highres(pad_highres(h)))])
+//   decode (volume/encode_decode.py:59-85):
+//     kmp_window_from_lowres       pad_neighborhood(pad_lowres(lowres, dims), p)
+//     predictions_fn(window)       (caller)
+//     kmp_decode_with_predictions  trim(highres_from_lowres_and_maps(pad_lowres(lowres),
+//                                  [decode_fn(p, e) for p, e in zip(preds, pad_maps(maps))]))
+//
+// Every element the trims keep lies inside the unpadded arrays (an output block o < E reads
+// highres 2o + parity < n), so the coder kernels need no mirroring at all: the pads only ever
+// produce entries the trims drop.  The window is a gather through the composed mirror maps
+// (even reflect pad, then the symmetric neighbourhood pad).
+#include "kmp_codec.h"
+
+namespace kmp {
+namespace cb {
+
+constexpr int kThreads = 256;
+
+static inline unsigned grid_for(int64_t n) {
+  int64_t g = ceil_div(n, kThreads);
+  return (unsigned)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+// window[b, j, c] = src[b, mult * sym(sym(j - p, L), E), c] per spatial axis (mult 2: highres,
+// 1: trimmed lowres); W = L + 2p, unused leading axis has extent 1.
+template <typename T>
+__global__ void __launch_bounds__(kThreads) window_kernel(const T* __restrict__ src, int64_t B, Geo g, int64_t S0,
+                                                        int64_t S1, int64_t S2, int mult, int nsp, int p, int64_t C,
+                                                        int64_t W0, int64_t W1, int64_t W2, T* __restrict__ out,
+                                                        int64_t total) {
+  const int pz = nsp == 3 ? p : 0;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b, jz, jy, jx, c;
+    unflat5(t, W0, W1, W2, C, b, jz, jy, jx, c);
+    const int64_t z = mult * sym_index(sym_index(jz - pz, g.L[0]), g.E[0]);
+    const int64_t y = mult * sym_index(sym_index(jy - p, g.L[1]), g.E[1]);
+    const int64_t x = mult * sym_index(sym_index(jx - p, g.L[2]), g.E[2]);
+    out[t] = src[(((b * S0 + z) * S1 + y) * S2 + x) * C + c];
+  }
+}
+
+// Untrimmed (prediction) and trimmed (coded) extents of map k.
+__device__ __forceinline__ void map_ext(const Geo& g, int nsp, int k, int64_t (&u)[3], int64_t (&e)[3]) {
+  int par[3];
+  map_parity(nsp, k, par);
+  for (int a = 0; a < 3; ++a) {
+    if (a < 3 - nsp) { u[a] = e[a] = 1; continue; }
+    u[a] = par[a] ? g.Lc[a] : g.L[a];
+    e[a] = par[a] ? g.Lc[a] : g.E[a];
+  }
+}
+
+// Per-map extents, precomputed on the host: untrimmed (prediction) u and trimmed (coded) e.
+struct MapExt {
+  int32_t u[7][3], e[7][3];
+  int32_t par[7][3];
+};
+
+static MapExt map_exts(const Geo& g, int nsp) {
+  MapExt m{};
+  for (int k = 0; k < (nsp == 3 ? 7 : 3); ++k) {
+    int par[3];
+    map_parity(nsp, k, par);
+    for (int a = 0; a < 3; ++a) {
+      m.par[k][a] = par[a];
+      if (a < 3 - nsp) { m.u[k][a] = m.e[k][a] = 1; continue; }
+      m.u[k][a] = (int32_t)(par[a] ? g.Lc[a] : g.L[a]);
+      m.e[k][a] = (int32_t)(par[a] ? g.Lc[a] : g.E[a]);
+    }
+  }
+  return m;
+}
+
+// 32-bit index versions (every array below 2^31 elements), C == 1: one output block per thread,
+// x fastest, the 2^d highres block addressed from one base.
+template <typename T, int CODER, bool DEC, int NM>
+__global__ void __launch_bounds__(kThreads) code_preds_kernel32(const T* __restrict__ src, CMapPtrs maps_in,
+                                                              MapPtrs maps_out, CMapPtrs preds, T* __restrict__ dst,
+                                                              MapExt me, int32_t n0, int32_t n1, int32_t n2,
+                                                              int32_t E0, int32_t E1, int32_t E2, int32_t total) {
+  using TO = typename coder_out<CODER>::type;
+  for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    uint32_t q = (uint32_t)t;
+    const int32_t ox = q % (uint32_t)E2; q /= (uint32_t)E2;
+    const int32_t oy = q % (uint32_t)E1; q /= (uint32_t)E1;
+    const int32_t oz = q % (uint32_t)E0;
+    const int32_t b = q / (uint32_t)E0;
+    const int32_t hbase = ((b * n0 + 2 * oz) * n1 + 2 * oy) * n2 + 2 * ox;
+    if constexpr (DEC) dst[hbase] = src[t];
+    else dst[t] = src[hbase];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const int32_t* e = me.e[k];
+      if (oz >= e[0] || oy >= e[1] || ox >= e[2]) continue;
+      const int32_t* u = me.u[k];
+      const int32_t* par = me.par[k];
+      const int32_t hidx = hbase + (par[0] * n1 + par[1]) * n2 + par[2];
+      const T pred = ((const T*)preds.p[k])[((b * u[0] + oz) * u[1] + oy) * u[2] + ox];
+      const int32_t midx = ((b * e[0] + oz) * e[1] + oy) * e[2] + ox;
+      if constexpr (DEC) {
+        const TO enc = ((const TO*)maps_in.p[k])[midx];
+        dst[hidx] = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
+      } else {
+        ((TO*)maps_out.p[k])[midx] = code_encode<CODER>(to_i32(pred), to_i32(src[hidx]));
+      }
+    }
+  }
+}
+
+template <typename T, int CODER>
+__global__ void __launch_bounds__(kThreads) encode_preds_kernel(const T* __restrict__ hi, Geo g, int nsp, int64_t C,
+                                                              CMapPtrs preds, T* __restrict__ lowres, MapPtrs maps,
+                                                              int64_t total) {
+  using TO = typename coder_out<CODER>::type;
+  const int nmaps = nsp == 3 ? 7 : 3;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b, oz, oy, ox, c;
+    unflat5(t, g.E[0], g.E[1], g.E[2], C, b, oz, oy, ox, c);
+    auto hv = [&](int pz, int py, int px) -> T {
+      return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
+    };
+    lowres[t] = hv(0, 0, 0);
+    for (int k = 0; k < nmaps; ++k) {
+      int par[3];
+      map_parity(nsp, k, par);
+      int64_t u[3], e[3];
+      map_ext(g, nsp, k, u, e);
+      if (oz >= e[0] || oy >= e[1] || ox >= e[2]) continue;
+      const T pred = ((const T*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
+      ((TO*)maps.p[k])[(((b * e[0] + oz) * e[1] + oy) * e[2] + ox) * C + c] =
+          code_encode<CODER>(to_i32(pred), to_i32(hv(par[0], par[1], par[2])));
+    }
+  }
+}
+
+template <typename T, int CODER>
+__global__ void __launch_bounds__(kThreads) decode_preds_kernel(const T* __restrict__ lowres, CMapPtrs maps, Geo g,
+                                                              int nsp, int64_t C, CMapPtrs preds, T* __restrict__ hi,
+                                                              int64_t total) {
+  using TO = typename coder_out<CODER>::type;
+  const int nmaps = nsp == 3 ? 7 : 3;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b, oz, oy, ox, c;
+    unflat5(t, g.E[0], g.E[1], g.E[2], C, b, oz, oy, ox, c);
+    auto hout = [&](int pz, int py, int px) -> T& {
+      return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
+    };
+    hout(0, 0, 0) = lowres[t];
+    for (int k = 0; k < nmaps; ++k) {
+      int par[3];
+      map_parity(nsp, k, par);
+      int64_t u[3], e[3];
+      map_ext(g, nsp, k, u, e);
+      if (oz >= e[0] || oy >= e[1] || ox >= e[2]) continue;
+      const T pred = ((const T*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
+      const TO enc = ((const TO*)maps.p[k])[(((b * e[0] + oz) * e[1] + oy) * e[2] + ox) * C + c];
+      hout(par[0], par[1], par[2]) = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
+    }
+  }
+}
+
+template <typename F>
+static int dispatch_coder(int dtype, int coder, F&& f) {  // the built-in coder of each sample dtype
+  if (dtype == KMP_U8 && coder == KMP_CODER_U8) return f(uint8_t{}, std::integral_constant<int, KMP_CODER_U8>{});
+  if (dtype == KMP_U16 && coder == KMP_CODER_U16) return f(uint16_t{}, std::integral_constant<int, KMP_CODER_U16>{});
+  if (dtype == KMP_I32 && coder == KMP_CODER_RAW) return f(int32_t{}, std::integral_constant<int, KMP_CODER_RAW>{});
+  if (dtype == KMP_U32 && coder == KMP_CODER_U32) return f(uint32_t{}, std::integral_constant<int, KMP_CODER_U32>{});
+  return fail(KMP_ERR_UNSUPPORTED, "callback coder kernels support (uint8, U8), (uint16, U16), (int32, RAW), "
+                                   "(uint32, U32); got dtype " + std::to_string(dtype) + " coder " + std::to_string(coder));
+}
+
+static int window_launch(int nsp, int dtype, const void* src, int mult, const int64_t* S, int64_t B, int64_t C,
+                         const Geo& g, int p, void* out, hipStream_t stream) {
+  int64_t W[3], total = B * C;
+  for (int a = 0; a < 3; ++a) {
+    W[a] = a < 3 - nsp ? 1 : g.L[a] + 2 * p;
+    total *= W[a];
+  }
+  if (total == 0) return KMP_OK;
+  return dispatch_any_dtype(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    window_kernel<T><<<grid_for(total), kThreads, 0, stream>>>((const T*)src, B, g, S[0], S[1], S[2], mult, nsp, p, C,
+                                                               W[0], W[1], W[2], (T*)out, total);
+    return check_launch("window");
+  });
+}
+
+}  // namespace cb
+}  // namespace kmp
+
+using namespace kmp;
+
+extern "C" {
+
+int kmp_window_from_highres(int32_t nsp, int32_t dtype, const void* highres, int64_t B, const int64_t shape[3],
+                            int64_t C, int32_t padding, void* window_out, kmp_stream_t stream) {
+  KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
+  KMP_REQUIRE(highres && window_out && shape && padding >= 0 && B >= 0 && C >= 1, "bad argument");
+  for (int a = 0; a < nsp; ++a) KMP_REQUIRE(shape[a] >= 2, "spatial dims must be >= 2");
+  const Geo g = make_geo_from_highres(nsp, shape);
+  int64_t S[3];
+  for (int a = 0; a < 3; ++a) S[a] = g.n[a];
+  return cb::window_launch(nsp, dtype, highres, 2, S, B, C, g, padding, window_out, (hipStream_t)stream);
+}
+
+int kmp_window_from_lowres(int32_t nsp, int32_t dtype, const void* lowres, int64_t B, const int64_t shape[3],
+                           int64_t C, const int32_t dims[3], int32_t padding, void* window_out, kmp_stream_t stream) {
+  KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
+  KMP_REQUIRE(lowres && window_out && shape && dims && padding >= 0 && B >= 0 && C >= 1, "bad argument");
+  for (int a = 0; a < nsp; ++a) {
+    KMP_REQUIRE(dims[a] == 0 || dims[a] == 1, "dims must be 0 or 1");
+    KMP_REQUIRE(shape[a] >= 1 && shape[a] + dims[a] >= 2, "lowres too small");
+  }
+  const Geo g = make_geo_from_lowres(nsp, shape, dims);
+  int64_t S[3];
+  for (int a = 0; a < 3; ++a) S[a] = g.E[a];
+  return cb::window_launch(nsp, dtype, lowres, 1, S, B, C, g, padding, window_out, (hipStream_t)stream);
+}
+
+int kmp_encode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const void* highres, int64_t B,
+                                const int64_t shape[3], int64_t C, const void* const preds[7], void* lowres_out,
+                                void* const maps_out[7], kmp_stream_t stream) {
+  KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
+  KMP_REQUIRE(highres && shape && preds && lowres_out && maps_out && B >= 0 && C >= 1, "bad argument");
+  for (int a = 0; a < nsp; ++a) KMP_REQUIRE(shape[a] >= 2, "spatial dims must be >= 2");
+  const Geo g = make_geo_from_highres(nsp, shape);
+  CMapPtrs pp{};
+  MapPtrs mp{};
+  for (int k = 0; k < (nsp == 3 ? 7 : 3); ++k) {
+    KMP_REQUIRE(preds[k] && maps_out[k], "null map pointer");
+    pp.p[k] = preds[k];
+    mp.p[k] = maps_out[k];
+  }
+  const int64_t total = B * g.E[0] * g.E[1] * g.E[2] * C;
+  if (total == 0) return KMP_OK;
+  const bool small = C == 1 && B * g.n[0] * g.n[1] * g.n[2] < ((int64_t)1 << 31) &&
+                     B * g.L[0] * g.L[1] * g.L[2] < ((int64_t)1 << 31);
+  return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
+    using T = decltype(tag);
+    constexpr int CODER = decltype(coder_c)::value;
+    if (small) {
+      const cb::MapExt me = cb::map_exts(g, nsp);
+      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, false, 7> : cb::code_preds_kernel32<T, CODER, false, 3>;
+      k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)highres, CMapPtrs{}, mp, pp, (T*)lowres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
+          (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)total);
+    } else {
+      cb::encode_preds_kernel<T, CODER><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)highres, g, nsp, C, pp, (T*)lowres_out, mp, total);
+    }
+    return check_launch("encode_with_predictions");
+  });
+}
+
+int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const void* lowres,
+                                const void* const maps[7], int64_t B, const int64_t shape[3], int64_t C,
+                                const int32_t dims[3], const void* const preds[7], void* highres_out,
+                                kmp_stream_t stream) {
+  KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
+  KMP_REQUIRE(lowres && maps && shape && dims && preds && highres_out && B >= 0 && C >= 1, "bad argument");
+  for (int a = 0; a < nsp; ++a) {
+    KMP_REQUIRE(dims[a] == 0 || dims[a] == 1, "dims must be 0 or 1");
+    KMP_REQUIRE(shape[a] >= 1 && shape[a] + dims[a] >= 2, "lowres too small");
+  }
+  const Geo g = make_geo_from_lowres(nsp, shape, dims);
+  CMapPtrs pp{}, mp{};
+  for (int k = 0; k < (nsp == 3 ? 7 : 3); ++k) {
+    KMP_REQUIRE(preds[k] && maps[k], "null map pointer");
+    pp.p[k] = preds[k];
+    mp.p[k] = maps[k];
+  }
+  const int64_t total = B * g.E[0] * g.E[1] * g.E[2] * C;
+  if (total == 0) return KMP_OK;
+  const bool small = C == 1 && B * g.n[0] * g.n[1] * g.n[2] < ((int64_t)1 << 31) &&
+                     B * g.L[0] * g.L[1] * g.L[2] < ((int64_t)1 << 31);
+  return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
+    using T = decltype(tag);
+    constexpr int CODER = decltype(coder_c)::value;
+    if (small) {
+      const cb::MapExt me = cb::map_exts(g, nsp);
+      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, true, 7> : cb::code_preds_kernel32<T, CODER, true, 3>;
+      k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)lowres, mp, MapPtrs{}, pp, (T*)highres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
+          (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)total);
+    } else {
+      cb::decode_preds_kernel<T, CODER><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)lowres, mp, g, nsp, C, pp, (T*)highres_out, total);
+    }
+    return check_launch("decode_with_predictions");
+  });
+}
+
+}  // extern "C"

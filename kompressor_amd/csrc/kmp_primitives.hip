@@ -237,6 +237,44 @@ __global__ void __launch_bounds__(kThreads) cell_mean_map_kernel(const T* __rest
   }
 }
 
+// u8 / u16, C == 1, 32-bit indices: the f32 sum of at most 4 cell means is exact there, so the
+// scale-and-truncate is an integer shift (the same values as aggregate_map).
+template <typename T, int NSP>
+__global__ void __launch_bounds__(kThreads) maps_from_cell_means_int_kernel(const T* __restrict__ cm, int32_t Lcz,
+                                                                          int32_t Lcy, int32_t Lcx, MapPtrs outs,
+                                                                          int32_t total) {
+  constexpr int NM = NSP == 3 ? 7 : 3;
+  const int32_t f0 = NSP == 3 ? Lcz + 1 : 1, f1 = Lcy + 1, f2 = Lcx + 1;
+  for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    uint32_t q = (uint32_t)t;
+    const int32_t ox = q % (uint32_t)f2; q /= (uint32_t)f2;
+    const int32_t oy = q % (uint32_t)f1; q /= (uint32_t)f1;
+    const int32_t oz = q % (uint32_t)f0;
+    const int32_t b = q / (uint32_t)f0;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      if (k == center_map(NSP)) continue;
+      int par[3];
+      map_parity(NSP, k, par);
+      const int32_t e0 = NSP == 3 ? (par[0] ? Lcz : Lcz + 1) : 1, e1 = par[1] ? Lcy : Lcy + 1, e2 = par[2] ? Lcx : Lcx + 1;
+      if (oz >= e0 || oy >= e1 || ox >= e2) continue;
+      Contrib c[4];
+      const int nc = map_contribs(NSP, k, c);
+      uint32_t s = 0, cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i >= nc) break;
+        const int32_t z = oz - c[i].dz, y = oy - c[i].dy, x = ox - c[i].dx;
+        if (z >= 0 && z < (NSP == 3 ? Lcz : 1) && y >= 0 && y < Lcy && x >= 0 && x < Lcx) {
+          s += cm[((b * (NSP == 3 ? Lcz : 1) + z) * Lcy + y) * Lcx + x];
+          ++cnt;
+        }
+      }
+      ((T*)outs.p[k])[((b * e0 + oz) * e1 + oy) * e2 + ox] = (T)(s >> (cnt >> 1));
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T* __restrict__ cm, int64_t B,
                                                                       Ext3 cells, int64_t C, int nsp, MapPtrs outs,
@@ -523,8 +561,14 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     cell_mean_map_kernel<T><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>((const T*)padded_lowres, B, S, C,
                                                                                    nsp, padding, cells, cm, ncell);
     if (int st = check_launch("mean_predict_maps")) return st;
-    maps_from_cell_means_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, B, cells, C, nsp, outs,
-                                                                                          total);
+    if ((std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) && C == 1 && total < ((int64_t)1 << 31)) {
+      auto k = nsp == 3 ? maps_from_cell_means_int_kernel<T, 3> : maps_from_cell_means_int_kernel<T, 2>;
+      k<<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, (int32_t)cells.e[0], (int32_t)cells.e[1],
+                                                              (int32_t)cells.e[2], outs, (int32_t)total);
+    } else {
+      maps_from_cell_means_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, B, cells, C, nsp, outs,
+                                                                                            total);
+    }
     return check_launch("mean_predict_maps");
   });
 }

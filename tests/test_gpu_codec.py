@@ -59,19 +59,50 @@ def test_fused_codec_matches_golden(kom, name, kernel_mode):
 
 
 @pytest.mark.parametrize('name', [n for n in CODEC_CASES if 'tile64' not in n and 'tile256' not in n])
-def test_callback_path_matches_golden(kom, name):
-    """Generic path: the predictor is an opaque callable (no fused kernel), exactly the
-    reference's step sequence on HIP primitives."""
+@pytest.mark.parametrize('coders', ['builtin', 'opaque'])
+def test_callback_path_matches_golden(kom, name, coders):
+    """Callback path: the predictor is an opaque callable (no fused kernel).  With the built-in
+    coder the steps around it run as the fused window / coder kernels (kmp_callback.hip); with an
+    opaque coder too, exactly the reference's step sequence on HIP primitives."""
     g = load_golden(name)
     ndim, p = int(g['ndim']), int(g['padding'])
     ns = _ns(kom, ndim)
     enc, dec = _coders(ns, g['coder'])
+    if coders == 'opaque':
+        enc0, dec0 = enc, dec
+        enc = lambda a, b: enc0(a, b)  # noqa: E731
+        dec = lambda a, b: dec0(a, b)  # noqa: E731
     mean = kom.MeanPredictor(p, ndim)
     opaque = lambda lowres: mean(lowres)  # noqa: E731
     lowres, (maps, dims) = ns.encode(opaque, enc, g['highres'], padding=p)
+    last = kom._lib.lib.kmp_last_launch().decode()
+    assert (last == 'encode_with_predictions') == (coders == 'builtin'), last
     _assert_encoded(g, lowres, maps, dims, ndim)
     rec = ns.decode(opaque, dec, lowres, (maps, dims), padding=p)
     assert np.array_equal(rec, g['highres'])
+
+
+@pytest.mark.parametrize('name', ['vol_rand_mixed_p1', 'img_rand_p2', 'vol_ramp_odd_p0', 'img_ramp_even_p1'])
+def test_callback_window_is_the_reference_window(kom, name):
+    """predictions_fn receives exactly pad_neighborhood(lowres_from_highres(pad_highres(h)), p) on
+    encode and pad_neighborhood(pad_lowres(lowres, dims), p) on decode (the fused windows)."""
+    import oracle
+    g = load_golden(name)
+    ndim, p = int(g['ndim']), int(g['padding'])
+    ns, ons = _ns(kom, ndim), (oracle.volume if ndim == 3 else oracle.image)
+    enc, dec = _coders(ns, g['coder'])
+    mean = kom.MeanPredictor(p, ndim)
+    seen = []
+
+    def fn(window):
+        seen.append(window.cpu().numpy())
+        return mean(window)
+
+    lowres, (maps, dims) = ns.encode(fn, enc, torch.from_numpy(g['highres']).cuda(), padding=p)
+    hp, _ = ons.pad_highres(g['highres'])
+    assert np.array_equal(seen[0], ons.pad_neighborhood(ons.lowres_from_highres(hp), p))
+    ns.decode(fn, dec, lowres, (maps, dims), padding=p)
+    assert np.array_equal(seen[1], ons.pad_neighborhood(ons.pad_lowres(g['lowres'], tuple(g['dims'])), p))
 
 
 def reference_style_predictions_fn(kom, padding, ndim):

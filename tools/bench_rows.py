@@ -152,7 +152,8 @@ def main():
         emit('volume_chunks:encode', 'encode_chunks chunk=32, fused region launches', 2 * raw_v, te)
         emit('volume_chunks:decode', 'decode_chunks chunk=32, fused region launches', 2 * raw_v, td)
 
-    # the reference-style callback path: a plain predictions_fn + coder, primitive kernels only
+    # the callback path: an opaque predictions_fn (here the mean predictor's primitive) with the
+    # built-in coder -- window gather, predictions_fn, one fused coder launch (kmp_callback.hip)
     if not want or 'volume_callback' in want:
         pred = kom.MeanPredictor(0, 3)
         cb = lambda lowres: pred(lowres)  # noqa: E731  (not recognised as fused: the reference's step sequence)
@@ -160,8 +161,8 @@ def main():
         lo, (maps, dims) = V.encode(cb, V.encode_values_uint16, sub)
         te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), 3)
         td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), 3)
-        emit('volume_callback:encode', 'callback encode (pad, gathers, predictor, 7 coders, trims)', sub.numel() * 4, te)
-        emit('volume_callback:decode', 'callback decode (pads, predictor, 7 coders, scatter, trim)', sub.numel() * 4, td)
+        emit('volume_callback:encode', 'callback encode (window, opaque predictions_fn, fused coder + trims)', sub.numel() * 4, te)
+        emit('volume_callback:decode', 'callback decode (window, opaque predictions_fn, fused coder + interleave)', sub.numel() * 4, td)
 
     # categorical rank coder (utils.py:58-111): 1M elements x 256 float32 logits
     if not want or 'categorical' in want:
