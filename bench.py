@@ -33,10 +33,9 @@ WORKLOADS = {
                   metric='encode+decode GB/s/GPU (device-resident), 1024 x 256² uint8 image tiles',
                   name='1024 uint8 images of 256^2 (BASELINE config C2)'),
     # C5: 2048^3 float32 = 4096 chunks of 128^3 over 8 GPUs -> 512 chunks (4 GiB) per GPU,
-    # host-resident (pinned), streamed H2D -> kernel -> D2H
+    # host-resident (pinned): the fused kernels read / write the pinned host arrays over the link
     'stream': dict(ndim=3, shape=(512, 128, 128, 128, 1), dtype=np.float32,
-                   metric='encode+decode GB/s/GPU (pinned host -> GPU -> host, H2D/kernel/D2H overlapped), '
-                          '2048³ float32 as 128³ chunks',
+                   metric='encode+decode GB/s/GPU (pinned host -> GPU -> host), 2048³ float32 as 128³ chunks',
                    name='2048^3 float32 streamed as 128^3 chunks, 512 chunks per GPU (BASELINE config C5)'),
 }
 
@@ -97,7 +96,7 @@ def cpu_baseline(spec, host, padding, ntiles):
 
 def e2e_leg(kom, host, predictor, ndim, chunk, reps=3):
     """Host-resident rate: pinned host tiles in, pinned host outputs out, per direction
-    (kompressor_amd.stream.TileStream: zero-copy fused kernels for 8/16-bit samples, else a
+    (kompressor_amd.stream.TileStream: zero-copy fused kernels by default, KMP_STREAM_COPY=1 a
     3-stream H2D / kernel / D2H pipeline).  Median of ``reps`` after one warm-up."""
     src = kom.stream.pinned(host.shape, torch.from_numpy(host[:0]).dtype)
     src.copy_(torch.from_numpy(host))
@@ -397,8 +396,8 @@ def main_stream(args):
         elapsed, t_enc, t_dec = tt.tolist()
     raw = src.numel() * 4
 
-    # kernel roofline of the same codec device-resident (the uint32 path: cell-mean + residual
-    # launches of kmp_codec_generic.hip) on a 64-chunk slice
+    # kernel roofline of the same codec device-resident (the uint32 one-pass kernel,
+    # kmp_codec_wave3d32.hip) on a 64-chunk slice
     k = min(64, n)
     d_hi = src[:k].cuda().view(torch.uint32)
     coder = _nd.NATURAL_CODER[torch.uint32]
@@ -407,7 +406,10 @@ def main_stream(args):
     ws = torch.empty(max(1, _nd.workspace_bytes(d_hi, predictor, 3)), dtype=torch.uint8, device='cuda')
     enc = lambda: _nd.fused_encode_into(d_hi, predictor, coder, d_lo, d_maps, 3, workspace=ws)  # noqa: E731
     dec = lambda: _nd.fused_decode_into(d_lo, d_maps, d_dims, predictor, coder, d_rec, 3, workspace=ws)  # noqa: E731
-    enc(), dec()
+    enc()
+    kname_enc = kom._lib.lib.kmp_last_launch().decode()
+    dec()
+    kname_dec = kom._lib.lib.kmp_last_launch().decode()
     k_enc, k_dec = direction_times(enc, dec, 5, None)
     assert torch.equal(d_rec, d_hi)
     kraw = d_hi.numel() * 4
@@ -434,10 +436,12 @@ def main_stream(args):
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'u32 (float32 bit-cast)', 'data': 'synthetic (standard normal float32)',
             'config': {'workload': spec['name'], 'global_batch': n * world, 'tile': list(chunk_shape[:3]),
-                       'predictor': f'MeanPredictor(padding={args.padding})', 'streams': 3, 'chunk_per_copy': 1,
+                       'predictor': f'MeanPredictor(padding={args.padding})',
+                       'mode': 'zero-copy (one fused launch per direction reads / writes pinned host memory)'
+                               if ts.zero_copy else 'copy pipeline (3 streams, 1 chunk per copy)',
                        'parallelism': f'chunks sharded, dp{world}' if world > 1 else 'single GPU'},
             'ms_encode': round(t_enc / args.steps * 1e3, 3), 'ms_decode': round(t_dec / args.steps * 1e3, 3),
-            'roofline': {'bound': 'hbm', 'kernel': f'generic u32 {dominant} (cell_mean + residual launches)',
+            'roofline': {'bound': 'hbm', 'kernel': kname_enc if dominant == 'encode' else kname_dec,
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
                          'algorithmic_bytes_per_launch': 2 * kraw,

@@ -88,7 +88,7 @@ __device__ __forceinline__ int lsrc1(int r, int L, int E) {
 template <typename T>
 __device__ __forceinline__ uint32_t cvt_sat(float v) {
   uint32_t u;
-  asm volatile("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(v));
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(v));
   constexpr uint32_t hi = sizeof(T) == 2 ? 0xffffu : 0xffu;
   return u < hi ? u : hi;
 }

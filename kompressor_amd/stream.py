@@ -18,13 +18,16 @@ GPU's address space (``kmp_host_device_pointer``), so ONE fused launch reads the
 writes the host outputs over the link itself -- reads and writes interleave, using both link
 directions at once, with no staging buffers and no per-map DMA descriptors (8 outputs per chunk
 made the copy pipeline descriptor-bound: 16.4 GB/s vs 20.1 GB/s end to end at C3 on MI355X,
-``profiles/round1/h2d_probe.log``).  32-bit samples keep the copy pipeline: their generic
-two-pass kernels would read the input across the link twice.
+``profiles/round1/h2d_probe.log``).  32-bit samples (float32 bit-cast to uint32, int32) have a
+one-pass kernel too (``kmp_codec_wave3d32.hip``) and stream zero-copy as well; ``zero_copy=False``
+(or ``KMP_STREAM_COPY=1``) selects the copy pipeline.
 
 float32 data (config C5) is coded losslessly by bit-casting to uint32 and using the mod-2^32
 coder (``encode_values_uint32``), a build extension: the reference has no lossless float coder
 (``encode_values_raw`` truncates through ``int32``, ``utils.py:28-30``).
 """
+
+import os
 
 import torch
 
@@ -53,7 +56,9 @@ class TileStream:
     def __init__(self, predictor, tile_shape, dtype, chunk, slots=3, ndim=3, zero_copy=None):
         dev.require_gpu()
         self.ndim = ndim
-        self.zero_copy = (dtype in (torch.uint8, torch.uint16)) if zero_copy is None else bool(zero_copy)
+        if zero_copy is None:
+            zero_copy = os.environ.get('KMP_STREAM_COPY', '0') == '0'
+        self.zero_copy = bool(zero_copy)
         self.predictor = predictor
         self.chunk = int(chunk)
         self.slots = int(slots)

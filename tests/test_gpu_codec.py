@@ -372,3 +372,39 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
     lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(7, 9), padding=p), x)
+
+
+@pytest.mark.parametrize('shape,dtype', [
+    ((4, 16, 16, 16, 1), np.uint32),
+    ((8, 9, 10, 32, 1), np.uint32),        # odd depth, 8 rows per wave
+    ((1, 24, 28, 128, 1), np.uint32),      # 2 rows per wave (the C5 chunk geometry)
+    ((3, 12, 14, 64, 1), np.int32),        # raw coder, negative samples
+    ((8, 6, 7, 8, 1), np.int32),           # 2 lanes per row, odd height
+])
+def test_wave32_matches_oracle(kom, shape, dtype):
+    """The 32-bit-sample wave kernel (kmp_codec_wave3d32.hip): float32 cell means and map
+    aggregation in the reference's order are NOT exact for full-range 32-bit samples, so this pins
+    the order against the oracle bit for bit; float32 bit patterns (C5) included."""
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = kom.volume, oracle.volume
+    rng = np.random.default_rng(13)
+    if dtype == np.uint32:
+        x = rng.integers(0, 1 << 32, size=shape, dtype=np.uint64).astype(np.uint32)
+        flat = x.reshape(-1)
+        k = flat[::7].size
+        flat[::7] = (rng.standard_normal(k) * 1e3).astype(np.float32).view(np.uint32)  # float32 bit patterns
+        enc, dec, oenc = ns.encode_values_uint32, ns.decode_values_uint32, ons.encode_values_uint32
+    else:
+        x = rng.integers(-(1 << 31), 1 << 31, size=shape, dtype=np.int64).astype(np.int32)
+        enc, dec, oenc = ns.encode_values_raw, ns.decode_values_raw, ons.encode_values_raw
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(0, 3), oenc, x)
+    pred = kom.MeanPredictor(0, 3)
+    lo, (maps, dims) = ns.encode(pred, enc, x)
+    assert _last_launch(kom) == 'wave3d32_encode'
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims)), x)
+    assert _last_launch(kom) == 'wave3d32_decode'
