@@ -35,14 +35,41 @@ static inline unsigned grid_for(int64_t n) {
   return (unsigned)g;
 }
 
-// Decompose a flat index over [B, e0, e1, e2, C].
-struct Idx5 {
-  int64_t b, i0, i1, i2, c;
+// Every kernel below is instantiated with a 32-bit index type when all the arrays it touches
+// have fewer than 2^30 elements (64-bit multiplies and divisions are multi-instruction sequences
+// on gfx950), and with I otherwise.
+template <typename I>
+struct IdxT {
+  I b, i0, i1, i2, c;
 };
-__device__ __forceinline__ Idx5 unflatten5(int64_t t, int64_t e0, int64_t e1, int64_t e2, int64_t C) {
-  Idx5 r;
-  unflat5(t, e0, e1, e2, C, r.b, r.i0, r.i1, r.i2, r.c);
+// Decompose a flat index over [B, e0, e1, e2, C].
+template <typename I>
+__device__ __forceinline__ IdxT<I> unflat_t(I t, I e0, I e1, I e2, I C) {
+  IdxT<I> r;
+  if constexpr (sizeof(I) == 4) {
+    uint32_t u = (uint32_t)t;
+    if (C == 1) {
+      r.c = 0;
+    } else {
+      r.c = (I)(u % (uint32_t)C);
+      u /= (uint32_t)C;
+    }
+    r.i2 = (I)(u % (uint32_t)e2); u /= (uint32_t)e2;
+    r.i1 = (I)(u % (uint32_t)e1); u /= (uint32_t)e1;
+    r.i0 = (I)(u % (uint32_t)e0);
+    r.b = (I)(u / (uint32_t)e0);
+  } else {
+    unflat5(t, e0, e1, e2, C, r.b, r.i0, r.i1, r.i2, r.c);
+  }
   return r;
+}
+template <typename I>
+__device__ __forceinline__ I sym_idx(I i, I n) {  // sym_index in the kernel's index type
+  if (i >= 0 && i < n) return i;
+  if (i >= -n && i < 2 * n) return i < 0 ? -1 - i : 2 * n - 1 - i;
+  I m = i % (2 * n);
+  if (m < 0) m += 2 * n;
+  return m < n ? m : 2 * n - 1 - m;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -51,20 +78,28 @@ __device__ __forceinline__ Idx5 unflatten5(int64_t t, int64_t e0, int64_t e1, in
 struct Ext3 {
   int64_t e[3];
 };
+template <typename I>
+struct E3 {
+  I e[3];
+};
+template <typename I>
+static inline E3<I> e3(const Ext3& x) {
+  return E3<I>{{(I)x.e[0], (I)x.e[1], (I)x.e[2]}};
+}
 
 // out_k[b, o, c] = in[b, 2*o + par_k, c] for every class k whose pointer is set and whose
 // extent contains o.  Class 0 = all-even (lowres), classes 1..7 (1..3) = maps.
-template <typename T>
-__global__ void __launch_bounds__(kThreads) deinterleave_kernel(const T* __restrict__ in, int64_t B, Ext3 n,
-                                                              int64_t C, int nsp, MapPtrs outs, void* lowres,
-                                                              int64_t total) {
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) deinterleave_kernel(const T* __restrict__ in, I B, E3<I> n,
+                                                              I C, int nsp, MapPtrs outs, void* lowres,
+                                                              I total) {
   const int nmaps = nsp == 3 ? 7 : 3;
   // frame = ceil(n/2) per axis (dummy axes: 1)
-  const int64_t f0 = (n.e[0] + 1) / 2, f1 = (n.e[1] + 1) / 2, f2 = (n.e[2] + 1) / 2;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, f0, f1, f2, C);
+  const I f0 = (n.e[0] + 1) / 2, f1 = (n.e[1] + 1) / 2, f2 = (n.e[2] + 1) / 2;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, f0, f1, f2, C);
     auto src = [&](int pz, int py, int px) -> T {
-      const int64_t z = 2 * q.i0 + pz, y = 2 * q.i1 + py, x = 2 * q.i2 + px;
+      const I z = 2 * q.i0 + pz, y = 2 * q.i1 + py, x = 2 * q.i2 + px;
       return in[(((q.b * n.e[0] + z) * n.e[1] + y) * n.e[2] + x) * C + q.c];
     };
     if (lowres) {
@@ -76,8 +111,8 @@ __global__ void __launch_bounds__(kThreads) deinterleave_kernel(const T* __restr
       int par[3];
       map_parity(nsp, k, par);
       // extent of class: parity 1 -> floor(n/2), parity 0 -> ceil(n/2); dummy axis -> 1
-      int64_t e[3];
-      const int64_t idx[3] = {q.i0, q.i1, q.i2};
+      I e[3];
+      const I idx[3] = {q.i0, q.i1, q.i2};
       bool ok = true;
       for (int a = 0; a < 3; ++a) {
         e[a] = (a < 3 - nsp) ? 1 : (par[a] ? n.e[a] / 2 : (n.e[a] + 1) / 2);
@@ -92,24 +127,24 @@ __global__ void __launch_bounds__(kThreads) deinterleave_kernel(const T* __restr
 
 // out[b, 2*o + par_k, c] = class_k[b, o, c]; out extent 2L-1 per axis.  Class extents follow
 // highres_from_lowres_and_maps: lowres L, maps (par ? L-1 : L).
-template <typename T>
+template <typename T, typename I>
 __global__ void __launch_bounds__(kThreads) interleave_kernel(const T* __restrict__ lowres, CMapPtrs maps,
-                                                            int64_t B, Ext3 L, int64_t C, int nsp, T* __restrict__ out,
-                                                            int64_t total) {
+                                                            I B, E3<I> L, I C, int nsp, T* __restrict__ out,
+                                                            I total) {
   const int nmaps = nsp == 3 ? 7 : 3;
-  const int64_t h0 = 2 * L.e[0] - 1, h1 = 2 * L.e[1] - 1, h2 = 2 * L.e[2] - 1;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, L.e[0], L.e[1], L.e[2], C);
+  const I h0 = 2 * L.e[0] - 1, h1 = 2 * L.e[1] - 1, h2 = 2 * L.e[2] - 1;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, L.e[0], L.e[1], L.e[2], C);
     auto dst = [&](int pz, int py, int px) -> T& {
-      const int64_t z = 2 * q.i0 + pz, y = 2 * q.i1 + py, x = 2 * q.i2 + px;
+      const I z = 2 * q.i0 + pz, y = 2 * q.i1 + py, x = 2 * q.i2 + px;
       return out[(((q.b * h0 + z) * h1 + y) * h2 + x) * C + q.c];
     };
     dst(0, 0, 0) = lowres[t];
     for (int k = 0; k < nmaps; ++k) {
       int par[3];
       map_parity(nsp, k, par);
-      int64_t e[3];
-      const int64_t idx[3] = {q.i0, q.i1, q.i2};
+      I e[3];
+      const I idx[3] = {q.i0, q.i1, q.i2};
       bool ok = true;
       for (int a = 0; a < 3; ++a) {
         e[a] = (a < 3 - nsp) ? 1 : (par[a] ? L.e[a] - 1 : L.e[a]);
@@ -133,67 +168,141 @@ __constant__ int8_t c_targets3[19][3] = {
     {0, 0, 1}, {0, 2, 1}, {2, 2, 1}, {2, 0, 1}};                                // x0..x3
 __constant__ int8_t c_targets2[5][2] = {{1, 0}, {1, 2}, {0, 1}, {2, 1}, {1, 1}};  // image/utils.py:40-44
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) targets_kernel(const T* __restrict__ in, int64_t B, Ext3 n, int64_t C,
-                                                         int nsp, T* __restrict__ out, int64_t total) {
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) targets_kernel(const T* __restrict__ in, I B, E3<I> n, I C,
+                                                         int nsp, T* __restrict__ out, I total) {
   const int K = nsp == 3 ? 19 : 5;
-  const int64_t c0 = nsp == 3 ? (n.e[0] - 1) / 2 : 1, c1 = (n.e[1] - 1) / 2, c2 = (n.e[2] - 1) / 2;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, c0, c1, c2, C);
-    const int64_t cell = ((q.b * c0 + q.i0) * c1 + q.i1) * c2 + q.i2;
+  const I c0 = nsp == 3 ? (n.e[0] - 1) / 2 : 1, c1 = (n.e[1] - 1) / 2, c2 = (n.e[2] - 1) / 2;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, c0, c1, c2, C);
+    const I cell = ((q.b * c0 + q.i0) * c1 + q.i1) * c2 + q.i2;
     for (int k = 0; k < K; ++k) {
       int dz, dy, dx;
       if (nsp == 3) { dz = c_targets3[k][0]; dy = c_targets3[k][1]; dx = c_targets3[k][2]; }
       else { dz = 0; dy = c_targets2[k][0]; dx = c_targets2[k][1]; }
-      const int64_t z = nsp == 3 ? 2 * q.i0 + dz : 0, y = 2 * q.i1 + dy, x = 2 * q.i2 + dx;
+      const I z = nsp == 3 ? 2 * q.i0 + dz : 0, y = 2 * q.i1 + dy, x = 2 * q.i2 + dx;
       out[(cell * K + k) * C + q.c] = in[(((q.b * n.e[0] + z) * n.e[1] + y) * n.e[2] + x) * C + q.c];
     }
   }
 }
 
 // features_from_lowres: [B, S-2p-1..., N, C], N = (2p+2)^d, offsets z-major then y, x.
-template <typename T>
-__global__ void __launch_bounds__(kThreads) features_kernel(const T* __restrict__ in, int64_t B, Ext3 S, int64_t C,
-                                                          int nsp, int p, T* __restrict__ out, int64_t total) {
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) features_kernel(const T* __restrict__ in, I B, E3<I> S, I C,
+                                                          int nsp, int p, T* __restrict__ out, I total) {
   const int k = 2 * p + 2;
   const int kz = nsp == 3 ? k : 1;
   const int N = kz * k * k;
-  const int64_t c0 = nsp == 3 ? S.e[0] - 2 * p - 1 : 1, c1 = S.e[1] - 2 * p - 1, c2 = S.e[2] - 2 * p - 1;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, c0, c1, c2, C);
-    const int64_t cell = ((q.b * c0 + q.i0) * c1 + q.i1) * c2 + q.i2;
+  const I c0 = nsp == 3 ? S.e[0] - 2 * p - 1 : 1, c1 = S.e[1] - 2 * p - 1, c2 = S.e[2] - 2 * p - 1;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, c0, c1, c2, C);
+    const I cell = ((q.b * c0 + q.i0) * c1 + q.i1) * c2 + q.i2;
     int f = 0;
     for (int dz = 0; dz < kz; ++dz)
       for (int dy = 0; dy < k; ++dy)
         for (int dx = 0; dx < k; ++dx, ++f) {
-          const int64_t z = q.i0 + dz, y = q.i1 + dy, x = q.i2 + dx;
+          const I z = q.i0 + dz, y = q.i1 + dy, x = q.i2 + dx;
           out[(cell * N + f) * C + q.c] = in[(((q.b * S.e[0] + z) * S.e[1] + y) * S.e[2] + x) * C + q.c];
         }
+  }
+}
+
+// C == 1, 32-bit indices, compile-time neighbourhood: one cell per thread, its N features
+// gathered into registers and written as 16-byte vectors (or one 4 / 8-byte store when the whole
+// cell is smaller); the output is 16-byte aligned.
+template <typename T, int NSP, int P>
+__global__ void __launch_bounds__(kThreads) features_vec_kernel(const T* __restrict__ in, int32_t S0, int32_t S1,
+                                                              int32_t S2, T* __restrict__ out, int32_t cells) {
+  constexpr int K = 2 * P + 2, KZ = NSP == 3 ? K : 1, N = KZ * K * K;
+  constexpr int NB = N * (int)sizeof(T);
+  constexpr int SB = NB >= 16 ? 16 : NB;  // store width: 16 bytes, or the whole cell when smaller
+  static_assert(NB % SB == 0 && (SB == 16 || SB == 8 || SB == 4), "whole stores per cell");
+  using SV = typename std::conditional<SB == 16, uint4, typename std::conditional<SB == 8, uint2, uint32_t>::type>::type;
+  const int32_t c0 = NSP == 3 ? S0 - 2 * P - 1 : 1, c1 = S1 - 2 * P - 1, c2 = S2 - 2 * P - 1;
+  for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cells; t += gridDim.x * blockDim.x) {
+    uint32_t q = (uint32_t)t;
+    const int32_t x = q % (uint32_t)c2; q /= (uint32_t)c2;
+    const int32_t y = q % (uint32_t)c1; q /= (uint32_t)c1;
+    const int32_t z = q % (uint32_t)c0;
+    const int32_t b = q / (uint32_t)c0;
+    const T* base = in + ((b * S0 + z) * S1 + y) * S2 + x;
+    T f[N];
+#pragma unroll
+    for (int dz = 0; dz < KZ; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < K; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx) f[(dz * K + dy) * K + dx] = base[(dz * S1 + dy) * S2 + dx];
+    SV* o = (SV*)(out + (int64_t)t * N);
+#pragma unroll
+    for (int v = 0; v < NB / SB; ++v) {
+      SV w;
+      __builtin_memcpy(&w, (const char*)f + v * SB, SB);
+      o[v] = w;
+    }
+  }
+}
+
+// u8 / u16, C == 1, 32-bit indices: the f32 sum of at most 4 integer predictions is exact, so the
+// reference's scale-and-truncate is an integer shift (the values of aggregate_map).
+template <typename T, int NSP>
+__global__ void __launch_bounds__(kThreads) maps_from_predictions_int_kernel(const T* __restrict__ preds, int32_t Lcz,
+                                                                           int32_t Lcy, int32_t Lcx, MapPtrs outs,
+                                                                           int32_t total) {
+  constexpr int NM = NSP == 3 ? 7 : 3, K = NSP == 3 ? 19 : 5;
+  const int32_t f0 = NSP == 3 ? Lcz + 1 : 1, f1 = Lcy + 1, f2 = Lcx + 1, cz = NSP == 3 ? Lcz : 1;
+  for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    uint32_t q = (uint32_t)t;
+    const int32_t ox = q % (uint32_t)f2; q /= (uint32_t)f2;
+    const int32_t oy = q % (uint32_t)f1; q /= (uint32_t)f1;
+    const int32_t oz = q % (uint32_t)f0;
+    const int32_t b = q / (uint32_t)f0;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      int par[3];
+      map_parity(NSP, k, par);
+      const int32_t e0 = NSP == 3 ? (par[0] ? Lcz : Lcz + 1) : 1, e1 = par[1] ? Lcy : Lcy + 1, e2 = par[2] ? Lcx : Lcx + 1;
+      if (oz >= e0 || oy >= e1 || ox >= e2) continue;
+      Contrib c[4];
+      const int nc = map_contribs(NSP, k, c);
+      uint32_t s = 0, cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i >= nc) break;
+        const int32_t z = oz - c[i].dz, y = oy - c[i].dy, x = ox - c[i].dx;
+        if (z >= 0 && z < cz && y >= 0 && y < Lcy && x >= 0 && x < Lcx) {
+          s += preds[(((b * cz + z) * Lcy + y) * Lcx + x) * K + c[i].ch];
+          ++cnt;
+        }
+      }
+      ((T*)outs.p[k])[((b * e0 + oz) * e1 + oy) * e2 + ox] = (T)(k == center_map(NSP) ? s : s >> (cnt >> 1));
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // maps_from_predictions: float32 aggregation of [B, cells..., K, C] predictions.
 // ------------------------------------------------------------------------------------------
-template <typename T>
-__global__ void __launch_bounds__(kThreads) maps_from_predictions_kernel(const T* __restrict__ preds, int64_t B,
-                                                                       Ext3 cells, int64_t C, int nsp, MapPtrs outs,
-                                                                       int64_t total) {
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) maps_from_predictions_kernel(const T* __restrict__ preds, I B,
+                                                                       E3<I> cells, I C, int nsp, MapPtrs outs,
+                                                                       I total) {
   const int nmaps = nsp == 3 ? 7 : 3;
   const int K = nsp == 3 ? 19 : 5;
   // frame = cells + 1 per spatial axis
-  const int64_t f0 = nsp == 3 ? cells.e[0] + 1 : 1, f1 = cells.e[1] + 1, f2 = cells.e[2] + 1;
-  const int64_t Lcz = cells.e[0], Lcy = cells.e[1], Lcx = cells.e[2];
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, f0, f1, f2, C);
-    auto get = [&](int64_t z, int64_t y, int64_t x, int ch) -> T {
+  const I f0 = nsp == 3 ? cells.e[0] + 1 : 1, f1 = cells.e[1] + 1, f2 = cells.e[2] + 1;
+  const I Lcz = cells.e[0], Lcy = cells.e[1], Lcx = cells.e[2];
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, f0, f1, f2, C);
+    auto get = [&](int64_t z64, int64_t y64, int64_t x64, int ch) -> T {
+      const I z = (I)z64, y = (I)y64, x = (I)x64;
       return preds[(((((q.b * Lcz + z) * Lcy + y) * Lcx + x) * K) + ch) * C + q.c];
     };
     for (int k = 0; k < nmaps; ++k) {
       int par[3];
       map_parity(nsp, k, par);
-      int64_t e[3];
-      const int64_t idx[3] = {q.i0, q.i1, q.i2};
+      I e[3];
+      const I idx[3] = {q.i0, q.i1, q.i2};
       bool ok = true;
       for (int a = 0; a < 3; ++a) {
         e[a] = (a < 3 - nsp) ? 1 : (par[a] ? cells.e[a] : cells.e[a] + 1);
@@ -202,7 +311,7 @@ __global__ void __launch_bounds__(kThreads) maps_from_predictions_kernel(const T
       if (!ok) continue;
       T* o = (T*)outs.p[k];
       o[(((q.b * e[0] + q.i0) * e[1] + q.i1) * e[2] + q.i2) * C + q.c] =
-          aggregate_map<T>(nsp, k, q.i0, q.i1, q.i2, Lcz, Lcy, Lcx, get);
+          aggregate_map<T>(nsp, k, (int64_t)q.i0, (int64_t)q.i1, (int64_t)q.i2, (int64_t)Lcz, (int64_t)Lcy, (int64_t)Lcx, get);
     }
   }
 }
@@ -211,9 +320,9 @@ __global__ void __launch_bounds__(kThreads) maps_from_predictions_kernel(const T
 // Mean predictor on a padded lowres window (tests/volume/test_encode_decode.py:46-53):
 // cell mean = astype(T)(f32 sum of the (2p+2)^d neighbourhood / N), then the map aggregation.
 // ------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ T cell_mean_padded(const T* __restrict__ in, int64_t b, int64_t cz, int64_t cy, int64_t cx,
-                                              int64_t c, Ext3 S, int64_t C, int nsp, int p) {
+template <typename T, typename I>
+__device__ __forceinline__ T cell_mean_padded(const T* __restrict__ in, I b, I cz, I cy, I cx,
+                                              I c, E3<I> S, I C, int nsp, int p) {
   const int k = 2 * p + 2;
   const int kz = nsp == 3 ? k : 1;
   float s = 0.0f;
@@ -227,13 +336,13 @@ __device__ __forceinline__ T cell_mean_padded(const T* __restrict__ in, int64_t 
 // Two passes: (1) the per-cell means ARE the C map (volume/utils.py:117: channel 6 unscaled; 2D
 // channel 4), so they are written there once; (2) every other map aggregates up to 4 of them
 // (the f32 scatter-add / scale / truncate of volume/utils.py:83-155, kmp_aggregate.h).
-template <typename T>
-__global__ void __launch_bounds__(kThreads) cell_mean_map_kernel(const T* __restrict__ in, int64_t B, Ext3 S,
-                                                               int64_t C, int nsp, int p, Ext3 cells,
-                                                               T* __restrict__ out, int64_t total) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, cells.e[0], cells.e[1], cells.e[2], C);
-    out[t] = cell_mean_padded<T>(in, q.b, q.i0, q.i1, q.i2, q.c, S, C, nsp, p);
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) cell_mean_map_kernel(const T* __restrict__ in, I B, E3<I> S,
+                                                               I C, int nsp, int p, E3<I> cells,
+                                                               T* __restrict__ out, I total) {
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, cells.e[0], cells.e[1], cells.e[2], C);
+    out[t] = cell_mean_padded<T, I>(in, q.b, q.i0, q.i1, q.i2, q.c, S, C, nsp, p);
   }
 }
 
@@ -275,24 +384,25 @@ __global__ void __launch_bounds__(kThreads) maps_from_cell_means_int_kernel(cons
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T* __restrict__ cm, int64_t B,
-                                                                      Ext3 cells, int64_t C, int nsp, MapPtrs outs,
-                                                                      int64_t total) {
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T* __restrict__ cm, I B,
+                                                                      E3<I> cells, I C, int nsp, MapPtrs outs,
+                                                                      I total) {
   const int nmaps = nsp == 3 ? 7 : 3;
-  const int64_t Lcz = cells.e[0], Lcy = cells.e[1], Lcx = cells.e[2];
-  const int64_t f0 = nsp == 3 ? Lcz + 1 : 1, f1 = Lcy + 1, f2 = Lcx + 1;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, f0, f1, f2, C);
-    auto get = [&](int64_t z, int64_t y, int64_t x, int) -> T {
+  const I Lcz = cells.e[0], Lcy = cells.e[1], Lcx = cells.e[2];
+  const I f0 = nsp == 3 ? Lcz + 1 : 1, f1 = Lcy + 1, f2 = Lcx + 1;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, f0, f1, f2, C);
+    auto get = [&](int64_t z64, int64_t y64, int64_t x64, int) -> T {
+      const I z = (I)z64, y = (I)y64, x = (I)x64;
       return cm[(((q.b * Lcz + z) * Lcy + y) * Lcx + x) * C + q.c];
     };
     for (int k = 0; k < nmaps; ++k) {
       if (k == center_map(nsp)) continue;
       int par[3];
       map_parity(nsp, k, par);
-      int64_t e[3];
-      const int64_t idx[3] = {q.i0, q.i1, q.i2};
+      I e[3];
+      const I idx[3] = {q.i0, q.i1, q.i2};
       bool ok = true;
       for (int a = 0; a < 3; ++a) {
         e[a] = (a < 3 - nsp) ? 1 : (par[a] ? cells.e[a] : cells.e[a] + 1);
@@ -301,7 +411,7 @@ __global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T*
       if (!ok) continue;
       T* o = (T*)outs.p[k];
       o[(((q.b * e[0] + q.i0) * e[1] + q.i1) * e[2] + q.i2) * C + q.c] =
-          aggregate_map<T>(nsp, k, q.i0, q.i1, q.i2, Lcz, Lcy, Lcx, get);
+          aggregate_map<T>(nsp, k, (int64_t)q.i0, (int64_t)q.i1, (int64_t)q.i2, (int64_t)Lcz, (int64_t)Lcy, (int64_t)Lcx, get);
     }
   }
 }
@@ -309,37 +419,63 @@ __global__ void __launch_bounds__(kThreads) maps_from_cell_means_kernel(const T*
 // ------------------------------------------------------------------------------------------
 // jnp.pad on the spatial axes ('symmetric' / 'reflect'); negative pads crop.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t reflect_index(int64_t i, int64_t n) {
+template <typename I>
+__device__ __forceinline__ I reflect_index(I i, I n) {
   if (n == 1) return 0;
-  const int64_t per = 2 * (n - 1);
-  int64_t m = i % per;
+  const I per = 2 * (n - 1);
+  I m = i % per;
   if (m < 0) m += per;
   return m < n ? m : per - m;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) pad_kernel(const T* __restrict__ in, int64_t B, Ext3 n, int64_t C,
-                                                     Ext3 lo, Ext3 out_e, int mode, T* __restrict__ out,
-                                                     int64_t total) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, out_e.e[0], out_e.e[1], out_e.e[2], C);
-    const int64_t o[3] = {q.i0, q.i1, q.i2};
-    int64_t s[3];
+template <typename T, typename I>
+__global__ void __launch_bounds__(kThreads) pad_kernel(const T* __restrict__ in, I B, E3<I> n, I C,
+                                                     E3<I> lo, E3<I> out_e, int mode, T* __restrict__ out,
+                                                     I total) {
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, out_e.e[0], out_e.e[1], out_e.e[2], C);
+    const I o[3] = {q.i0, q.i1, q.i2};
+    I s[3];
     for (int a = 0; a < 3; ++a) {
-      const int64_t i = o[a] - lo.e[a];
-      s[a] = (i >= 0 && i < n.e[a]) ? i : (mode == 0 ? sym_index(i, n.e[a]) : reflect_index(i, n.e[a]));
+      const I i = o[a] - lo.e[a];
+      s[a] = (i >= 0 && i < n.e[a]) ? i : (mode == 0 ? sym_idx<I>(i, n.e[a]) : reflect_index<I>(i, n.e[a]));
     }
     out[t] = in[(((q.b * n.e[0] + s[0]) * n.e[1] + s[1]) * n.e[2] + s[2]) * C + q.c];
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// Coders (utils.py:28-55), 8 elements per thread when the count allows.
+// Coders (utils.py:28-55), one element per thread.
 // ------------------------------------------------------------------------------------------
-template <int DIR, int CODER, typename TP, typename TX>
-__global__ void __launch_bounds__(kThreads) code_kernel(const TP* __restrict__ pred, const TX* __restrict__ x, int64_t n,
+// 16-byte vector form for operands and result of one element size (the common case: the coder
+// of the sample dtype on same-dtype predictions), 16-byte aligned; ``n16`` vectors.
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+template <int DIR, int CODER, typename TV>
+__global__ void __launch_bounds__(kThreads) code_vec_kernel(const u32x4v* __restrict__ pred,
+                                                          const u32x4v* __restrict__ x, int64_t n16,
+                                                          u32x4v* __restrict__ out) {
+  using TO = typename coder_out<CODER>::type;
+  constexpr int V = 16 / sizeof(TV);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n16; t += (int64_t)gridDim.x * blockDim.x) {
+    const u32x4v pv = __builtin_nontemporal_load(pred + t), xv = __builtin_nontemporal_load(x + t);
+    const TV* pp = (const TV*)&pv;
+    const TV* xx = (const TV*)&xv;
+    u32x4v ov;
+    TO* oo = (TO*)&ov;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int32_t p = to_i32(pp[i]), v = to_i32(xx[i]);
+      oo[i] = DIR == KMP_ENCODE ? code_encode<CODER>(p, v) : code_decode<CODER>(p, v);
+    }
+    __builtin_nontemporal_store(ov, out + t);
+  }
+}
+
+template <int DIR, int CODER, typename TP, typename TX, typename I>
+__global__ void __launch_bounds__(kThreads) code_kernel(const TP* __restrict__ pred, const TX* __restrict__ x, I n,
                                                       typename coder_out<CODER>::type* __restrict__ out) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < n; t += (I)gridDim.x * blockDim.x) {
     const int32_t p = to_i32(pred[t]);
     const int32_t v = to_i32(x[t]);
     out[t] = DIR == KMP_ENCODE ? code_encode<CODER>(p, v) : code_decode<CODER>(p, v);
@@ -355,15 +491,15 @@ __device__ __forceinline__ TO convert(TI v) {
   else return (TO)v;
 }
 
-template <typename TI, typename TO>
-__global__ void __launch_bounds__(kThreads) copy_box_kernel(const TI* __restrict__ in, Ext3 in_e, Ext3 in_off,
-                                                          TO* __restrict__ out, Ext3 out_e, Ext3 out_off, Ext3 ext,
-                                                          int64_t C, int64_t total) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    Idx5 q = unflatten5(t, ext.e[0], ext.e[1], ext.e[2], C);
-    const int64_t si = (((q.b * in_e.e[0] + in_off.e[0] + q.i0) * in_e.e[1] + in_off.e[1] + q.i1) * in_e.e[2] +
+template <typename TI, typename TO, typename I>
+__global__ void __launch_bounds__(kThreads) copy_box_kernel(const TI* __restrict__ in, E3<I> in_e, E3<I> in_off,
+                                                          TO* __restrict__ out, E3<I> out_e, E3<I> out_off, E3<I> ext,
+                                                          I C, I total) {
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    IdxT<I> q = unflat_t<I>(t, ext.e[0], ext.e[1], ext.e[2], C);
+    const I si = (((q.b * in_e.e[0] + in_off.e[0] + q.i0) * in_e.e[1] + in_off.e[1] + q.i1) * in_e.e[2] +
                         in_off.e[2] + q.i2) * C + q.c;
-    const int64_t so = (((q.b * out_e.e[0] + out_off.e[0] + q.i0) * out_e.e[1] + out_off.e[1] + q.i1) * out_e.e[2] +
+    const I so = (((q.b * out_e.e[0] + out_off.e[0] + q.i0) * out_e.e[1] + out_off.e[1] + q.i1) * out_e.e[2] +
                         out_off.e[2] + q.i2) * C + q.c;
     out[so] = convert<TO>(in[si]);
   }
@@ -377,6 +513,18 @@ static inline Ext3 ext_from(int nsp, const int64_t* shape) {
   for (int a = 0; a < 3; ++a) e.e[a] = (a < 3 - nsp) ? 1 : shape[a - (3 - nsp)];
   return e;
 }
+
+// 32-bit kernel indices when every array the launch touches is below 2^30 elements
+static inline bool fits32(std::initializer_list<int64_t> counts) {
+  for (int64_t c : counts)
+    if (c >= ((int64_t)1 << 30)) return false;
+  return true;
+}
+template <typename F>
+static int with_index(bool small, F&& f) {
+  return small ? f(int32_t{}) : f(int64_t{});
+}
+static inline int64_t vol(int64_t B, const Ext3& e, int64_t C) { return B * e.e[0] * e.e[1] * e.e[2] * C; }
 
 static inline int check_common(int nsp, int64_t B, const int64_t* shape, int64_t C) {
   KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
@@ -404,7 +552,7 @@ int kmp_device_ok(void) {
     return 0;
   }
   hipFuncAttributes attr;
-  e = hipFuncGetAttributes(&attr, (const void*)&pad_kernel<uint8_t>);
+  e = hipFuncGetAttributes(&attr, (const void*)&pad_kernel<uint8_t, int32_t>);
   if (e != hipSuccess) {
     set_error(std::string("libkompressor_hip has no code object for this device (built for gfx950): ") +
               hipGetErrorString(e));
@@ -433,9 +581,12 @@ int kmp_lowres_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t 
   MapPtrs none{};
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    deinterleave_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, B, n, C, nsp, none,
-                                                                                   out, total);
-    return check_launch("lowres_from_highres");
+    return with_index(fits32({vol(B, n, C)}), [&](auto itag) {
+      using I = decltype(itag);
+      deinterleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)in, (I)B, e3<I>(n), (I)C, nsp, none, out, (I)total);
+      return check_launch("lowres_from_highres");
+    });
   });
 }
 
@@ -453,9 +604,12 @@ int kmp_maps_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B,
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    deinterleave_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, B, n, C, nsp, outs,
-                                                                                   nullptr, total);
-    return check_launch("maps_from_highres");
+    return with_index(fits32({vol(B, n, C)}), [&](auto itag) {
+      using I = decltype(itag);
+      deinterleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)in, (I)B, e3<I>(n), (I)C, nsp, outs, nullptr, (I)total);
+      return check_launch("maps_from_highres");
+    });
   });
 }
 
@@ -469,9 +623,12 @@ int kmp_targets_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t
   if (total <= 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    targets_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, B, n, C, nsp, (T*)out,
-                                                                              total);
-    return check_launch("targets_from_highres");
+    return with_index(fits32({vol(B, n, C), total * (nsp == 3 ? 19 : 5)}), [&](auto itag) {
+      using I = decltype(itag);
+      targets_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, (I)B, e3<I>(n), (I)C,
+                                                                                  nsp, (T*)out, (I)total);
+      return check_launch("targets_from_highres");
+    });
   });
 }
 
@@ -489,9 +646,14 @@ int kmp_highres_from_lowres_and_maps(int32_t nsp, int32_t dtype, const void* low
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    interleave_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, mp, B, L, C, nsp,
-                                                                                 (T*)out, total);
-    return check_launch("highres_from_lowres_and_maps");
+    const Ext3 H{{2 * L.e[0] - 1, 2 * L.e[1] - 1, 2 * L.e[2] - 1}};
+    return with_index(fits32({vol(B, H, C)}), [&](auto itag) {
+      using I = decltype(itag);
+      interleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, mp, (I)B,
+                                                                                     e3<I>(L), (I)C, nsp, (T*)out,
+                                                                                     (I)total);
+      return check_launch("highres_from_lowres_and_maps");
+    });
   });
 }
 
@@ -508,9 +670,26 @@ int kmp_features_from_lowres(int32_t nsp, int32_t dtype, const void* lowres, int
   if (cells == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    features_kernel<T><<<grid_for(cells), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, B, S, C, nsp, padding,
-                                                                               (T*)out, cells);
-    return check_launch("features_from_lowres");
+    const int k = 2 * padding + 2;
+    const bool small = fits32({vol(B, S, C), cells * (nsp == 3 ? k * k * k : k * k)});
+    if (small && C == 1 && ((uintptr_t)out & 15) == 0 && padding <= 1 && sizeof(T) <= 2) {
+      auto launch = [&](auto kern) {
+        kern<<<grid_for(cells), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, (int32_t)S.e[0], (int32_t)S.e[1],
+                                                                    (int32_t)S.e[2], (T*)out, (int32_t)cells);
+        return check_launch("features_from_lowres");
+      };
+      if constexpr (sizeof(T) <= 2) {
+        if (nsp == 3) return padding == 0 ? launch(features_vec_kernel<T, 3, 0>) : launch(features_vec_kernel<T, 3, 1>);
+        return padding == 0 ? launch(features_vec_kernel<T, 2, 0>) : launch(features_vec_kernel<T, 2, 1>);
+      }
+    }
+    return with_index(small, [&](auto itag) {
+      using I = decltype(itag);
+      features_kernel<T, I><<<grid_for(cells), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, (I)B, e3<I>(S),
+                                                                                   (I)C, nsp, padding, (T*)out,
+                                                                                   (I)cells);
+      return check_launch("features_from_lowres");
+    });
   });
 }
 
@@ -529,9 +708,21 @@ int kmp_maps_from_predictions(int32_t nsp, int32_t dtype, const void* preds, int
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    maps_from_predictions_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)preds, B, ce, C,
-                                                                                            nsp, outs, total);
-    return check_launch("maps_from_predictions");
+    const bool small = fits32({vol(B, ce, C) * (nsp == 3 ? 19 : 5), total});
+    if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
+      if (small && C == 1) {
+        auto kern = nsp == 3 ? maps_from_predictions_int_kernel<T, 3> : maps_from_predictions_int_kernel<T, 2>;
+        kern<<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)preds, (int32_t)ce.e[0], (int32_t)ce.e[1],
+                                                                    (int32_t)ce.e[2], outs, (int32_t)total);
+        return check_launch("maps_from_predictions");
+      }
+    }
+    return with_index(small, [&](auto itag) {
+      using I = decltype(itag);
+      maps_from_predictions_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)preds, (I)B, e3<I>(ce), (I)C, nsp, outs, (I)total);
+      return check_launch("maps_from_predictions");
+    });
   });
 }
 
@@ -558,16 +749,25 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
   return dispatch_int_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     T* cm = (T*)outs.p[center_map(nsp)];
-    cell_mean_map_kernel<T><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>((const T*)padded_lowres, B, S, C,
-                                                                                   nsp, padding, cells, cm, ncell);
-    if (int st = check_launch("mean_predict_maps")) return st;
+    const bool small = fits32({vol(B, S, C), total});
+    int st = with_index(small, [&](auto itag) {
+      using I = decltype(itag);
+      cell_mean_map_kernel<T, I><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)padded_lowres, (I)B, e3<I>(S), (I)C, nsp, padding, e3<I>(cells), cm, (I)ncell);
+      return check_launch("mean_predict_maps");
+    });
+    if (st) return st;
     if ((std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) && C == 1 && total < ((int64_t)1 << 31)) {
       auto k = nsp == 3 ? maps_from_cell_means_int_kernel<T, 3> : maps_from_cell_means_int_kernel<T, 2>;
       k<<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, (int32_t)cells.e[0], (int32_t)cells.e[1],
                                                               (int32_t)cells.e[2], outs, (int32_t)total);
     } else {
-      maps_from_cell_means_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(cm, B, cells, C, nsp, outs,
-                                                                                            total);
+      return with_index(small, [&](auto itag) {
+        using I = decltype(itag);
+        maps_from_cell_means_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
+            cm, (I)B, e3<I>(cells), (I)C, nsp, outs, (I)total);
+        return check_launch("mean_predict_maps");
+      });
     }
     return check_launch("mean_predict_maps");
   });
@@ -592,9 +792,13 @@ int kmp_pad(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
-    pad_kernel<T><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, B, n, C, lo, oe, mode, (T*)out,
-                                                                          total);
-    return check_launch("pad");
+    return with_index(fits32({vol(B, n, C), total}), [&](auto itag) {
+      using I = decltype(itag);
+      pad_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, (I)B, e3<I>(n), (I)C,
+                                                                              e3<I>(lo), e3<I>(oe), mode, (T*)out,
+                                                                              (I)total);
+      return check_launch("pad");
+    });
   });
 }
 
@@ -620,9 +824,12 @@ int kmp_copy_box(int32_t nsp, int32_t in_dtype, const void* in, const int64_t in
     using TI = decltype(itag);
     return dispatch_any_dtype(out_dtype, [&](auto otag) {
       using TO = decltype(otag);
-      copy_box_kernel<TI, TO><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const TI*)in, ie, io, (TO*)out,
-                                                                                      oe, oo, ee, C, total);
-      return check_launch("copy_box");
+      return with_index(fits32({vol(B, ie, C), vol(B, oe, C)}), [&](auto itag) {
+        using I = decltype(itag);
+        copy_box_kernel<TI, TO, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
+            (const TI*)in, e3<I>(ie), e3<I>(io), (TO*)out, e3<I>(oe), e3<I>(oo), e3<I>(ee), (I)C, (I)total);
+        return check_launch("copy_box");
+      });
     });
   });
 }
@@ -641,9 +848,22 @@ int kmp_code(int32_t direction, int32_t coder, int32_t pred_dtype, const void* p
       using TP = decltype(ptag);
       return dispatch_any_dtype(x_dtype, [&](auto xtag) {
         using TX = decltype(xtag);
-        code_kernel<DIR, CODER, TP, TX><<<grid_for(n), kThreads, 0, s>>>(
-            (const TP*)pred, (const TX*)x, n, (typename coder_out<CODER>::type*)out);
-        return check_launch("code");
+        using TO = typename coder_out<CODER>::type;
+        if constexpr (sizeof(TP) == sizeof(TX) && sizeof(TX) == sizeof(TO) && !std::is_same<TP, float>::value &&
+                      !std::is_same<TX, float>::value) {
+          constexpr int V = 16 / sizeof(TX);
+          if ((((uintptr_t)pred | (uintptr_t)x | (uintptr_t)out) & 15) == 0 && n % V == 0) {
+            code_vec_kernel<DIR, CODER, TX><<<grid_for(n / V), kThreads, 0, s>>>(
+                (const u32x4v*)pred, (const u32x4v*)x, n / V, (u32x4v*)out);
+            return check_launch("code");
+          }
+        }
+        return with_index(fits32({n}), [&](auto itag) {
+          using I = decltype(itag);
+          code_kernel<DIR, CODER, TP, TX, I><<<grid_for(n), kThreads, 0, s>>>(
+              (const TP*)pred, (const TX*)x, (I)n, (typename coder_out<CODER>::type*)out);
+          return check_launch("code");
+        });
       });
     });
   };
