@@ -227,6 +227,26 @@ int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
                                 const int32_t dims[3], const void* const preds[7], void* highres_out,
                                 kmp_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Bit-plane container payload (kmp_pack.hip; SURVEY.md §8f f-3 -- no reference counterpart, */
+/* the reference returns the residual arrays unreduced, volume/encode_decode.py:56; format    */
+/* spec: oracle/packing.py).  n samples of ``dtype`` (8/16/32-bit), zigzag-mapped, blocks of 64 */
+/* stored as width 64-bit bit-planes.  ``workspace`` holds kmp_pack_workspace_bytes(n) bytes.  */
+/* ---------------------------------------------------------------------------------------- */
+int64_t kmp_pack_blocks(int64_t n);
+int64_t kmp_pack_workspace_bytes(int64_t n);
+/* byte offset in the workspace of the uint64 payload length (in 64-bit words) the plan writes */
+int64_t kmp_pack_total_offset(int64_t n);
+/* widths[nblocks] of x, and the block offsets + total payload words into the workspace */
+int kmp_pack_plan(int32_t dtype, const void* x, int64_t n, uint8_t* widths, void* workspace, kmp_stream_t stream);
+/* the payload (8-byte aligned) of x, after kmp_pack_plan on the same workspace */
+int kmp_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* widths, const void* workspace,
+             uint64_t* payload, kmp_stream_t stream);
+/* block offsets from stored widths, then the samples */
+int kmp_unpack_plan(const uint8_t* widths, int64_t n, void* workspace, kmp_stream_t stream);
+int kmp_unpack(int32_t dtype, const uint64_t* payload, int64_t n, const uint8_t* widths, const void* workspace,
+               void* out, kmp_stream_t stream);
+
 /* Categorical rank coder utils.py:58-111: ``logits`` float32 [n, L]; x/out of ``dtype`` [n]. */
 int kmp_categorical(int32_t direction, const float* logits, int64_t n, int64_t L, int32_t dtype, const void* x,
                     void* out, kmp_stream_t stream);

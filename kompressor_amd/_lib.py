@@ -86,6 +86,13 @@ _PROTOS = {
     'kmp_window_from_lowres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32p, _i32, _vp, _vp]),
     'kmp_encode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp, _vpp,
                                                    _vp]),
+    'kmp_pack_blocks': (ctypes.c_int64, [_i64]),
+    'kmp_pack_workspace_bytes': (ctypes.c_int64, [_i64]),
+    'kmp_pack_total_offset': (ctypes.c_int64, [_i64]),
+    'kmp_pack_plan': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp]),
+    'kmp_pack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
+    'kmp_unpack_plan': (ctypes.c_int, [_vp, _i64, _vp, _vp]),
+    'kmp_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
                                                    _vp, _vp]),
 }

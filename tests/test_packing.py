@@ -1,0 +1,90 @@
+"""Bit-plane container: the numpy specification (oracle/packing.py) on the
+CPU, and the HIP kernels (kmp_pack.hip) byte-for-byte against it on the GPU.  The reference has
+no container stage, so these pin the build's own format ("parity unpinned" by the reference)."""
+
+import numpy as np
+import pytest
+
+from oracle import packing as OPK
+
+
+def _residuals(n, dtype, rng, spread=4):
+    """Small signed residuals as the coders store them (wrapped modulo 2^W for unsigned dtypes)."""
+    r = rng.integers(-spread, spread + 1, size=n)
+    if dtype == np.int32:
+        return r.astype(np.int32)
+    return (r % (int(np.iinfo(dtype).max) + 1)).astype(dtype)
+
+
+def test_spec_known_answer():
+    # residuals 0, -1, 1, -2 (uint16 wrap) zigzag to 0, 1, 2, 3: one block of width 2;
+    # bit-plane 0 = samples 1, 3 -> 0b1010, bit-plane 1 = samples 2, 3 -> 0b1100
+    x = np.array([0, 65535, 1, 65534], np.uint16)
+    w, payload = OPK.pack(x)
+    assert w.tolist() == [2] and payload.tolist() == [0b1010, 0b1100]
+    assert np.array_equal(OPK.unpack(w, payload, 4, np.uint16), x)
+    w, payload = OPK.pack(np.zeros(130, np.uint8))  # all-zero blocks take no payload
+    assert w.tolist() == [0, 0, 0] and payload.size == 0
+
+
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32])
+@pytest.mark.parametrize('n', [1, 63, 64, 65, 1000])
+def test_spec_round_trip(dtype, n):
+    rng = np.random.default_rng(n)
+    info = np.iinfo(dtype)
+    x = rng.integers(info.min, int(info.max) + 1, size=n, dtype=np.int64).astype(dtype)
+    x[: n // 2] = _residuals(n // 2, dtype, rng)
+    w, payload = OPK.pack(x)
+    assert len(w) == -(-n // 64) and payload.size == int(w.astype(np.int64).sum())
+    assert w.max() <= np.dtype(dtype).itemsize * 8
+    assert np.array_equal(OPK.unpack(w, payload, n, dtype), x)
+
+
+# --------------------------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32, np.float32])
+@pytest.mark.parametrize('shape', [(1,), (64,), (65,), (3, 17, 19), (2, 4096 * 64 + 5)])
+def test_pack_matches_spec(kom, dtype, shape):
+    rng = np.random.default_rng(sum(shape))
+    if dtype == np.float32:
+        x = rng.standard_normal(shape).astype(np.float32)
+        bits = x.view(np.uint32)
+    else:
+        info = np.iinfo(dtype)
+        x = rng.integers(info.min, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
+        flat = x.reshape(-1)
+        flat[: flat.size // 2] = _residuals(flat.size // 2, dtype, rng, spread=9)
+        bits = x
+    blob = kom.packing.pack(x)
+    assert isinstance(blob, np.ndarray) and blob.dtype == np.uint8
+    w, payload = OPK.pack(bits)
+    head = 40 + 8 * x.ndim
+    nb = len(w)
+    assert np.array_equal(blob[head:head + nb], w)
+    poff = head + (nb + 7) // 8 * 8
+    assert np.array_equal(blob[poff:].view(np.uint64), payload)
+    back = kom.packing.unpack(blob)
+    assert back.dtype == x.dtype and back.shape == x.shape
+    assert np.array_equal(back.view(np.uint8), x.view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_pack_encoded_round_trip_and_ratio(kom):
+    """encode -> pack_encoded -> unpack_encoded -> decode is lossless, and a smooth volume's coded
+    maps shrink (the container's purpose; random data cannot)."""
+    import torch
+    z, y, x = np.meshgrid(*[np.arange(64)] * 3, indexing='ij')
+    smooth = (1000 + 300 * np.sin(x / 9.0) * np.cos(y / 7.0) + 200 * np.sin(z / 11.0)).astype(np.uint16)
+    vol = np.stack([smooth + np.uint16(k) for k in range(8)])[..., None]
+    pred = kom.MeanPredictor(0, 3)
+    for data in (vol, torch.from_numpy(vol).cuda()):
+        lo, enc = kom.volume.encode(pred, kom.volume.encode_values_uint16, data)
+        blob = kom.packing.pack_encoded(lo, enc)
+        lo2, (maps2, dims2) = kom.packing.unpack_encoded(blob)
+        assert tuple(dims2) == tuple(enc[1])
+        rec = kom.volume.decode(pred, kom.volume.decode_values_uint16, lo2, (maps2, dims2))
+        rec = rec.cpu().numpy() if isinstance(rec, torch.Tensor) else rec
+        assert np.array_equal(rec, vol)
+        nbytes = blob.numel() if isinstance(blob, torch.Tensor) else blob.size
+        assert nbytes < 0.5 * vol.nbytes, nbytes / vol.nbytes

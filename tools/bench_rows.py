@@ -180,6 +180,28 @@ def main():
         emit('categorical:encode', 'rank coder encode, L=256', n * (L * 4 + 2), te, cpu)
         emit('categorical:decode', 'rank coder decode, L=256', n * (L * 4 + 2), td)
 
+    # bit-plane container on the coded maps of a smooth C3-shaped volume
+    if not want or 'packing' in want:
+        zz, yy, xx = torch.meshgrid(*[torch.arange(512, device='cuda', dtype=torch.float32)] * 3, indexing='ij')
+        sm = (20000 + 8000 * torch.sin(xx / 23.0) * torch.cos(yy / 17.0) + 6000 * torch.sin(zz / 29.0))
+        sm = (sm + torch.randint(-2, 3, sm.shape, device='cuda')).to(torch.int32).to(torch.uint16)
+        del zz, yy, xx
+        tiles = sm.view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5).reshape(512, 64, 64, 64, 1).contiguous()
+        del sm
+        pred = kom.MeanPredictor(0, 3)
+        lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, tiles)
+        m = maps[3]  # the C map: 32 MiB of u16 residuals
+        blob = kom.packing.pack(m)
+        assert torch.equal(kom.packing.unpack(blob), m)
+        coded = sum(kom.packing.pack(a).numel() for a in (lo, *maps))
+        tp = gpu_time(lambda: kom.packing.pack(m), args.reps)
+        tu = gpu_time(lambda: kom.packing.unpack(blob), args.reps)
+        ratio = round(tiles.numel() * 2 / coded, 3)
+        emit('packing:pack', f'bit-plane pack of a 32 MiB coded map (whole volume ratio {ratio}x)',
+             m.numel() * 2 + blob.numel(), tp)
+        emit('packing:unpack', 'bit-plane unpack of the same map', m.numel() * 2 + blob.numel(), tu)
+        del tiles, lo, maps
+
     # geometry primitives (volume/utils.py) on the C3 tile batch
     if not want or 'primitives' in want:
         hp, _ = _nd.d_pad_highres(vol, 3)                       # [512, 65^3]
