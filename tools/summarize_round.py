@@ -6,7 +6,7 @@ from collections import defaultdict
 src, dst = sys.argv[1], sys.argv[2]
 os.makedirs(dst, exist_ok=True)
 tag = os.path.basename(src.rstrip('/'))
-for name in ('bench', 'bench_image', 'pytest_gpu', 'smoke'):
+for name in ('bench', 'bench_image', 'bench_stream', 'pytest_gpu', 'smoke'):
     f = os.path.join(src, name + '.log')
     if os.path.exists(f):
         shutil.copy(f, os.path.join(dst, f'{tag}_{name}.log'))
