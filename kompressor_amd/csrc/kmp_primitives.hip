@@ -28,6 +28,9 @@ int check_launch(const char* what) {
 
 constexpr int kThreads = 256;
 
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));                // 16-B aligned
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));    // any alignment
+
 static inline unsigned grid_for(int64_t n) {
   int64_t g = ceil_div(n, kThreads);
   if (g > 65536) g = 65536;
@@ -316,6 +319,149 @@ __global__ void __launch_bounds__(kThreads) maps_from_predictions_kernel(const T
   }
 }
 
+// LDS-staged form (C == 1, < 2^30 elements).  A workgroup owns YB frame rows x XO frame columns
+// of ZC consecutive output planes, for all maps, and rolls along z: cell plane z (rows y0-1 ..
+// y0+YB-1, cells ox0-1 .. ox0+XO-1: YB+1 contiguous runs of cells x K channels in HBM) is staged
+// into an LDS ring of two planes with 16-byte loads (row pitch rounded to 16 B, so every LDS
+// store is aligned), and plane z+1 is fetched into registers while plane z's outputs aggregate
+// from LDS.  HBM reads are (YB+1)/YB x (ZC+1)/ZC of the predictions; the per-element kernel
+// above reads the channel-interleaved cells with a 19-element lane stride instead (~19 cache
+// lines per load instruction).  Arithmetic is the same: integer shifts for u8 / u16, the
+// reference's f32 channel-order sum + scale + truncation otherwise.
+constexpr int kMfpCpt = 8;  // 16-byte chunks per thread per staged plane (host-checked)
+
+__device__ __forceinline__ void divmod_small(int32_t i, int32_t n, float rcp, int32_t& q, int32_t& r) {
+  q = (int32_t)((float)i * rcp);  // i < 2^21: off by at most one
+  r = i - q * n;
+  if (r < 0) { --q; r += n; } else if (r >= n) { ++q; r -= n; }
+}
+
+template <typename T, int NSP>
+__global__ void __launch_bounds__(kThreads) maps_from_predictions_lds_kernel(
+    const T* __restrict__ preds, int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs, int32_t YB, int32_t XO,
+    int32_t ZC, int32_t nzc, int32_t nyb, int32_t nxb, int32_t RP, int32_t nchunk, float rcp_nchunk,
+    int64_t total_elems) {
+  constexpr int NM = NSP == 3 ? 7 : 3, K = NSP == 3 ? 19 : 5;
+  constexpr int V = 16 / (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* lds = (T*)smem;
+  int32_t w = (int32_t)blockIdx.x;
+  const int32_t xb = w % nxb; w /= nxb;
+  const int32_t yb = w % nyb; w /= nyb;
+  const int32_t zc = w % nzc;
+  const int32_t b = w / nzc;
+  const int32_t y0 = yb * YB, ox0 = xb * XO;
+  const int32_t xc0 = ox0 > 0 ? ox0 - 1 : 0;
+  const int32_t xc1 = (ox0 + XO - 1 < Lcx - 1) ? ox0 + XO - 1 : Lcx - 1;  // last staged cell
+  const int32_t nxc_k = (xc1 - xc0 + 1) * K;                                // staged elements per row
+  const int32_t cz = NSP == 3 ? Lcz : 1;
+  const int32_t fz = NSP == 3 ? Lcz + 1 : 1;
+  const int32_t oz0 = zc * ZC, oz1 = (oz0 + ZC < fz) ? oz0 + ZC : fz;  // output planes [oz0, oz1)
+  const int32_t slice_work = (YB + 1) * nchunk;
+
+  u32x4v buf[kMfpCpt];
+  auto fetch = [&](int32_t z) {  // cell plane z -> registers
+#pragma unroll
+    for (int c = 0; c < kMfpCpt; ++c) {
+      buf[c] = u32x4v{0u, 0u, 0u, 0u};
+      const int32_t i = threadIdx.x + c * kThreads;
+      if (i >= slice_work) continue;
+      int32_t r, ch;
+      divmod_small(i, nchunk, rcp_nchunk, r, ch);
+      const int32_t y = y0 - 1 + r;
+      if (y < 0 || y >= Lcy || ch * V >= nxc_k) continue;
+      const int64_t g = ((((int64_t)b * cz + z) * Lcy + y) * Lcx + xc0) * K + (int64_t)ch * V;
+      if (g + V <= total_elems) {
+        buf[c] = *(const u32x4u*)(preds + g);
+      } else {
+        T* bt = (T*)&buf[c];
+        for (int e = 0; e < V && g + e < total_elems; ++e) bt[e] = preds[g + e];
+      }
+    }
+  };
+  auto put = [&](int32_t z) {  // registers -> ring slot z & 1
+    T* base = lds + (z & 1) * (YB + 1) * RP;
+#pragma unroll
+    for (int c = 0; c < kMfpCpt; ++c) {
+      const int32_t i = threadIdx.x + c * kThreads;
+      if (i >= slice_work) continue;
+      int32_t r, ch;
+      divmod_small(i, nchunk, rcp_nchunk, r, ch);
+      *(u32x4v*)(base + r * RP + ch * V) = buf[c];
+    }
+  };
+  auto at = [&](int32_t z, int32_t r, int32_t x, int ch) -> T {  // cell (z, y0-1+r, x), channel ch
+    return lds[((z & 1) * (YB + 1) + r) * RP + (x - xc0) * K + ch];
+  };
+
+  // prologue: cell plane oz0 - 1 (3D, when it exists) and oz0
+  if (NSP == 3 && oz0 >= 1) {
+    fetch(oz0 - 1);
+    put(oz0 - 1);
+  }
+  if (oz0 < cz) {
+    fetch(oz0);
+    put(oz0);
+  }
+  __syncthreads();
+
+  for (int32_t oz = oz0; oz < oz1; ++oz) {
+    const bool more = oz + 1 < oz1 && oz + 1 < cz;
+    if (more) fetch(oz + 1);  // in flight while plane oz aggregates
+    for (int32_t i = threadIdx.x; i < YB * XO; i += kThreads) {
+      const int32_t xo = i % XO, r = i / XO;
+      const int32_t oy = y0 + r, ox = ox0 + xo;
+      if (oy > Lcy || ox > Lcx) continue;
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        int par[3];
+        map_parity(NSP, k, par);
+        const int32_t e0 = NSP == 3 ? (par[0] ? Lcz : Lcz + 1) : 1, e1 = par[1] ? Lcy : Lcy + 1,
+                      e2 = par[2] ? Lcx : Lcx + 1;
+        if (oz >= e0 || oy >= e1 || ox >= e2) continue;
+        Contrib c[4];
+        const int nc = map_contribs(NSP, k, c);
+        T v;
+        if constexpr (sizeof(T) <= 2 && !std::is_same<T, float>::value) {
+          uint32_t sum = 0, cnt = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (j >= nc) break;
+            const int32_t z = oz - c[j].dz, y = oy - c[j].dy, x = ox - c[j].dx;
+            if (z >= 0 && z < cz && y >= 0 && y < Lcy && x >= 0 && x < Lcx) {
+              sum += at(z, r + 1 - c[j].dy, x, c[j].ch);
+              ++cnt;
+            }
+          }
+          v = (T)(k == center_map(NSP) ? sum : sum >> (cnt >> 1));
+        } else if (k == center_map(NSP)) {
+          v = at(oz, r + 1, ox, c[0].ch);
+        } else {
+          float sum = 0.0f;
+          int cnt = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (j >= nc) break;
+            const int32_t z = oz - c[j].dz, y = oy - c[j].dy, x = ox - c[j].dx;
+            if (z >= 0 && z < cz && y >= 0 && y < Lcy && x >= 0 && x < Lcx) {
+              sum += (float)at(z, r + 1 - c[j].dy, x, c[j].ch);
+              ++cnt;
+            }
+          }
+          if (cnt == 4) sum *= 0.25f;
+          else if (cnt == 2) sum *= 0.5f;
+          v = cast_f32<T>(sum);
+        }
+        ((T*)outs.p[k])[((b * e0 + oz) * e1 + oy) * e2 + ox] = v;
+      }
+    }
+    if (!more) break;  // uniform
+    __syncthreads();  // plane oz - 1's slot is free
+    put(oz + 1);
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Mean predictor on a padded lowres window (tests/volume/test_encode_decode.py:46-53):
 // cell mean = astype(T)(f32 sum of the (2p+2)^d neighbourhood / N), then the map aggregation.
@@ -449,8 +595,6 @@ __global__ void __launch_bounds__(kThreads) pad_kernel(const T* __restrict__ in,
 // ------------------------------------------------------------------------------------------
 // 16-byte vector form for operands and result of one element size (the common case: the coder
 // of the sample dtype on same-dtype predictions), 16-byte aligned; ``n16`` vectors.
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-
 template <int DIR, int CODER, typename TV>
 __global__ void __launch_bounds__(kThreads) code_vec_kernel(const u32x4v* __restrict__ pred,
                                                           const u32x4v* __restrict__ x, int64_t n16,
@@ -506,6 +650,178 @@ __global__ void __launch_bounds__(kThreads) copy_box_kernel(const TI* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
+// Row kernels (C == 1, < 2^31 elements): one work item = V = 16 / sizeof(T) consecutive outputs
+// of one row.  The row decomposition (3 divisions) is paid once per 16 bytes instead of once per
+// element, and interior chunks move as one 16-byte load / store per lane.  Rows of these arrays
+// have odd lengths (65, 33, ...), so row starts are only element-aligned: the vectors are
+// declared byte-aligned and gfx950 serves them as unaligned dwordx4 accesses.  Partial chunks
+// and mirrored edges fall back to per-element accesses inside the same item.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+struct Vec16 {
+  static constexpr int V = 16 / (int)sizeof(T);
+  T e[V];
+  __device__ __forceinline__ void load(const T* p) {
+    const u32x4u v = *(const u32x4u*)p;
+    __builtin_memcpy(e, &v, 16);
+  }
+  __device__ __forceinline__ void store(T* p) const {
+    u32x4u v;
+    __builtin_memcpy(&v, e, 16);
+    *(u32x4u*)p = v;
+  }
+};
+
+struct RowItem {
+  int32_t b, z, y, j;
+};
+// item t over [B, nz, ny, nch] (all extents >= 1)
+__device__ __forceinline__ RowItem row_item(uint32_t t, uint32_t nz, uint32_t ny, uint32_t nch) {
+  RowItem r;
+  r.j = (int32_t)(t % nch); t /= nch;
+  r.y = (int32_t)(t % ny); t /= ny;
+  r.z = (int32_t)(t % nz);
+  r.b = (int32_t)(t / nz);
+  return r;
+}
+
+// jnp.pad rows: out[b, z, y, x] = in[b, m(z - lz), m(y - ly), m(x - lx)]
+template <typename T>
+__global__ void __launch_bounds__(kThreads) rows_pad_kernel(const T* __restrict__ in, E3<int32_t> n, E3<int32_t> lo,
+                                                          E3<int32_t> oe, int mode, T* __restrict__ out, int32_t nch,
+                                                          int32_t items) {
+  constexpr int V = Vec16<T>::V;
+  auto m = [&](int32_t i, int32_t ext) { return (i >= 0 && i < ext) ? i : (mode == 0 ? sym_idx<int32_t>(i, ext)
+                                                                                      : reflect_index<int32_t>(i, ext)); };
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, oe.e[0], oe.e[1], nch);
+    const int32_t sz = m(q.z - lo.e[0], n.e[0]), sy = m(q.y - lo.e[1], n.e[1]);
+    const T* src = in + ((q.b * n.e[0] + sz) * n.e[1] + sy) * n.e[2];
+    T* dst = out + ((q.b * oe.e[0] + q.z) * oe.e[1] + q.y) * oe.e[2];
+    const int32_t x0 = q.j * V, s0 = x0 - lo.e[2];
+    if (x0 + V <= oe.e[2] && s0 >= 0 && s0 + V <= n.e[2]) {
+      Vec16<T> v;
+      v.load(src + s0);
+      v.store(dst + x0);
+    } else {
+      for (int32_t x = x0; x < x0 + V && x < oe.e[2]; ++x) dst[x] = src[m(x - lo.e[2], n.e[2])];
+    }
+  }
+}
+
+// Parity split of highres rows (lowres_from_highres / maps_from_highres): item = (b, hz, hy)
+// highres row (every ``step``-th when only the lowres is wanted), chunk j = highres x in
+// [2jV, 2jV + 2V): even x -> class (pz, py, 0), odd x -> class (pz, py, 1).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) rows_deinterleave_kernel(const T* __restrict__ in, E3<int32_t> n, int nsp,
+                                                                   int step, T* lowres, MapPtrs outs, int32_t nch,
+                                                                   int32_t items) {
+  constexpr int V = Vec16<T>::V;
+  const int32_t rz = (n.e[0] + step - 1) / step, ry = (n.e[1] + step - 1) / step;
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, rz, ry, nch);
+    const int32_t hz = q.z * step, hy = q.y * step;
+    const int pz = (nsp == 3) ? (hz & 1) : 0, py = hy & 1;
+    T* dst[2] = {nullptr, nullptr};
+    int32_t ex[2];
+    int32_t ez = nsp == 3 ? (pz ? n.e[0] / 2 : (n.e[0] + 1) / 2) : 1, ey = py ? n.e[1] / 2 : (n.e[1] + 1) / 2;
+    ex[0] = (n.e[2] + 1) / 2;
+    ex[1] = n.e[2] / 2;
+    const int32_t orow = (q.b * ez + (hz >> 1)) * ey + (hy >> 1);
+    if (pz == 0 && py == 0 && lowres) dst[0] = (T*)lowres + orow * ex[0];
+    if (outs.p[0]) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        if (k >= (nsp == 3 ? 7 : 3)) break;
+        int par[3];
+        map_parity(nsp, k, par);
+        if (par[0] == pz && par[1] == py) dst[par[2]] = (T*)outs.p[k] + orow * ex[par[2]];
+      }
+    }
+    const T* src = in + ((q.b * n.e[0] + hz) * n.e[1] + hy) * n.e[2];
+    const int32_t x0 = q.j * V;
+    if (2 * x0 + 2 * V <= n.e[2]) {
+      Vec16<T> a, b, ev, od;
+      a.load(src + 2 * x0);
+      b.load(src + 2 * x0 + V);
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        ev.e[i] = a.e[2 * i]; od.e[i] = a.e[2 * i + 1];
+        ev.e[V / 2 + i] = b.e[2 * i]; od.e[V / 2 + i] = b.e[2 * i + 1];
+      }
+      if (dst[0]) ev.store(dst[0] + x0);
+      if (dst[1]) od.store(dst[1] + x0);
+    } else {
+      for (int32_t x = 2 * x0; x < 2 * x0 + 2 * V && x < n.e[2]; ++x)
+        if (dst[x & 1]) dst[x & 1][x >> 1] = src[x];
+    }
+  }
+}
+
+// Parity merge (highres_from_lowres_and_maps): item = highres row (b, hz, hy), chunk j = highres x
+// in [2jV, 2jV + 2V) from class (pz, py, 0) (lowres when pz = py = 0) and class (pz, py, 1).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) rows_interleave_kernel(const T* __restrict__ lowres, CMapPtrs maps,
+                                                                 E3<int32_t> L, int nsp, T* __restrict__ out,
+                                                                 int32_t nch, int32_t items) {
+  constexpr int V = Vec16<T>::V;
+  const int32_t h0 = 2 * L.e[0] - 1, h1 = 2 * L.e[1] - 1, h2 = 2 * L.e[2] - 1;
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, h0, h1, nch);
+    const int pz = (nsp == 3) ? (q.z & 1) : 0, py = q.y & 1;
+    const T* srcp[2] = {nullptr, nullptr};
+    const int32_t ez = nsp == 3 ? (pz ? L.e[0] - 1 : L.e[0]) : 1, ey = py ? L.e[1] - 1 : L.e[1];
+    const int32_t ex[2] = {L.e[2], L.e[2] - 1};
+    const int32_t irow = (q.b * ez + (q.z >> 1)) * ey + (q.y >> 1);
+    if (pz == 0 && py == 0) srcp[0] = lowres + irow * ex[0];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k >= (nsp == 3 ? 7 : 3)) break;
+      int par[3];
+      map_parity(nsp, k, par);
+      if (par[0] == pz && par[1] == py) srcp[par[2]] = (const T*)maps.p[k] + irow * ex[par[2]];
+    }
+    T* dst = out + ((q.b * h0 + q.z) * h1 + q.y) * h2;
+    const int32_t x0 = q.j * V;
+    if (x0 + V <= ex[1]) {
+      Vec16<T> ev, od, a, b;
+      ev.load(srcp[0] + x0);
+      od.load(srcp[1] + x0);
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        a.e[2 * i] = ev.e[i]; a.e[2 * i + 1] = od.e[i];
+        b.e[2 * i] = ev.e[V / 2 + i]; b.e[2 * i + 1] = od.e[V / 2 + i];
+      }
+      a.store(dst + 2 * x0);
+      b.store(dst + 2 * x0 + V);
+    } else {
+      for (int32_t x = 2 * x0; x < 2 * x0 + 2 * V && x < h2; ++x) dst[x] = srcp[x & 1][x >> 1];
+    }
+  }
+}
+
+// Same-dtype box copy (slicing / .at[box].set of the chunk driver, trims)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) rows_copy_kernel(const T* __restrict__ in, E3<int32_t> ie, E3<int32_t> io,
+                                                           T* __restrict__ out, E3<int32_t> oe, E3<int32_t> oo,
+                                                           E3<int32_t> ext, int32_t nch, int32_t items) {
+  constexpr int V = Vec16<T>::V;
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, ext.e[0], ext.e[1], nch);
+    const T* src = in + ((q.b * ie.e[0] + io.e[0] + q.z) * ie.e[1] + io.e[1] + q.y) * ie.e[2] + io.e[2];
+    T* dst = out + ((q.b * oe.e[0] + oo.e[0] + q.z) * oe.e[1] + oo.e[1] + q.y) * oe.e[2] + oo.e[2];
+    const int32_t x0 = q.j * V;
+    if (x0 + V <= ext.e[2]) {
+      Vec16<T> v;
+      v.load(src + x0);
+      v.store(dst + x0);
+    } else {
+      for (int32_t x = x0; x < ext.e[2]; ++x) dst[x] = src[x];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // C-ABI helpers
 // ------------------------------------------------------------------------------------------
 static inline Ext3 ext_from(int nsp, const int64_t* shape) {
@@ -525,6 +841,18 @@ static int with_index(bool small, F&& f) {
   return small ? f(int32_t{}) : f(int64_t{});
 }
 static inline int64_t vol(int64_t B, const Ext3& e, int64_t C) { return B * e.e[0] * e.e[1] * e.e[2] * C; }
+
+// the row kernels serve C == 1 arrays below 2^30 elements (KMP_DISABLE_ROWS=1: element kernels)
+static bool rows_ok(int64_t C, std::initializer_list<int64_t> counts) {
+  static const bool off = [] {
+    const char* v = std::getenv("KMP_DISABLE_ROWS");
+    return v && std::atoi(v);
+  }();
+  return !off && C == 1 && fits32(counts);
+}
+static inline E3<int32_t> e32(const Ext3& x) { return e3<int32_t>(x); }
+template <typename T>
+static inline int32_t row_chunks(int64_t n) { return (int32_t)ceil_div(n, 16 / (int64_t)sizeof(T)); }
 
 static inline int check_common(int nsp, int64_t B, const int64_t* shape, int64_t C) {
   KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
@@ -581,6 +909,13 @@ int kmp_lowres_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t 
   MapPtrs none{};
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
+    if (rows_ok(C, {vol(B, n, C)})) {
+      const int32_t nch = row_chunks<T>((n.e[2] + 1) / 2);
+      const int64_t items = B * ((n.e[0] + 1) / 2) * ((n.e[1] + 1) / 2) * nch;
+      rows_deinterleave_kernel<T><<<grid_for(items), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)in, e32(n), nsp, 2, (T*)out, none, nch, (int32_t)items);
+      return check_launch("lowres_from_highres");
+    }
     return with_index(fits32({vol(B, n, C)}), [&](auto itag) {
       using I = decltype(itag);
       deinterleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
@@ -604,6 +939,13 @@ int kmp_maps_from_highres(int32_t nsp, int32_t dtype, const void* in, int64_t B,
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
+    if (rows_ok(C, {vol(B, n, C)})) {
+      const int32_t nch = row_chunks<T>((n.e[2] + 1) / 2);
+      const int64_t items = B * n.e[0] * n.e[1] * nch;
+      rows_deinterleave_kernel<T><<<grid_for(items), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)in, e32(n), nsp, 1, nullptr, outs, nch, (int32_t)items);
+      return check_launch("maps_from_highres");
+    }
     return with_index(fits32({vol(B, n, C)}), [&](auto itag) {
       using I = decltype(itag);
       deinterleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(
@@ -647,6 +989,13 @@ int kmp_highres_from_lowres_and_maps(int32_t nsp, int32_t dtype, const void* low
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     const Ext3 H{{2 * L.e[0] - 1, 2 * L.e[1] - 1, 2 * L.e[2] - 1}};
+    if (rows_ok(C, {vol(B, H, C)})) {
+      const int32_t nch = row_chunks<T>(L.e[2]);
+      const int64_t items = B * H.e[0] * H.e[1] * nch;
+      rows_interleave_kernel<T><<<grid_for(items), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)lowres, mp, e32(L), nsp, (T*)out, nch, (int32_t)items);
+      return check_launch("highres_from_lowres_and_maps");
+    }
     return with_index(fits32({vol(B, H, C)}), [&](auto itag) {
       using I = decltype(itag);
       interleave_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)lowres, mp, (I)B,
@@ -709,6 +1058,30 @@ int kmp_maps_from_predictions(int32_t nsp, int32_t dtype, const void* preds, int
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     const bool small = fits32({vol(B, ce, C) * (nsp == 3 ? 19 : 5), total});
+    if (rows_ok(C, {vol(B, ce, C) * (nsp == 3 ? 19 : 5), total})) {
+      constexpr int V = 16 / (int)sizeof(T);
+      const int K = nsp == 3 ? 19 : 5, NS = nsp == 3 ? 2 : 1;
+      const int32_t XO = (int32_t)std::min<int64_t>(ce.e[2] + 1, 64);
+      const char* yb_env = std::getenv("KMP_MFP_YB");
+      const int32_t YB = yb_env ? std::max(1, std::atoi(yb_env)) : std::max(1, std::min(8, kThreads / XO));
+      const int32_t nyb = (int32_t)ceil_div(ce.e[1] + 1, YB), nxb = (int32_t)ceil_div(ce.e[2] + 1, XO);
+      const int32_t nchunk = (int32_t)ceil_div((int64_t)(XO + 1) * K, V);
+      const int32_t RP = nchunk * V;
+      // enough workgroups to fill the chip: split the z roll into nzc runs of ZC output planes
+      const int64_t fz = nsp == 3 ? ce.e[0] + 1 : 1;
+      const char* want_env = std::getenv("KMP_MFP_WANT");
+      const int64_t want = ceil_div(want_env ? std::atoi(want_env) : 4096, B * nyb * nxb);
+      const int32_t ZC = (int32_t)ceil_div(fz, std::max<int64_t>(1, std::min<int64_t>(want, fz)));
+      const int32_t nzc = (int32_t)ceil_div(fz, ZC);
+      const size_t lds = (size_t)NS * (YB + 1) * RP * sizeof(T);
+      const int64_t nblk = B * nzc * nyb * nxb;
+      if ((int64_t)(YB + 1) * nchunk > kThreads * kMfpCpt) return fail(KMP_ERR_ARG, "maps_from_predictions: tile");
+      auto kern = nsp == 3 ? maps_from_predictions_lds_kernel<T, 3> : maps_from_predictions_lds_kernel<T, 2>;
+      kern<<<(unsigned)nblk, kThreads, lds, (hipStream_t)stream>>>(
+          (const T*)preds, (int32_t)ce.e[0], (int32_t)ce.e[1], (int32_t)ce.e[2], outs, YB, XO, ZC, nzc, nyb, nxb, RP,
+          nchunk, 1.0f / (float)nchunk, vol(B, ce, C) * K);
+      return check_launch("maps_from_predictions");
+    }
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
       if (small && C == 1) {
         auto kern = nsp == 3 ? maps_from_predictions_int_kernel<T, 3> : maps_from_predictions_int_kernel<T, 2>;
@@ -792,6 +1165,13 @@ int kmp_pad(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
+    if (rows_ok(C, {vol(B, n, C), total})) {
+      const int32_t nch = row_chunks<T>(oe.e[2]);
+      const int64_t items = B * oe.e[0] * oe.e[1] * nch;
+      rows_pad_kernel<T><<<grid_for(items), kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)in, e32(n), e32(lo), e32(oe), mode, (T*)out, nch, (int32_t)items);
+      return check_launch("pad");
+    }
     return with_index(fits32({vol(B, n, C), total}), [&](auto itag) {
       using I = decltype(itag);
       pad_kernel<T, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>((const T*)in, (I)B, e3<I>(n), (I)C,
@@ -824,6 +1204,15 @@ int kmp_copy_box(int32_t nsp, int32_t in_dtype, const void* in, const int64_t in
     using TI = decltype(itag);
     return dispatch_any_dtype(out_dtype, [&](auto otag) {
       using TO = decltype(otag);
+      if constexpr (std::is_same<TI, TO>::value) {
+        if (rows_ok(C, {vol(B, ie, C), vol(B, oe, C)})) {
+          const int32_t nch = row_chunks<TI>(ee.e[2]);
+          const int64_t items = B * ee.e[0] * ee.e[1] * nch;
+          rows_copy_kernel<TI><<<grid_for(items), kThreads, 0, (hipStream_t)stream>>>(
+              (const TI*)in, e32(ie), e32(io), (TO*)out, e32(oe), e32(oo), e32(ee), nch, (int32_t)items);
+          return check_launch("copy_box");
+        }
+      }
       return with_index(fits32({vol(B, ie, C), vol(B, oe, C)}), [&](auto itag) {
         using I = decltype(itag);
         copy_box_kernel<TI, TO, I><<<grid_for(total), kThreads, 0, (hipStream_t)stream>>>(

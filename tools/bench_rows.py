@@ -220,8 +220,13 @@ def main():
              gpu_time(lambda: _nd.d_features_from_lowres(lowres, 0, 3), args.reps))
         preds = feats[..., :1, :].expand(*feats.shape[:4], 19, 1).contiguous()
         mp = _nd.d_maps_from_predictions(preds, 3)
-        emit('maps_from_predictions', 'f32 19-way aggregation', preds.numel() * 2 + sum(m.numel() * 2 for m in mp),
+        emit('maps_from_predictions', 'u16 predictions, 19-way f32-order aggregation', preds.numel() * 2 + sum(m.numel() * 2 for m in mp),
              gpu_time(lambda: _nd.d_maps_from_predictions(preds, 3), args.reps))
+        pf = preds.to(torch.float32)
+        mpf = _nd.d_maps_from_predictions(pf, 3)
+        emit('maps_from_predictions_f32', 'f32 predictions (a network output) -> f32 maps',
+             pf.numel() * 4 + sum(m.numel() * 4 for m in mpf), gpu_time(lambda: _nd.d_maps_from_predictions(pf, 3), args.reps))
+        del pf, mpf
         volume = vol.view(8, 8, 8, 64, 64, 64).permute(0, 3, 1, 4, 2, 5).reshape(512, 512, 512, 1)
         emit('tiles:split', '512^3 volume -> 512 x 64^3', 2 * raw_v,
              gpu_time(lambda: kom.tiles.volume_to_tiles(volume, 64), args.reps))
