@@ -243,6 +243,11 @@ int kmp_pack_plan(int32_t dtype, const void* x, int64_t n, uint8_t* widths, void
 int kmp_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* widths, const void* workspace,
              uint64_t* payload, kmp_stream_t stream);
 /* block offsets from stored widths, then the samples */
+/* container header bytes written by a kernel (no host copy): dst[0:len) = bytes (len <= 128),  */
+/* dst[zero_from:zero_to) = 0, and, when words_at >= 0, the u64 payload word count of the last    */
+/* kmp_pack_plan on ``workspace`` (n samples) at dst + words_at -- stream-ordered after the plan */
+int kmp_pack_header(uint8_t* dst, const uint8_t* bytes, int32_t len, int64_t zero_from, int64_t zero_to,
+                    const void* workspace, int64_t n, int64_t words_at, kmp_stream_t stream);
 int kmp_unpack_plan(const uint8_t* widths, int64_t n, void* workspace, kmp_stream_t stream);
 int kmp_unpack(int32_t dtype, const uint64_t* payload, int64_t n, const uint8_t* widths, const void* workspace,
                void* out, kmp_stream_t stream);

@@ -16,6 +16,7 @@ namespace kmp {
 
 constexpr int kCatWaves = 4;
 constexpr int kCatStage = 1024;  // logits staged in LDS per wave (longer rows read global memory)
+constexpr uint32_t kCatSmallRank = 8;  // decode: ranks below this peel maxima instead of a radix select
 
 __device__ __forceinline__ bool cat_less(float a, float b) {  // a sorts before b
   const bool na = a != a, nb = b != b;
@@ -94,86 +95,90 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_kernel(const float
 }
 
 
-// ---- decode by a wave-wide bitonic sort (L <= 64 * E) ----------------------------------------
-// The descending rank of class i is #{j : key_j > key_i or (key_j == key_i and j > i)}, i.e. the
-// position of the combined 64-bit key (key_i << 32 | i) in DESCENDING order of all combined keys.
-// key is the float mapped to an order-preserving uint32 (-0 -> +0, every NaN -> 0xffffffff: NaN
-// after every number, NaNs equal -- the cat_less / cat_equal order).  The wave sorts its E
-// combined keys per lane (blocked layout, element p = lane * E + e) with a bitonic network --
-// in-register compare-exchange for partner distances < E, xor shuffles above -- and reads the
-// class at position k.  O(L log^2 L) per element instead of the counting kernel's O(L^2).
+// ---- decode by a wave-wide radix select (L <= 64 * E) -----------------------------------------
+// The descending rank of class i is #{j : key_j > key_i or (key_j == key_i and j > i)}, where key
+// is the float mapped to an order-preserving uint32 (-0 -> +0, every NaN -> 0xffffffff: NaN after
+// every number, NaNs equal -- the cat_less / cat_equal order).  Lane l holds classes e * 64 + l.
+// The class of rank k: the largest threshold T with #{key >= T} >= k + 1, found bit by bit from
+// the top (32 rounds of E ballots + popcounts), is the (k+1)-th largest key; among the classes
+// with key == T the answer is the (k - #{key > T})-th highest index.  O(32 E) per element instead
+// of a sorting network's O(L log^2 L).
 __device__ __forceinline__ uint32_t order_key(float f) {
   if (f != f) return 0xffffffffu;
   uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 template <typename T, int E>
-__global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_sort_kernel(const float* __restrict__ logits,
-                                                                                int64_t n, int64_t L,
-                                                                                const T* __restrict__ x,
-                                                                                T* __restrict__ out) {
-  constexpr int NE = 64 * E;
-  __shared__ uint32_t pos_idx[kCatWaves][NE];
+__global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_select_kernel(const float* __restrict__ logits,
+                                                                                  int64_t n, int64_t L,
+                                                                                  const T* __restrict__ x,
+                                                                                  T* __restrict__ out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int64_t el = (int64_t)blockIdx.x * kCatWaves + w; el < n; el += (int64_t)gridDim.x * kCatWaves) {
     const float* row = logits + el * L;
-    uint64_t v[E];
+    uint32_t key[E];
+    bool ok[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      v[e] = i < L ? (((uint64_t)order_key(row[i]) << 32) | (uint32_t)i) : 0ull;  // padding sorts last
+      const int i = e * 64 + lane;
+      ok[e] = i < L;
+      key[e] = ok[e] ? order_key(row[i]) : 0u;
     }
-    // bitonic network, descending overall
+    int64_t kk = (int64_t)(std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el]);
+    const uint32_t k = (uint32_t)(kk < 0 ? 0 : (kk >= L ? L - 1 : kk));
+    auto count = [&](auto pred) {  // wave-uniform #{valid classes with pred(key)}
+      uint32_t c = 0;
 #pragma unroll
-    for (int k = 2; k <= NE; k <<= 1) {
+      for (int e = 0; e < E; ++e) c += __popcll(__ballot(ok[e] && pred(key[e])));
+      return c;
+    };
+    uint32_t t = 0, m = 0;
+    if (k < kCatSmallRank) {
+      // small ranks (a good predictor's usual case): peel the k + 1 largest keys one at a time;
+      // t = the (k+1)-th largest key, m = how many classes with key t rank before the answer
+      uint64_t above = 1ull << 32;   // keys >= above are used up
+      uint32_t taken = 0;            // classes peeled so far
+      while (true) {
+        uint32_t best = 0;
+        bool any = false;
 #pragma unroll
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        if (j < E) {
+        for (int e = 0; e < E; ++e)
+          if (ok[e] && (uint64_t)key[e] < above) { best = key[e] > best || !any ? key[e] : best; any = true; }
+        const bool lane_any = any;
+        uint32_t wmax = lane_any ? best : 0u;
 #pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const int pe = e ^ j;
-            if (pe > e) {
-              const int p = lane * E + e;
-              const bool desc = (p & k) == 0;  // this block sorts descending
-              const uint64_t a = v[e], b = v[pe];
-              const bool sw = desc ? (a < b) : (a > b);
-              v[e] = sw ? b : a;
-              v[pe] = sw ? a : b;
-            }
-          }
-        } else {
-          const int m = j / E;  // partner lane distance
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const int p = lane * E + e;
-            const uint64_t o = shfl_xor64(v[e], m);
-            const bool lower = (p & j) == 0;  // p < partner
-            const bool desc = (p & k) == 0;
-            // keep the larger of the pair at the lower position in a descending block
-            const bool keep_max = (lower == desc);
-            v[e] = keep_max ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
-          }
+        for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off, 64));
+        const uint32_t ties = count([&](uint32_t v) { return v == wmax; });
+        if (taken + ties > k) {
+          t = wmax;
+          m = k - taken;
+          break;
         }
+        taken += ties;
+        above = wmax;
       }
+    } else {
+#pragma unroll 4
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = t | (1u << bit);
+        if (count([&](uint32_t v) { return v >= cand; }) >= k + 1) t = cand;
+      }
+      m = k - count([&](uint32_t v) { return v > t; });
     }
+    int64_t cls = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e) pos_idx[w][lane * E + e] = (uint32_t)v[e];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane == 0) {
-      int64_t k = (int64_t)(std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el]);
-      k = k < 0 ? 0 : (k >= L ? L - 1 : k);
-      out[el] = (T)pos_idx[w][k];
+    for (int e = E - 1; e >= 0; --e) {  // m-th highest class index with key == t
+      uint64_t word = __ballot(ok[e] && key[e] == t);
+      const uint32_t c = (uint32_t)__popcll(word);
+      if (m < c) {
+        for (uint32_t s = 0; s < m; ++s) word &= ~(1ull << (63 - __clzll(word)));
+        cls = e * 64 + (63 - __clzll(word));
+        break;
+      }
+      m -= c;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane == 0) out[el] = (T)cls;
   }
 }
 
@@ -195,16 +200,16 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
       categorical_kernel<T, KMP_ENCODE><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L, (const T*)x,
                                                                                           (T*)out);
     else if (L <= 64)
-      categorical_decode_sort_kernel<T, 1><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+      categorical_decode_select_kernel<T, 1><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
                                                                                              (const T*)x, (T*)out);
     else if (L <= 128)
-      categorical_decode_sort_kernel<T, 2><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+      categorical_decode_select_kernel<T, 2><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
                                                                                              (const T*)x, (T*)out);
     else if (L <= 256)
-      categorical_decode_sort_kernel<T, 4><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+      categorical_decode_select_kernel<T, 4><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
                                                                                              (const T*)x, (T*)out);
     else if (L <= 512)
-      categorical_decode_sort_kernel<T, 8><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
+      categorical_decode_select_kernel<T, 8><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L,
                                                                                              (const T*)x, (T*)out);
     else
       categorical_kernel<T, KMP_DECODE><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L, (const T*)x,

@@ -36,39 +36,46 @@ def _pad8(n):
     return (n + 7) // 8 * 8
 
 
-def _host_bytes(b):
-    return torch.tensor(list(b), dtype=torch.uint8).to('cuda')
+def _device_bytes(b):
+    """A device uint8 tensor holding ``b`` (<= 128 bytes), written by a kernel, no host copy."""
+    out = dev.empty((len(b),), torch.uint8)
+    check(lib.kmp_pack_header(out.data_ptr(), b, len(b), 0, 0, None, 0, -1, dev.stream()), 'pack')
+    return out
 
 
 def _pack_device(t):
+    """Plan (block widths + scan) and pack straight into a worst-case-sized blob, then ONE host
+    synchronisation to learn the payload length; the blob returned is a view of that buffer."""
     t = t.contiguous()
     code = dev.dtype_code(t)
     n = t.numel()
     nb = int(lib.kmp_pack_blocks(n))
     ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    widths = dev.empty((max(nb, 1),), torch.uint8)
-    check(lib.kmp_pack_plan(code, t.data_ptr(), n, widths.data_ptr(), ws.data_ptr(), dev.stream()), 'pack')
-    toff = int(lib.kmp_pack_total_offset(n))
-    words = int(ws[toff:toff + 8].view(torch.int64).item())  # the one host synchronisation
-    head = _HEAD.pack(ARRAY_MAGIC, VERSION, code, t.dim(), 0, n, nb, words) + struct.pack(f'<{t.dim()}q', *t.shape)
+    head = _HEAD.pack(ARRAY_MAGIC, VERSION, code, t.dim(), 0, n, nb, 0) + struct.pack(f'<{t.dim()}q', *t.shape)
     woff = len(head)
     poff = woff + _pad8(nb)
-    out = torch.zeros((poff + 8 * words,), dtype=torch.uint8, device='cuda')
-    out[:woff].copy_(_host_bytes(head))
-    if nb:
-        out[woff:woff + nb].copy_(widths[:nb])
-    check(lib.kmp_pack(code, t.data_ptr(), n, widths.data_ptr(), ws.data_ptr(), out.data_ptr() + poff, dev.stream()),
+    cap = poff + nb * t.element_size() * 64  # every block at full width
+    out = dev.empty((cap,), torch.uint8)
+    wptr = out.data_ptr() + woff
+    check(lib.kmp_pack_plan(code, t.data_ptr(), n, wptr, ws.data_ptr(), dev.stream()), 'pack')
+    check(lib.kmp_pack(code, t.data_ptr(), n, wptr, ws.data_ptr(), out.data_ptr() + poff, dev.stream()), 'pack')
+    # header + widths padding + the scan's word count (offset 32), from kernel arguments
+    check(lib.kmp_pack_header(out.data_ptr(), head, len(head), woff + nb, poff, ws.data_ptr(), n, 32, dev.stream()),
           'pack')
-    return out
+    words = int(out[32:40].view(torch.int64).item())  # the one host synchronisation
+    return out[:poff + 8 * words]
 
 
 def _parse_array(b):
-    """(dtype code, shape, n, nb, widths offset, payload offset, total bytes) of an array blob."""
-    head = bytes(b[:_HEAD.size].cpu().numpy())
-    magic, version, code, ndim, _, n, nb, words = _HEAD.unpack(head)
-    if magic != ARRAY_MAGIC or version != VERSION:
+    """(dtype code, shape, n, nb, widths offset, payload offset, total bytes) of an array blob:
+    one device-to-host read of the header."""
+    hb = bytes(b[:min(b.numel(), _HEAD.size + 8 * 8)].cpu().numpy())
+    if len(hb) < _HEAD.size:
+        raise ValueError('truncated array blob')
+    magic, version, code, ndim, _, n, nb, words = _HEAD.unpack(hb[:_HEAD.size])
+    if magic != ARRAY_MAGIC or version != VERSION or ndim > 8:
         raise ValueError(f'not a kompressor_amd array blob (magic {magic!r}, version {version})')
-    shape = struct.unpack(f'<{ndim}q', bytes(b[_HEAD.size:_HEAD.size + 8 * ndim].cpu().numpy()))
+    shape = struct.unpack(f'<{ndim}q', hb[_HEAD.size:_HEAD.size + 8 * ndim])
     woff = _HEAD.size + 8 * ndim
     poff = woff + _pad8(nb)
     return code, shape, n, nb, woff, poff, poff + 8 * words
@@ -109,11 +116,11 @@ def pack_encoded(lowres, encoded):
     head += struct.pack(f'<{nsp}i', *[int(d) for d in dims])
     head += b'\0' * (_pad8(len(head)) - len(head))
     head += struct.pack(f'<{len(blobs)}q', *[int(bl.numel()) for bl in blobs])
-    parts = [_host_bytes(head)]
+    parts = [_device_bytes(head)]
     for bl in blobs:
         parts.append(bl)
         if bl.numel() % 8:
-            parts.append(torch.zeros((8 - bl.numel() % 8,), dtype=torch.uint8, device='cuda'))
+            parts.append(_device_bytes(bytes(8 - bl.numel() % 8)))
     return dev.from_device(torch.cat(parts), kind)
 
 

@@ -228,9 +228,15 @@ def test_categorical_coder_vs_oracle(kom):
     import oracle
     rng = np.random.default_rng(7)
     for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32),
-                  (64, np.uint8), (128, np.uint16), (512, np.uint16)):
+                  (64, np.uint8), (128, np.uint16), (512, np.uint16), (1, np.uint8), (2, np.uint8),
+                  (65, np.uint8), (511, np.uint16), (-200, np.uint8), (-500, np.uint16)):
+        heavy_ties = L < 0  # few distinct values: long runs of equal keys ordered by class index
+        L = abs(L)
         logits = rng.standard_normal((513, L)).astype(np.float32)
-        logits[::7, 3] = logits[::7, 1]  # ties
+        if heavy_ties:
+            logits = rng.integers(0, 3, size=(513, L)).astype(np.float32)
+        if L > 3:
+            logits[::7, 3] = logits[::7, 1]  # ties
         if L > 4:
             logits[5, :] = 0.5          # an all-tie row
             logits[6, :4] = [np.nan, -0.0, 0.0, np.nan]      # NaN after every number, -0 == +0

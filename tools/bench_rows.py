@@ -178,7 +178,10 @@ def main():
             t = cpu_time(lambda: oracle.common.encode_categorical(lh, gh))
             cpu = (4096 * (L * 4 + 2) / t / 1e9, '4096 elements, oracle stable argsort, 1 thread')
         emit('categorical:encode', 'rank coder encode, L=256', n * (L * 4 + 2), te, cpu)
-        emit('categorical:decode', 'rank coder decode, L=256', n * (L * 4 + 2), td)
+        emit('categorical:decode', 'rank coder decode, L=256, uniform random ranks', n * (L * 4 + 2), td)
+        small = torch.randint(0, 4, (n,), device='cuda', dtype=torch.uint8)  # a good predictor's ranks
+        ts = gpu_time(lambda: kom.volume.decode_categorical(logits, small), args.reps)
+        emit('categorical:decode_small_ranks', 'rank coder decode, L=256, ranks < 4', n * (L * 4 + 2), ts)
 
     # bit-plane container on the coded maps of a smooth C3-shaped volume
     if not want or 'packing' in want:
