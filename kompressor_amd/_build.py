@@ -1,6 +1,7 @@
 """Build ``libkompressor_hip.so`` in-tree with hipcc for gfx950 (no JIT, no torch extension).
 
-``python -m kompressor_amd._build`` or ``__graft_entry__.build()``.  Objects are compiled in
+``python kompressor_amd/_build.py`` or ``__graft_entry__.build()`` (by path: ``-m`` would import
+the package first, which needs a library that already exports every symbol).  Objects are compiled in
 parallel and cached by source mtime under ``kompressor_amd/build/``.
 """
 
