@@ -19,6 +19,8 @@
 // highres 2o + parity < n), so the coder kernels need no mirroring at all: the pads only ever
 // produce entries the trims drop.  The window is a gather through the composed mirror maps
 // (even reflect pad, then the symmetric neighbourhood pad).
+#include <cstdlib>
+
 #include "kmp_codec.h"
 
 namespace kmp {
@@ -46,6 +48,52 @@ __global__ void __launch_bounds__(kThreads) window_kernel(const T* __restrict__ 
     const int64_t y = mult * sym_index(sym_index(jy - p, g.L[1]), g.E[1]);
     const int64_t x = mult * sym_index(sym_index(jx - p, g.L[2]), g.E[2]);
     out[t] = src[(((b * S0 + z) * S1 + y) * S2 + x) * C + c];
+  }
+}
+
+// Row form (C == 1, < 2^30 elements): item = 16 B of one window row; the row's source row is
+// resolved once, interior chunks are one 16-byte copy (lowres source) or two 16-byte loads whose
+// even elements are kept (highres source), edge chunks mirror per element.
+__device__ __forceinline__ int32_t sym32(int32_t i, int32_t n) {
+  if (i >= 0 && i < n) return i;
+  if (i >= -n && i < 2 * n) return i < 0 ? -1 - i : 2 * n - 1 - i;
+  int32_t m = i % (2 * n);
+  if (m < 0) m += 2 * n;
+  return m < n ? m : 2 * n - 1 - m;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) rows_window_kernel(const T* __restrict__ src, int32_t S0, int32_t S1,
+                                                             int32_t S2, Geo g, int mult, int pz, int p, int32_t W0,
+                                                             int32_t W1, int32_t W2, T* __restrict__ out, int32_t nch,
+                                                             int32_t items) {
+  constexpr int V = Vec16<T>::V;
+  const int32_t L0 = (int32_t)g.L[0], L1 = (int32_t)g.L[1], L2 = (int32_t)g.L[2];
+  const int32_t E0 = (int32_t)g.E[0], E1 = (int32_t)g.E[1], E2 = (int32_t)g.E[2];
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, W0, W1, nch);
+    const int32_t z = mult * sym32(sym32(q.z - pz, L0), E0), y = mult * sym32(sym32(q.y - p, L1), E1);
+    const T* row = src + ((q.b * S0 + z) * S1 + y) * S2;
+    T* dst = out + ((q.b * W0 + q.z) * W1 + q.y) * W2;
+    const int32_t x0 = q.j * V, xs = x0 - p;
+    const bool inner = x0 + V <= W2 && xs >= 0 && xs + V <= E2;
+    if (inner && mult == 1) {
+      Vec16<T> v;
+      v.load(row + xs);
+      v.store(dst + x0);
+    } else if (inner && 2 * xs + 2 * V <= S2) {
+      Vec16<T> a, b, o;
+      a.load(row + 2 * xs);
+      b.load(row + 2 * xs + V);
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        o.e[i] = a.e[2 * i];
+        o.e[V / 2 + i] = b.e[2 * i];
+      }
+      o.store(dst + x0);
+    } else {
+      for (int32_t x = x0; x < x0 + V && x < W2; ++x) dst[x] = row[mult * sym32(sym32(x - p, L2), E2)];
+    }
   }
 }
 
@@ -189,6 +237,14 @@ static int window_launch(int nsp, int dtype, const void* src, int mult, const in
   if (total == 0) return KMP_OK;
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
+    const int64_t src_n = B * S[0] * S[1] * S[2] * C;
+    if (C == 1 && total < ((int64_t)1 << 30) && src_n < ((int64_t)1 << 30) && !std::getenv("KMP_DISABLE_ROWS")) {
+      const int64_t nch = ceil_div(W[2], Vec16<T>::V), items = B * W[0] * W[1] * nch;
+      rows_window_kernel<T><<<grid_for(items), kThreads, 0, stream>>>(
+          (const T*)src, (int32_t)S[0], (int32_t)S[1], (int32_t)S[2], g, mult, nsp == 3 ? p : 0, p, (int32_t)W[0],
+          (int32_t)W[1], (int32_t)W[2], (T*)out, (int32_t)nch, (int32_t)items);
+      return check_launch("window");
+    }
     window_kernel<T><<<grid_for(total), kThreads, 0, stream>>>((const T*)src, B, g, S[0], S[1], S[2], mult, nsp, p, C,
                                                                W[0], W[1], W[2], (T*)out, total);
     return check_launch("window");

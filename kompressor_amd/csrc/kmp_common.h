@@ -188,6 +188,42 @@ struct CMapPtrs {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// 16-byte vectors: aligned, and any-alignment (gfx950 serves unaligned dwordx4 global accesses;
+// rows of odd length are only element-aligned)
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
+// V = 16 / sizeof(T) consecutive elements moved as one 16-byte access
+template <typename T>
+struct Vec16 {
+  static constexpr int V = 16 / (int)sizeof(T);
+  T e[V];
+  __device__ __forceinline__ void load(const T* p) {
+    const u32x4u v = *(const u32x4u*)p;
+    __builtin_memcpy(e, &v, 16);
+  }
+  __device__ __forceinline__ void store(T* p) const {
+    u32x4u v;
+    __builtin_memcpy(&v, e, 16);
+    *(u32x4u*)p = v;
+  }
+};
+
+// row-kernel work item: chunk j of row (b, z, y)
+struct RowItem {
+  int32_t b, z, y, j;
+};
+// item t over [B, nz, ny, nch] (all extents >= 1)
+__device__ __forceinline__ RowItem row_item(uint32_t t, uint32_t nz, uint32_t ny, uint32_t nch) {
+  RowItem r;
+  r.j = (int32_t)(t % nch); t /= nch;
+  r.y = (int32_t)(t % ny); t /= ny;
+  r.z = (int32_t)(t % nz);
+  r.b = (int32_t)(t / nz);
+  return r;
+}
+
+
 // Flat index t over [B, e0, e1, e2, C] (C fastest).  The grid-stride kernels decompose one index
 // per element: 64-bit division is a long emulated sequence on gfx950, so indices below 2^32 (every
 // array axis and, in practice, every flat index fits) take 32-bit divisions; C == 1 skips one.

@@ -63,7 +63,6 @@ struct Lay {
   static constexpr int LPB = kBlock / SPL;  // lanes per block
 };
 typedef uint32_t u32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 template <int W>
 __device__ __forceinline__ u32x4v load16(const void* x, int64_t n, int64_t i0) {  // samples i0 .. i0+SPL-1

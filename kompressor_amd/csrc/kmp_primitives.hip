@@ -28,9 +28,6 @@ int check_launch(const char* what) {
 
 constexpr int kThreads = 256;
 
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));                // 16-B aligned
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));    // any alignment
-
 static inline unsigned grid_for(int64_t n) {
   int64_t g = ceil_div(n, kThreads);
   if (g > 65536) g = 65536;
@@ -657,34 +654,6 @@ __global__ void __launch_bounds__(kThreads) copy_box_kernel(const TI* __restrict
 // declared byte-aligned and gfx950 serves them as unaligned dwordx4 accesses.  Partial chunks
 // and mirrored edges fall back to per-element accesses inside the same item.
 // ------------------------------------------------------------------------------------------
-template <typename T>
-struct Vec16 {
-  static constexpr int V = 16 / (int)sizeof(T);
-  T e[V];
-  __device__ __forceinline__ void load(const T* p) {
-    const u32x4u v = *(const u32x4u*)p;
-    __builtin_memcpy(e, &v, 16);
-  }
-  __device__ __forceinline__ void store(T* p) const {
-    u32x4u v;
-    __builtin_memcpy(&v, e, 16);
-    *(u32x4u*)p = v;
-  }
-};
-
-struct RowItem {
-  int32_t b, z, y, j;
-};
-// item t over [B, nz, ny, nch] (all extents >= 1)
-__device__ __forceinline__ RowItem row_item(uint32_t t, uint32_t nz, uint32_t ny, uint32_t nch) {
-  RowItem r;
-  r.j = (int32_t)(t % nch); t /= nch;
-  r.y = (int32_t)(t % ny); t /= ny;
-  r.z = (int32_t)(t % nz);
-  r.b = (int32_t)(t / nz);
-  return r;
-}
-
 // jnp.pad rows: out[b, z, y, x] = in[b, m(z - lz), m(y - ly), m(x - lx)]
 template <typename T>
 __global__ void __launch_bounds__(kThreads) rows_pad_kernel(const T* __restrict__ in, E3<int32_t> n, E3<int32_t> lo,

@@ -94,3 +94,24 @@ def test_maps_from_predictions_lds(kom, dtype, w, nsp):
     got = _nd.d_maps_from_predictions(torch.from_numpy(preds).cuda(), nsp)
     for a, b in zip(got, ons.maps_from_predictions(preds)):
         assert np.array_equal(_np(a), b)
+
+
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16])
+@pytest.mark.parametrize('w', [5, 16, 17, 33, 34, 50, 65, 97])
+@pytest.mark.parametrize('nsp,p', [(3, 0), (3, 1), (3, 2), (2, 0), (2, 1), (2, 2)])
+def test_rows_window_and_mean_predictor(kom, dtype, w, nsp, p):
+    """The callback path's window gathers (from highres and from lowres + dims) and the mean
+    predictor's two row passes, against the oracle's composition, across chunk boundaries."""
+    ons = oracle.volume if nsp == 3 else oracle.image
+    shape = (2, 7, 9, w, 1) if nsp == 3 else (3, 9, w, 1)
+    hi = _rand(shape, dtype, w + p)
+    hp, dims = ons.pad_highres(hi)
+    want = ons.pad_neighborhood(ons.lowres_from_highres(hp), p)
+    got = _nd.d_window_from_highres(torch.from_numpy(hi).cuda(), p, nsp)
+    assert np.array_equal(_np(got), want)
+    lo = ons.trim(ons.lowres_from_highres(hp), dims)
+    got_lo = _nd.d_window_from_lowres(torch.from_numpy(lo).cuda(), tuple(dims), p, nsp)
+    assert np.array_equal(_np(got_lo), ons.pad_neighborhood(ons.pad_lowres(lo, tuple(dims)), p))
+    maps = kom.MeanPredictor(p, nsp)(got)
+    for a, b in zip(maps, oracle.predictors.mean_predictions_fn(p, nsp)(want)):
+        assert np.array_equal(_np(a), b)
