@@ -125,14 +125,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     mok_y[k] = live && (!par[1] || vy1);
   }
 
-  // ---- every load of the block, issued before any use ----
+  // ---- every load of the block, issued before any use, in the order the planes consume them
+  // (node planes c0-1, c0, then per output plane u: node plane c0+u+1 and the plane's stream
+  // rows), so output plane u waits only for its own loads (vmcnt counts in issue order) ----
   NR N[PL + 2];  // node planes c0-1+t
   OR O[PL];      // output planes c0+u
-#pragma unroll
-  for (int t = 0; t < PL + 2; ++t) {
+  auto load_node = [&](int t) __attribute__((always_inline)) {
     N[t] = NR{};
     const int q = c0 - 1 + t;
-    if (q < 0 || (t >= 2 && q - 1 >= Z1)) continue;  // uniform
+    if (q < 0 || (t >= 2 && q - 1 >= Z1)) return;  // uniform
     const int sz = lsrc(q, a.Lz, a.Ez);
     if constexpr (DEC) {
       const T* p = lin + sz * lplane;
@@ -161,12 +162,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
       }
     }
-  }
-#pragma unroll
-  for (int u = 0; u < PL; ++u) {
+  };
+  auto load_out = [&](int u) __attribute__((always_inline)) {
     O[u] = OR{};
     const int q = c0 + u;
-    if (q >= Z1) continue;
+    if (q >= Z1) return;
     const bool vz1 = q < a.Lcz;
     if constexpr (DEC) {
 #pragma unroll
@@ -181,6 +181,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       if (live && vz1) O[u].o0 = ld16(p + hplane + ho_own);
       if (live && vz1 && vy1) O[u].o1 = ld16(p + hplane + ho_own + a.W);
     }
+  };
+  if constexpr (DEC) {  // measured: decode 92.1 -> 89.5 us at C3; encode prefers all node rows first
+    load_node(0);
+    load_node(1);
+#pragma unroll
+    for (int u = 0; u < PL; ++u) {
+      load_node(u + 2);
+      load_out(u);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < PL + 2; ++t) load_node(t);
+#pragma unroll
+    for (int u = 0; u < PL; ++u) load_out(u);
   }
 
   // ---- 2x2 node sums per node plane (rows Y and, on the wave's first row, Y-1) ----
