@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _device as dev
-from . import _lib
+from . import _lib, _trace
 from ._lib import check, lib
 
 PARITY = {
@@ -513,6 +513,7 @@ def _callback_maps(maps, nsp):
     return [_dev(m) for m in maps]
 
 
+@_trace.traced('kmp.encode')
 def encode(predictions_fn, encode_fn, highres, padding, nsp):
     validate_padding(padding)
     dims = highres_dims(highres.shape, nsp)
@@ -532,7 +533,8 @@ def encode(predictions_fn, encode_fn, highres, padding, nsp):
         if coder is not None:
             # the callback path with a built-in coder: window gather, predictions_fn, one coder launch
             validate_lowres_shape((h.shape[0], *L, *_ch(h.shape, nsp)), nsp)
-            pred_maps = _callback_maps(predictions_fn(d_window_from_highres(h, padding, nsp)), nsp)
+            with _trace.stage('kmp.predictions_fn'):
+                pred_maps = _callback_maps(predictions_fn(d_window_from_highres(h, padding, nsp)), nsp)
             if _preds_fit(pred_maps, h.dtype, h.shape[0], L, _ch(h.shape, nsp), nsp):
                 lowres, encoded, dims = _alloc_encoded(h, coder, nsp)
                 check(lib.kmp_encode_with_predictions(nsp, dev.dtype_code(h), coder, h.data_ptr(), h.shape[0],
@@ -555,6 +557,7 @@ def encode(predictions_fn, encode_fn, highres, padding, nsp):
     return dev.from_device(lowres, kind), (tuple(dev.from_device(m, kind) for m in encoded), tuple(dims))
 
 
+@_trace.traced('kmp.decode')
 def decode(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
     encoded_maps, dims = encoded
     dims = tuple(int(d) for d in dims)
@@ -576,7 +579,8 @@ def decode(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
         # the callback path with a built-in coder: window gather, predictions_fn, one coder launch
         _check_encoded_maps(lo, maps, dims, nsp)
         L = [e + d for e, d in zip(_sp(lo.shape, nsp), dims)]
-        pred_maps = _callback_maps(predictions_fn(d_window_from_lowres(lo, dims, padding, nsp)), nsp)
+        with _trace.stage('kmp.predictions_fn'):
+            pred_maps = _callback_maps(predictions_fn(d_window_from_lowres(lo, dims, padding, nsp)), nsp)
         if _preds_fit(pred_maps, lo.dtype, lo.shape[0], L, _ch(lo.shape, nsp), nsp):
             lo = lo.contiguous()
             out = dev.empty((lo.shape[0], *[2 * l - 1 - d for l, d in zip(L, dims)], *_ch(lo.shape, nsp)), lo.dtype)
@@ -605,6 +609,7 @@ def _per_level(fn, levels, what):
     return [fn] * levels
 
 
+@_trace.traced('kmp.encode_pyramid')
 def encode_pyramid(predictions_fn, encode_fn, highres, levels, padding, nsp):
     """``levels`` applications of ``encode`` (volume/encode_decode.py:30-56), each on the previous
     level's lowres.  ``predictions_fn`` / ``encode_fn`` may be one callable or one per level
@@ -618,6 +623,7 @@ def encode_pyramid(predictions_fn, encode_fn, highres, levels, padding, nsp):
     return x, out
 
 
+@_trace.traced('kmp.decode_pyramid')
 def decode_pyramid(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
     """Inverse of :func:`encode_pyramid`: decode the coarsest level first."""
     encoded = list(encoded)
@@ -713,6 +719,7 @@ def _chunks_for(L, chunk, padding, progress_fn, nsp):
     return list(_chunk_list(L, chunk, nsp, progress_fn))
 
 
+@_trace.traced('kmp.encode_chunks')
 def encode_chunks(predictions_fn, encode_fn, highres, chunk, padding, progress_fn, nsp):
     dims = highres_dims(highres.shape, nsp)
     padded_shape = (highres.shape[0], *[s + d for s, d in zip(_sp(highres.shape, nsp), dims)],
@@ -740,6 +747,7 @@ def encode_chunks(predictions_fn, encode_fn, highres, chunk, padding, progress_f
     return dev.from_device(lowres, kind), (tuple(dev.from_device(m, kind) for m in encoded), tuple(dims))
 
 
+@_trace.traced('kmp.decode_chunks')
 def decode_chunks(predictions_fn, decode_fn, lowres, encoded, chunk, padding, progress_fn, nsp):
     encoded_maps, dims = encoded
     dims = tuple(int(d) for d in dims)

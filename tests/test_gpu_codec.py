@@ -414,3 +414,15 @@ def test_wave32_matches_oracle(kom, shape, dtype):
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
     assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims)), x)
     assert _last_launch(kom) == 'wave3d32_decode'
+
+
+def test_trace_ranges_do_not_change_results(kom, monkeypatch):
+    """KMP_TRACE's roctx ranges wrap the same calls (SURVEY.md §5 tracing)."""
+    monkeypatch.setattr(kom._trace, 'ENABLED', True)
+    x = torch.randint(0, 65536, (2, 16, 16, 16, 1), dtype=torch.int32, device='cuda').to(torch.uint16)
+    pred = kom.MeanPredictor(1, 3)
+    cb = lambda w: pred(w)  # noqa: E731
+    lo, enc = kom.volume.encode(cb, kom.volume.encode_values_uint16, x, padding=1)
+    assert torch.equal(kom.volume.decode(cb, kom.volume.decode_values_uint16, lo, enc, padding=1), x)
+    lo2, enc2 = kom.volume.encode_chunks(pred, kom.volume.encode_values_uint16, x, chunk=6, padding=1)
+    assert torch.equal(lo2, lo)
