@@ -51,31 +51,44 @@ __device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: 
   return (uint32_t)fminf(fmaxf(v, 0.0f), hi);
 }
 
-// channel k of the linear predictor for 4 cells (features f[n][cell]), cast to T.  ``Wt`` is the
-// LDS copy of the weights, channel-major [19][8] followed by the bias [19]: uniform ds_reads
-// (broadcast), so the 171 constants never compete for scalar registers.
-template <typename T, int K>
-__device__ __forceinline__ void channel(const float (&f)[8][4], const float* Wt, uint32_t (&out)[4]) {
-  const float4 wa = *(const float4*)(Wt + K * 8), wb = *(const float4*)(Wt + K * 8 + 4);
-  const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-  const float bk = Wt[19 * 8 + K];
-  f32x2 a0 = {bk, bk}, a1 = {bk, bk};
+// Node values are kept as f32 pairs laid out for the packed FMAs: for the 4 cells X+4g .. X+4g+3
+// of a group, NP[.][g][0] = {node 4g, 4g+2}, [1] = {4g+1, 4g+3}, [2] = {4g+2, 4g+4}.  Cells
+// (0, 2) read pairs dx and cells (1, 3) pairs 1 + dx, so every feature operand is an aligned
+// register pair (pairing cells 0/1 and 2/3 instead needs node pairs (x+1, x+2) assembled by
+// moves in every channel: 214 v_mov per wave, 18 % of a VALU stream the SQ counters show busy
+// 75 % of the cycles).  The chain is unchanged: fma over n = dz*4 + dy*2 + dx from the bias.
+// ``Wt`` is the LDS copy of the weights, channel-major [19][8] with every weight stored twice
+// (the packed operand {w, w}), then the bias [19] (uniform ds_reads: the constants never compete
+// for scalar registers).
+template <typename T, int K, int G>
+__device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 (&NP1)[3][G][3], int pl, int g,
+                                        const float* Wt, uint32_t (&out)[4]) {
+  // weights stored pre-splat ({w, w} per n): each 16-byte read is two ready operand pairs
+  f32x2 w2[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *(const float4*)(Wt + K * 16 + 4 * q);
+    w2[2 * q] = (f32x2){v.x, v.y};
+    w2[2 * q + 1] = (f32x2){v.z, v.w};
+  }
+  const float bk = Wt[19 * 16 + K];
+  f32x2 a02 = {bk, bk}, a13 = {bk, bk};
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
-    const f32x2 wv2 = {w[n], w[n]};
-    a0 = __builtin_elementwise_fma((f32x2){f[n][0], f[n][1]}, wv2, a0);
-    a1 = __builtin_elementwise_fma((f32x2){f[n][2], f[n][3]}, wv2, a1);
+    const int dz = n >> 2, dy = (n >> 1) & 1, dx = n & 1;
+    const f32x2 wv2 = w2[n];
+    const f32x2(&R)[3] = dy ? NP1[pl + dz][g] : NP[pl + dz][g];
+    a02 = __builtin_elementwise_fma(R[dx], wv2, a02);
+    a13 = __builtin_elementwise_fma(R[1 + dx], wv2, a13);
   }
-  out[0] = cast_t<T>(a0.x);
-  out[1] = cast_t<T>(a0.y);
-  out[2] = cast_t<T>(a1.x);
-  out[3] = cast_t<T>(a1.y);
-
-
+  out[0] = cast_t<T>(a02.x);
+  out[1] = cast_t<T>(a13.x);
+  out[2] = cast_t<T>(a02.y);
+  out[3] = cast_t<T>(a13.y);
 }
 
 constexpr int kXch = 5;  // channels exchanged downwards: 3, 9, 10, 16 (plane c), 17 (plane c-1)
-constexpr int kWtWords = 172;  // 19 * 8 weights + 19 biases, rounded up to 16 B
+constexpr int kWtWords = 324;  // 19 * 8 weights stored twice + 19 biases, rounded up to 16 B
 
 template <typename T, bool DEC>
 __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
@@ -88,8 +101,12 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   float* Wt = (float*)smem;
   uint32_t* xrow = smem + kWtWords;
   for (int t = threadIdx.x; t < 19 * 9; t += blockDim.x) {
-    if (t < 152) Wt[(t % 19) * 8 + t / 19] = a.W[t];  // W[n][k] -> Wt[k][n]
-    else Wt[152 + (t - 152)] = a.b[t - 152];
+    if (t < 152) {  // W[n][k] -> Wt[k][n] twice
+      Wt[(t % 19) * 16 + 2 * (t / 19)] = a.W[t];
+      Wt[(t % 19) * 16 + 2 * (t / 19) + 1] = a.W[t];
+    } else {
+      Wt[304 + (t - 152)] = a.b[t - 152];
+    }
   }
   __syncthreads();
 
@@ -179,6 +196,7 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
 
   // ---- node values: own row Y, row Y+1 (shuffle / halo), each with node x+VX ----
   float nY[3][VX + 1], nY1[3][VX + 1];
+  constexpr int G = VX / 4;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     uint32_t n[VX], nd[VX];
@@ -207,30 +225,22 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
     nY[t][VX] = (float)nx;
     nY1[t][VX] = (float)(last ? ndx : bx);
   }
+  f32x2 NP[3][G][3], NP1[3][G][3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        NP[t][g][q] = (f32x2){nY[t][4 * g + q], nY[t][4 * g + q + 2]};
+        NP1[t][g][q] = (f32x2){nY1[t][4 * g + q], nY1[t][4 * g + q + 2]};
+      }
 
   // ---- channels: evaluated map group by map group so only a few are live at a time ----
-  // feat(PLANE, ...) gathers the 8 features of cells X+4g .. X+4g+3 of cell plane c-1+PLANE
-  auto feats = [&](int pl, int g, float (&f)[8][4]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = 4 * g + j;
-#pragma unroll
-      for (int dz = 0; dz < 2; ++dz) {
-        f[dz * 4 + 0][j] = nY[pl + dz][i];
-        f[dz * 4 + 1][j] = nY[pl + dz][i + 1];
-        f[dz * 4 + 2][j] = nY1[pl + dz][i];
-        f[dz * 4 + 3][j] = nY1[pl + dz][i + 1];
-      }
-    }
-  };
-  constexpr int G = VX / 4;
-  // CH(out, PLANE, K): channel K of this lane's VX cells of plane c-1+PLANE into out[1..VX]
 #define KMP_CH(OUT, PLANE, K)                                             \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                         \
-    float f[8][4];                                                        \
     uint32_t o[4];                                                        \
-    feats(PLANE, g, f);                                                   \
-    channel<T, K>(f, Wt, o);                                              \
+    channel<T, K, G>(NP, NP1, PLANE, g, Wt, o);                           \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j]; \
   }
 
