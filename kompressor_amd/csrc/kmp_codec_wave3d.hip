@@ -125,31 +125,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     mok_y[k] = live && (!par[1] || vy1);
   }
 
-  // ---- every load of the block, issued before any use, in the order the planes consume them
-  // (node planes c0-1, c0, then per output plane u: node plane c0+u+1 and the plane's stream
-  // rows), so output plane u waits only for its own loads (vmcnt counts in issue order) ----
+  // ---- every load of the block, issued before any use.  Encode: all node rows, then the stream
+  // rows.  Decode: in the order the planes consume them (node planes c0-1, c0, then per output
+  // plane u node plane c0+u+1 and its 7 map rows), so output plane u waits only for its own loads
+  // (vmcnt counts in issue order): 91.0 vs 92.0 us at C3, same box, 3 alternating runs ----
   NR N[PL + 2];  // node planes c0-1+t
   OR O[PL];      // output planes c0+u
-  auto load_node = [&](int t) __attribute__((always_inline)) {
-    N[t] = NR{};
-    const int q = c0 - 1 + t;
-    if (q < 0 || (t >= 2 && q - 1 >= Z1)) return;  // uniform
-    const int sz = lsrc(q, a.Lz, a.Ez);
-    if constexpr (DEC) {
-      const T* p = lin + sz * lplane;
-      if (a.nt_nodes) {
-        if (live) N[t].own = ld8(p + lo_own);
-      } else {
-        if (live) N[t].own = ld8c(p + lo_own);
-      }
-      if constexpr (ONE) {
-        if (need_up) N[t].halo = ld8c(p + lo_up);
-        if (need_dn) N[t].dn = ld8c(p + lo_dn);
-      } else {
-        if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
-      }
-    } else {
-      const T* p = hin + 2 * sz * hplane;
+  if constexpr (!DEC) {
+#pragma unroll
+    for (int t = 0; t < PL + 2; ++t) {
+      N[t] = NR{};
+      const int q = c0 - 1 + t;
+      if (q < 0 || (t >= 2 && q - 1 >= Z1)) continue;  // uniform
+      const T* p = hin + 2 * lsrc(q, a.Lz, a.Ez) * hplane;
       if (a.nt_nodes) {
         if (live) N[t].own = ld16(p + ho_own);
       } else {
@@ -162,27 +150,70 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
       }
     }
-  };
-  auto load_out = [&](int u) __attribute__((always_inline)) {
-    O[u] = OR{};
-    const int q = c0 + u;
-    if (q >= Z1) return;
-    const bool vz1 = q < a.Lcz;
-    if constexpr (DEC) {
 #pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        int par[3];
-        map_parity(3, k, par);
-        if (mok_y[k] && (!par[0] || vz1)) O[u].mv[k] = ld8(mbase[k] + q * mplane[k]);
-      }
-    } else {
+    for (int u = 0; u < PL; ++u) {
+      O[u] = OR{};
+      const int q = c0 + u;
+      if (q >= Z1) continue;
+      const bool vz1 = q < a.Lcz;
       const T* p = hin + 2 * q * hplane;
       if (live && vy1) O[u].e1 = ld16(p + ho_own + a.W);
       if (live && vz1) O[u].o0 = ld16(p + hplane + ho_own);
       if (live && vz1 && vy1) O[u].o1 = ld16(p + hplane + ho_own + a.W);
     }
-  };
-  if constexpr (DEC) {  // measured: decode 92.1 -> 89.5 us at C3; encode prefers all node rows first
+  } else {
+    auto load_node = [&](int t) __attribute__((always_inline)) {
+      N[t] = NR{};
+      const int q = c0 - 1 + t;
+      if (q < 0 || (t >= 2 && q - 1 >= Z1)) return;  // uniform
+      const int sz = lsrc(q, a.Lz, a.Ez);
+      if constexpr (DEC) {
+        const T* p = lin + sz * lplane;
+        if (a.nt_nodes) {
+          if (live) N[t].own = ld8(p + lo_own);
+        } else {
+          if (live) N[t].own = ld8c(p + lo_own);
+        }
+        if constexpr (ONE) {
+          if (need_up) N[t].halo = ld8c(p + lo_up);
+          if (need_dn) N[t].dn = ld8c(p + lo_dn);
+        } else {
+          if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
+        }
+      } else {
+        const T* p = hin + 2 * sz * hplane;
+        if (a.nt_nodes) {
+          if (live) N[t].own = ld16(p + ho_own);
+        } else {
+          if (live) N[t].own = ld16c(p + ho_own);
+        }
+        if constexpr (ONE) {
+          if (need_up) N[t].halo = ld16c(p + ho_up);
+          if (need_dn) N[t].dn = ld16c(p + ho_dn);
+        } else {
+          if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
+        }
+      }
+    };
+    auto load_out = [&](int u) __attribute__((always_inline)) {
+      O[u] = OR{};
+      const int q = c0 + u;
+      if (q >= Z1) return;
+      const bool vz1 = q < a.Lcz;
+      if constexpr (DEC) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          int par[3];
+          map_parity(3, k, par);
+          if (mok_y[k] && (!par[0] || vz1)) O[u].mv[k] = ld8(mbase[k] + q * mplane[k]);
+        }
+      } else {
+        const T* p = hin + 2 * q * hplane;
+        if (live && vy1) O[u].e1 = ld16(p + ho_own + a.W);
+        if (live && vz1) O[u].o0 = ld16(p + hplane + ho_own);
+        if (live && vz1 && vy1) O[u].o1 = ld16(p + hplane + ho_own + a.W);
+      }
+    };
     load_node(0);
     load_node(1);
 #pragma unroll
@@ -190,11 +221,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       load_node(u + 2);
       load_out(u);
     }
-  } else {
-#pragma unroll
-    for (int t = 0; t < PL + 2; ++t) load_node(t);
-#pragma unroll
-    for (int u = 0; u < PL; ++u) load_out(u);
   }
 
   // ---- 2x2 node sums per node plane (rows Y and, on the wave's first row, Y-1) ----

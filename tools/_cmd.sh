@@ -1,7 +1,11 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/lin; rm -rf $O; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_linear.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
-tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $O/pytest.log | head -60; exit $rc; }
-timeout -k 10 300 python tools/bench_rows.py --rows volume_linear_p0,volume_linear_p1 --no-cpu > $O/rows.log 2>&1; rc=$?
-grep -h row $O/rows.log | cut -c1-160; exit $rc
+O=gpurun_out/ab; rm -rf $O; mkdir -p $O
+for rep in 1 2 3; do for v in 0 1; do
+  KMP_W3_DEC_ORDER=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/v${v}_$rep -o run -- python3 tools/ktime.py volume 0 30 > $O/v${v}_$rep.log 2>&1 || exit 1
+  f=$(find $O/v${v}_$rep -name 'run_kernel_stats.csv'); python3 -c "
+import csv,sys
+for r in csv.DictReader(open('$f')):
+    if 'wave3d_plane' in r['Name']: print('order=$v rep=$rep', round(float(r['AverageNs'])/1e3,2), 'DEC' if 'true' in r['Name'] else 'ENC')
+"
+done; done
