@@ -88,3 +88,27 @@ def test_pack_encoded_round_trip_and_ratio(kom):
         assert np.array_equal(rec, vol)
         nbytes = blob.numel() if isinstance(blob, torch.Tensor) else blob.size
         assert nbytes < 0.5 * vol.nbytes, nbytes / vol.nbytes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(0,), (3, 0, 5)])
+def test_pack_empty(kom, shape):
+    x = np.zeros(shape, np.uint16)
+    blob = kom.packing.pack(x)
+    assert blob.size == 40 + 8 * x.ndim  # header + shape, no widths, no payload
+    back = kom.packing.unpack(blob)
+    assert back.shape == x.shape and back.dtype == x.dtype
+
+
+@pytest.mark.gpu
+def test_unpack_rejects_bad_blobs(kom):
+    x = np.arange(1000, dtype=np.uint16)
+    blob = kom.packing.pack(x)
+    with pytest.raises(ValueError):
+        kom.packing.unpack(blob[:-8])          # truncated payload
+    bad = blob.copy()
+    bad[:4] = np.frombuffer(b'XXXX', np.uint8)
+    with pytest.raises(ValueError):
+        kom.packing.unpack(bad)                # not a container
+    with pytest.raises(ValueError):
+        kom.packing.unpack(blob[:10])          # shorter than a header
