@@ -151,8 +151,15 @@ def init_dist():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        # one process per GPU over RCCL; KMP_BENCH_BACKEND=gloo rehearses the N > 1 logic with
+        # every rank on the devices one box has (ranks share a GPU when there are fewer GPUs)
+        backend = os.environ.get('KMP_BENCH_BACKEND', 'nccl')
+        dev_id = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_id)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_id))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -233,7 +240,8 @@ def c4_reassembly(kom, hi, predictor, ndim, dist, world, ws):
     raw = hi.numel() * hi.element_size()
     return {'tiles_per_rank': int(shard.shape[0]), 'ms_codec_plus_allgather': round(tt.item() * 1e3, 4),
             'volume_GBps': round(raw / tt.item() / 1e9, 2),
-            'collective': 'all_gather_into_tensor (RCCL) of per-rank decoded tile slabs'}
+            'collective': ('all_gather_into_tensor (RCCL) of per-rank decoded tile slabs'
+                           if dist.get_backend() == 'nccl' else f'all_gather ({dist.get_backend()}) of per-rank decoded tile slabs')}
 
 
 def main():
