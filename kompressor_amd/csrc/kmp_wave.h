@@ -93,8 +93,17 @@ __device__ __forceinline__ uint32_t cvt_sat(float v) {
   return u < hi ? u : hi;
 }
 
-__device__ __forceinline__ uint32_t shdn(uint32_t v, int d) { return (uint32_t)__shfl_down((int)v, d, 64); }
-__device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
+// Lane l reads lane l + d (shdn) / l - d (shup); out-of-range lanes keep their own value.  A
+// distance known to be 1 after inlining is one DPP move (wave_shl:1 / wave_shr:1, whole-wave
+// shifts on CDNA) instead of an LDS-crossbar ds_bpermute with its address computation.
+__device__ __forceinline__ uint32_t shdn(uint32_t v, int d) {
+  if (__builtin_constant_p(d) && d == 1) return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);
+  return (uint32_t)__shfl_down((int)v, d, 64);
+}
+__device__ __forceinline__ uint32_t shup(uint32_t v, int d) {
+  if (__builtin_constant_p(d) && d == 1) return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);
+  return (uint32_t)__shfl_up((int)v, d, 64);
+}
 
 }  // namespace wv
 }  // namespace kmp
