@@ -137,32 +137,45 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
     nodes(hd, t);
     xbox(t, xd);
   }
-  // y box sums over the virtual rows Y0 + j: cell row Y (so) and Y-1 (su)
-  uint32_t so[VX], su[VX];
+  // y box sums over the virtual rows Y0 + j: cell row Y (so) and Y-1 (su).  For 8-bit samples
+  // the sums stay below 2^16 ((2p+2)^2 * 255 <= 9180), so two columns travel packed in one
+  // 32-bit word: half the cross-lane shuffles and half the adds / selects (SWAR).
+  constexpr bool SWAR = sizeof(T) == 1;
+  constexpr int VW = SWAR ? VX / 2 : VX;
+  uint32_t po[VW], pu[VW], pd[VW];
 #pragma unroll
-  for (int i = 0; i < VX; ++i) so[i] = su[i] = 0;
+  for (int w = 0; w < VW; ++w) {
+    po[w] = SWAR ? (xo[2 * w] | xo[2 * w + 1] << 16) : xo[w];
+    pu[w] = SWAR ? (xu[2 * w] | xu[2 * w + 1] << 16) : xu[w];
+    pd[w] = SWAR ? (xd[2 * w] | xd[2 * w + 1] << 16) : xd[w];
+  }
+  uint32_t so[VW], su[VW];
+#pragma unroll
+  for (int w = 0; w < VW; ++w) so[w] = su[w] = 0;
 #pragma unroll
   for (int d = -P - 1; d <= P + 1; ++d) {
     const int j = r + d;
 #pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      uint32_t v = d == 0 ? xo[i] : (d < 0 ? shup(xo[i], -d * a.txn) : shdn(xo[i], d * a.txn));
+    for (int w = 0; w < VW; ++w) {
+      uint32_t v = d == 0 ? po[w] : (d < 0 ? shup(po[w], -d * a.txn) : shdn(po[w], d * a.txn));
       if (d < 0) {
-        const uint32_t h = d == -P - 1 ? xu[i] : shdn(xu[i], (d + P + 1) * a.txn);
+        const uint32_t h = d == -P - 1 ? pu[w] : shdn(pu[w], (d + P + 1) * a.txn);
         v = j < 0 ? h : v;
       } else if (d > 0) {
-        const uint32_t h = d == P + 1 ? xd[i] : shup(xd[i], (P + 1 - d) * a.txn);
+        const uint32_t h = d == P + 1 ? pd[w] : shup(pd[w], (P + 1 - d) * a.txn);
         v = j >= rows ? h : v;
       }
-      if (d >= -P) so[i] += v;
-      if (d <= P) su[i] += v;
+      if (d >= -P) so[w] += v;
+      if (d <= P) su[w] += v;
     }
   }
   uint32_t M1[VX + 1], M0[VX + 1];  // cell rows Y / Y-1, cols X-1 .. X+VX-1
 #pragma unroll
   for (int i = 0; i < VX; ++i) {
-    M1[i + 1] = so[i] / NN;
-    M0[i + 1] = su[i] / NN;
+    const uint32_t o = SWAR ? (so[i / 2] >> (16 * (i & 1))) & 0xffffu : so[i];
+    const uint32_t u = SWAR ? (su[i / 2] >> (16 * (i & 1))) & 0xffffu : su[i];
+    M1[i + 1] = o / NN;
+    M0[i + 1] = u / NN;
   }
   M1[0] = shup(M1[VX], 1);
   M0[0] = shup(M0[VX], 1);

@@ -31,6 +31,20 @@ __global__ void split8(const u32x4* __restrict__ a, u32x2* __restrict__ out, int
   }
 }
 
+// split16: each lane reads 32 B (two 16-B loads) and writes two 16-B halves to streams s and
+// s+4: the store shape of a codec lane owning 8 outputs (16 B of each map) instead of 4
+__global__ void split16(const u32x4* __restrict__ a, u32x4* __restrict__ out, int64_t n2, int64_t per) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / 256, col = i % 256;
+    const u32x4 v0 = __builtin_nontemporal_load(a + (row * 512 + col));
+    const u32x4 v1 = __builtin_nontemporal_load(a + (row * 512 + 256 + col));
+    const int s = row & 3;
+    const int64_t o = (row >> 2) * 256 + col;
+    __builtin_nontemporal_store(v0, out + (int64_t)s * per + o);
+    __builtin_nontemporal_store(v1, out + (int64_t)(s + 4) * per + o);
+  }
+}
+
 __global__ void merge8(const u32x2* __restrict__ in, u32x4* __restrict__ b, int64_t n, int64_t per) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t row = i / 256, col = i % 256;
@@ -164,6 +178,11 @@ int main() {
     run(nm, [&] { split8<<<blocks, 256>>>((const u32x4*)a, (u32x2*)b, n16, per); });
     snprintf(nm, sizeof nm, "merge8 grid=%d", blocks);
     run(nm, [&] { merge8<<<blocks, 256>>>((const u32x2*)b, (u32x4*)a, n16, per); });
+  }
+  for (int blocks : {2048, 4096, 8192}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "split16 grid=%d", blocks);
+    run(nm, [&] { split16<<<blocks, 256>>>((const u32x4*)a, (u32x4*)b, n16 / 2, n16 / 8); });
   }
   return 0;
 }
