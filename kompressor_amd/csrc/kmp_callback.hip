@@ -165,6 +165,125 @@ __global__ void __launch_bounds__(kThreads) code_preds_kernel32(const T* __restr
   }
 }
 
+// Row form of the coder pass (C == 1, 32-bit sizes): item = V = 16 / sizeof(T) consecutive
+// outputs x0 .. x0+V-1 of output row (oz, oy).  For each highres row parity (pz, py) the 2V
+// highres samples are two 16-byte accesses whose even / odd elements are the classes (pz, py, 0)
+// and (pz, py, 1) -- the lowres or a map -- and each class's prediction, residual / decoded row
+// is one 16-byte access (unaligned: rows of odd length).  Partial chunks go per element.
+__host__ __device__ constexpr int class_index(int nsp, int pz, int py, int px) {  // map k, -1 = lowres
+  return (pz == 0 && py == 0 && px == 0) ? -1
+         : nsp == 3 ? (pz ? (py ? (px ? 3 : 0) : (px ? 1 : 4)) : (py ? (px ? 2 : 5) : 6))
+                    : (py ? (px ? 2 : 0) : 1);
+}
+
+template <typename T, int CODER, bool DEC, int NSP>
+__global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __restrict__ src, CMapPtrs maps_in,
+                                                                 MapPtrs maps_out, CMapPtrs preds, T* __restrict__ dst,
+                                                                 MapExt me, int32_t n0, int32_t n1, int32_t n2,
+                                                                 int32_t E0, int32_t E1, int32_t E2, int32_t nch,
+                                                                 int32_t items) {
+  using TO = typename coder_out<CODER>::type;
+  static_assert(sizeof(TO) == sizeof(T), "same-width coder");
+  constexpr int V = Vec16<T>::V;
+  for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
+    const RowItem q = row_item((uint32_t)t, E0, E1, nch);
+    const int32_t oz = q.z, oy = q.y, x0 = q.j * V;
+#pragma unroll
+    for (int pz = 0; pz < (NSP == 3 ? 2 : 1); ++pz)
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        const int k0 = class_index(NSP, pz, py, 0), k1 = class_index(NSP, pz, py, 1);
+        const int32_t ez = NSP == 3 ? (pz ? me.e[k1][0] : E0) : 1, ey = py ? me.e[k1][1] : E1;
+        if (oz >= ez || oy >= ey) continue;
+        const int32_t e2_0 = k0 < 0 ? E2 : me.e[k0][2], e2_1 = me.e[k1][2];
+        const int32_t nx0 = min(V, e2_0 - x0), nx1 = min(V, e2_1 - x0);  // valid even / odd outputs
+        const int32_t hoff = ((q.b * n0 + 2 * oz + pz) * n1 + 2 * oy + py) * n2 + 2 * x0;
+        // class rows: (lowres | map k0) and map k1, their prediction rows
+        auto cls_off = [&](int k) { return ((q.b * me.e[k][0] + oz) * me.e[k][1] + oy) * me.e[k][2] + x0; };
+        auto pred_off = [&](int k) { return ((q.b * me.u[k][0] + oz) * me.u[k][1] + oy) * me.u[k][2] + x0; };
+        auto load_row = [&](const T* p, int32_t nv, Vec16<T>& v) {
+          if (nv == V) {
+            v.load(p);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) v.e[i] = i < nv ? p[i] : T(0);
+          }
+        };
+        auto store_row = [&](T* p, int32_t nv, const Vec16<T>& v) {
+          if (nv == V) {
+            v.store(p);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i)
+              if (i < nv) p[i] = v.e[i];
+          }
+        };
+        const int32_t lo_off = ((q.b * E0 + oz) * E1 + oy) * E2 + x0;
+        if constexpr (!DEC) {
+          Vec16<T> ev, od;
+          if (2 * x0 + 2 * V <= n2) {
+            Vec16<T> a, b2;
+            a.load(src + hoff);
+            b2.load(src + hoff + V);
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) {
+              ev.e[i] = a.e[2 * i]; od.e[i] = a.e[2 * i + 1];
+              ev.e[V / 2 + i] = b2.e[2 * i]; od.e[V / 2 + i] = b2.e[2 * i + 1];
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+              ev.e[i] = 2 * (x0 + i) < n2 ? src[hoff + 2 * i] : T(0);
+              od.e[i] = 2 * (x0 + i) + 1 < n2 ? src[hoff + 2 * i + 1] : T(0);
+            }
+          }
+          auto code_row = [&](int k, int32_t nv, const Vec16<T>& gt) {
+            Vec16<T> pr, res;
+            load_row((const T*)preds.p[k] + pred_off(k), nv, pr);
+#pragma unroll
+            for (int i = 0; i < V; ++i) res.e[i] = (T)code_encode<CODER>(to_i32(pr.e[i]), to_i32(gt.e[i]));
+            store_row((T*)maps_out.p[k] + cls_off(k), nv, res);
+          };
+          if (nx0 > 0) {
+            if (k0 < 0) store_row(dst + lo_off, nx0, ev);
+            else code_row(k0, nx0, ev);
+          }
+          if (nx1 > 0) code_row(k1, nx1, od);
+        } else {
+          auto decode_row = [&](int k, int32_t nv, Vec16<T>& outv) {
+            Vec16<T> pr, en;
+            load_row((const T*)preds.p[k] + pred_off(k), nv, pr);
+            load_row((const T*)maps_in.p[k] + cls_off(k), nv, en);
+#pragma unroll
+            for (int i = 0; i < V; ++i) outv.e[i] = (T)code_decode<CODER>(to_i32(pr.e[i]), to_i32((TO)en.e[i]));
+          };
+          Vec16<T> ev, od;
+          if (nx0 > 0) {
+            if (k0 < 0) load_row(src + lo_off, nx0, ev);
+            else decode_row(k0, nx0, ev);
+          }
+          if (nx1 > 0) decode_row(k1, nx1, od);
+          if (nx0 == V && nx1 == V && 2 * x0 + 2 * V <= n2) {
+            Vec16<T> a, b2;
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) {
+              a.e[2 * i] = ev.e[i]; a.e[2 * i + 1] = od.e[i];
+              b2.e[2 * i] = ev.e[V / 2 + i]; b2.e[2 * i + 1] = od.e[V / 2 + i];
+            }
+            a.store(dst + hoff);
+            b2.store(dst + hoff + V);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+              if (i < nx0) dst[hoff + 2 * i] = ev.e[i];
+              if (i < nx1) dst[hoff + 2 * i + 1] = od.e[i];
+            }
+          }
+        }
+      }
+  }
+}
+
 template <typename T, int CODER>
 __global__ void __launch_bounds__(kThreads) encode_preds_kernel(const T* __restrict__ hi, Geo g, int nsp, int64_t C,
                                                               CMapPtrs preds, T* __restrict__ lowres, MapPtrs maps,
@@ -304,7 +423,14 @@ int kmp_encode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
   return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
     using T = decltype(tag);
     constexpr int CODER = decltype(coder_c)::value;
-    if (small) {
+    if (small && !std::getenv("KMP_DISABLE_ROWS")) {
+      const cb::MapExt me = cb::map_exts(g, nsp);
+      const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
+      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, false, 3> : cb::rows_code_preds_kernel<T, CODER, false, 2>;
+      k<<<cb::grid_for(items), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)highres, CMapPtrs{}, mp, pp, (T*)lowres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
+          (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)nch, (int32_t)items);
+    } else if (small) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, false, 7> : cb::code_preds_kernel32<T, CODER, false, 3>;
       k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
@@ -342,7 +468,14 @@ int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
   return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
     using T = decltype(tag);
     constexpr int CODER = decltype(coder_c)::value;
-    if (small) {
+    if (small && !std::getenv("KMP_DISABLE_ROWS")) {
+      const cb::MapExt me = cb::map_exts(g, nsp);
+      const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
+      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, true, 3> : cb::rows_code_preds_kernel<T, CODER, true, 2>;
+      k<<<cb::grid_for(items), cb::kThreads, 0, (hipStream_t)stream>>>(
+          (const T*)lowres, mp, MapPtrs{}, pp, (T*)highres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
+          (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)nch, (int32_t)items);
+    } else if (small) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, true, 7> : cb::code_preds_kernel32<T, CODER, true, 3>;
       k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
