@@ -134,15 +134,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   if constexpr (!DEC) {
 #pragma unroll
     for (int t = 0; t < PL + 2; ++t) {
-      N[t] = NR{};
       const int q = c0 - 1 + t;
-      if (q < 0 || (t >= 2 && q - 1 >= Z1)) continue;  // uniform
-      const T* p = hin + 2 * lsrc(q, a.Lz, a.Ez) * hplane;
-      if (a.nt_nodes) {
-        if (live) N[t].own = ld16(p + ho_own);
-      } else {
-        if (live) N[t].own = ld16c(p + ho_own);
+      if (q < 0 || (t >= 2 && q - 1 >= Z1)) {  // uniform
+        N[t] = NR{};
+        continue;
       }
+      N[t].halo = N[t].dn = uint4{};
+      const T* p = hin + 2 * lsrc(q, a.Lz, a.Ez) * hplane;
+      // own node row: unconditional (row Yc is clamped in bounds; a dead lane's value is unused)
+      if (a.nt_nodes) N[t].own = ld16(p + ho_own);
+      else N[t].own = ld16c(p + ho_own);
       if constexpr (ONE) {
         if (need_up) N[t].halo = ld16c(p + ho_up);
         if (need_dn) N[t].dn = ld16c(p + ho_dn);
@@ -152,14 +153,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     }
 #pragma unroll
     for (int u = 0; u < PL; ++u) {
-      O[u] = OR{};
       const int q = c0 + u;
-      if (q >= Z1) continue;
-      const bool vz1 = q < a.Lcz;
+      if (q >= Z1) {  // uniform
+        O[u] = OR{};
+        continue;
+      }
+      // stream rows: unconditional from clamped addresses (row 2Y+1 / plane 2q+1 past the edge
+      // re-read row 2Y / plane 2q; the maps they would feed are not stored there)
+      const int r1 = 2 * Yc + 1 < a.H ? a.W : 0, p1 = 2 * q + 1 < a.D ? hplane : 0;
       const T* p = hin + 2 * q * hplane;
-      if (live && vy1) O[u].e1 = ld16(p + ho_own + a.W);
-      if (live && vz1) O[u].o0 = ld16(p + hplane + ho_own);
-      if (live && vz1 && vy1) O[u].o1 = ld16(p + hplane + ho_own + a.W);
+      O[u].e1 = ld16(p + ho_own + r1);
+      O[u].o0 = ld16(p + p1 + ho_own);
+      O[u].o1 = ld16(p + p1 + ho_own + r1);
     }
   } else {
     auto load_node = [&](int t) __attribute__((always_inline)) {
