@@ -121,7 +121,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     map_parity(3, k, par);
     const int ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
     mplane[k] = ey * a.Ex;
-    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + Yc * a.Ex + X;
+    const int ym = Yc < ey ? Yc : (ey > 0 ? ey - 1 : 0);  // in-bounds row (encode stores are gated by mok_y)
+    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + ym * a.Ex + X;
     mok_y[k] = live && (!par[1] || vy1);
   }
 
@@ -167,56 +168,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       O[u].o1 = ld16(p + p1 + ho_own + r1);
     }
   } else {
+    // own node rows and map rows unconditionally from clamped in-bounds addresses (values of rows
+    // past the edges are never used), halo rows only where a lane needs one
     auto load_node = [&](int t) __attribute__((always_inline)) {
-      N[t] = NR{};
       const int q = c0 - 1 + t;
-      if (q < 0 || (t >= 2 && q - 1 >= Z1)) return;  // uniform
-      const int sz = lsrc(q, a.Lz, a.Ez);
-      if constexpr (DEC) {
-        const T* p = lin + sz * lplane;
-        if (a.nt_nodes) {
-          if (live) N[t].own = ld8(p + lo_own);
-        } else {
-          if (live) N[t].own = ld8c(p + lo_own);
-        }
-        if constexpr (ONE) {
-          if (need_up) N[t].halo = ld8c(p + lo_up);
-          if (need_dn) N[t].dn = ld8c(p + lo_dn);
-        } else {
-          if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
-        }
+      if (q < 0 || (t >= 2 && q - 1 >= Z1)) {  // uniform
+        N[t] = NR{};
+        return;
+      }
+      N[t].halo = N[t].dn = uint2{};
+      const T* p = lin + lsrc(q, a.Lz, a.Ez) * lplane;
+      if (a.nt_nodes) N[t].own = ld8(p + lo_own);
+      else N[t].own = ld8c(p + lo_own);
+      if constexpr (ONE) {
+        if (need_up) N[t].halo = ld8c(p + lo_up);
+        if (need_dn) N[t].dn = ld8c(p + lo_dn);
       } else {
-        const T* p = hin + 2 * sz * hplane;
-        if (a.nt_nodes) {
-          if (live) N[t].own = ld16(p + ho_own);
-        } else {
-          if (live) N[t].own = ld16c(p + ho_own);
-        }
-        if constexpr (ONE) {
-          if (need_up) N[t].halo = ld16c(p + ho_up);
-          if (need_dn) N[t].dn = ld16c(p + ho_dn);
-        } else {
-          if (need_up || need_dn) N[t].halo = ld16c(p + (first ? ho_up : ho_dn));  // this lane's halo row
-        }
+        if (need_up || need_dn) N[t].halo = ld8c(p + (first ? lo_up : lo_dn));  // this lane's halo row
       }
     };
     auto load_out = [&](int u) __attribute__((always_inline)) {
-      O[u] = OR{};
       const int q = c0 + u;
-      if (q >= Z1) return;
-      const bool vz1 = q < a.Lcz;
-      if constexpr (DEC) {
+      if (q >= Z1) {  // uniform
+        O[u] = OR{};
+        return;
+      }
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          int par[3];
-          map_parity(3, k, par);
-          if (mok_y[k] && (!par[0] || vz1)) O[u].mv[k] = ld8(mbase[k] + q * mplane[k]);
-        }
-      } else {
-        const T* p = hin + 2 * q * hplane;
-        if (live && vy1) O[u].e1 = ld16(p + ho_own + a.W);
-        if (live && vz1) O[u].o0 = ld16(p + hplane + ho_own);
-        if (live && vz1 && vy1) O[u].o1 = ld16(p + hplane + ho_own + a.W);
+      for (int k = 0; k < 7; ++k) {
+        int par[3];
+        map_parity(3, k, par);
+        const int ez = par[0] ? a.Lcz : a.Ez;
+        if (ez > 0 && mplane[k] > 0) O[u].mv[k] = ld8(mbase[k] + (q < ez ? q : ez - 1) * mplane[k]);  // uniform
+        else O[u].mv[k] = uint2{};
       }
     };
     load_node(0);
