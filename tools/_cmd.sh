@@ -1,11 +1,13 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/ab; rm -rf $O; mkdir -p $O
-for rep in 1 2 3; do for v in 0 1; do
-  KMP_W3_DEC_ORDER=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/v${v}_$rep -o run -- python3 tools/ktime.py volume 0 30 > $O/v${v}_$rep.log 2>&1 || exit 1
-  f=$(find $O/v${v}_$rep -name 'run_kernel_stats.csv'); python3 -c "
-import csv,sys
+O=gpurun_out/w3ab; rm -rf $O; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_codec.py tests/test_gpu_fuzz.py tests/test_gpu_large.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $O/pytest.log | head -80; exit $rc; }
+for rep in 1 2 3; do for lib in tools/ab_base.so kompressor_amd/libkompressor_hip.so; do for wl in "image 0"; do
+  KOMPRESSOR_HIP_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$rep$(basename $lib) -o run -- python3 tools/ktime.py $wl 30 > /dev/null 2>&1 || exit 1
+  f=$(find $O/$rep$(basename $lib) -name 'run_kernel_stats.csv'); python3 -c "
+import csv
 for r in csv.DictReader(open('$f')):
-    if 'wave3d_plane' in r['Name']: print('order=$v rep=$rep', round(float(r['AverageNs'])/1e3,2), 'DEC' if 'true' in r['Name'] else 'ENC')
+    if 'kmp' in r['Name']: print('$(basename $lib)', 'rep=$rep', round(float(r['AverageNs'])/1e3,2), 'DEC' if ', true' in r['Name'] else 'ENC')
 "
-done; done
+done; done; done
