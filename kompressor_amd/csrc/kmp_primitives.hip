@@ -459,6 +459,116 @@ __global__ void __launch_bounds__(kThreads) maps_from_predictions_lds_kernel(
   }
 }
 
+// Fused mean predictor on a padded window (u8 / u16, C == 1): the z-rolling LDS aggregation of
+// maps_from_predictions_lds_kernel with the staged cell plane computed on the fly -- cell
+// (z, y, x) = astype(T)(f32 sum of its (2p+2)^d window nodes / N), exactly cell_mean_padded --
+// so the cell means are written once (as the C map, straight from LDS) and never re-read from
+// HBM; the two element kernels below (cell means, then maps) stay for the other layouts.
+constexpr int kMpCpt = 4;  // cells per thread per staged plane (host-checked)
+
+template <typename T, int NSP>
+__global__ void __launch_bounds__(kThreads) mean_predict_lds_kernel(
+    const T* __restrict__ win, E3<int32_t> S, int p, int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs, int32_t YB,
+    int32_t XO, int32_t ZC, int32_t nzc, int32_t nyb, int32_t nxb, int32_t RP) {
+  constexpr int NM = NSP == 3 ? 7 : 3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* lds = (uint32_t*)smem;  // [2 slots][YB + 1 rows][RP] cell means
+  int32_t w = (int32_t)blockIdx.x;
+  const int32_t xb = w % nxb; w /= nxb;
+  const int32_t yb = w % nyb; w /= nyb;
+  const int32_t zc = w % nzc;
+  const int32_t b = w / nzc;
+  const int32_t y0 = yb * YB, ox0 = xb * XO;
+  const int32_t xc0 = ox0 > 0 ? ox0 - 1 : 0;
+  const int32_t xc1 = (ox0 + XO - 1 < Lcx - 1) ? ox0 + XO - 1 : Lcx - 1;
+  const int32_t ncx = xc1 - xc0 + 1;
+  const int32_t cz = NSP == 3 ? Lcz : 1;
+  const int32_t fz = NSP == 3 ? Lcz + 1 : 1;
+  const int32_t oz0 = zc * ZC, oz1 = (oz0 + ZC < fz) ? oz0 + ZC : fz;
+  const int kk = 2 * p + 2, kz = NSP == 3 ? kk : 1;
+  const float nn = (float)(kz * kk * kk);
+  const int32_t slice = (YB + 1) * ncx;
+  const float rcp = 1.0f / (float)ncx;
+
+  uint32_t buf[kMpCpt];
+  auto fetch = [&](int32_t z) {  // cell means of cell plane z -> registers
+#pragma unroll
+    for (int c = 0; c < kMpCpt; ++c) {
+      buf[c] = 0;
+      const int32_t i = threadIdx.x + c * kThreads;
+      if (i >= slice) continue;
+      int32_t r, x;
+      divmod_small(i, ncx, rcp, r, x);
+      const int32_t y = y0 - 1 + r;
+      if (y < 0 || y >= Lcy) continue;
+      float sum = 0.0f;  // f32 sum in feature order (exact here: < 2^24)
+      for (int dz = 0; dz < kz; ++dz)
+        for (int dy = 0; dy < kk; ++dy) {
+          const T* row = win + ((b * S.e[0] + z + dz) * S.e[1] + y + dy) * S.e[2] + xc0 + x;
+          for (int dx = 0; dx < kk; ++dx) sum += (float)row[dx];
+        }
+      buf[c] = (uint32_t)cast_f32<T>(sum / nn);
+    }
+  };
+  auto put = [&](int32_t z) {
+    uint32_t* base = lds + (z & 1) * (YB + 1) * RP;
+#pragma unroll
+    for (int c = 0; c < kMpCpt; ++c) {
+      const int32_t i = threadIdx.x + c * kThreads;
+      if (i >= slice) continue;
+      int32_t r, x;
+      divmod_small(i, ncx, rcp, r, x);
+      base[r * RP + x] = buf[c];
+    }
+  };
+  auto at = [&](int32_t z, int32_t r, int32_t x) -> uint32_t { return lds[((z & 1) * (YB + 1) + r) * RP + (x - xc0)]; };
+
+  if (NSP == 3 && oz0 >= 1) {
+    fetch(oz0 - 1);
+    put(oz0 - 1);
+  }
+  if (oz0 < cz) {
+    fetch(oz0);
+    put(oz0);
+  }
+  __syncthreads();
+
+  for (int32_t oz = oz0; oz < oz1; ++oz) {
+    const bool more = oz + 1 < oz1 && oz + 1 < cz;
+    if (more) fetch(oz + 1);
+    for (int32_t i = threadIdx.x; i < YB * XO; i += kThreads) {
+      const int32_t xo = i % XO, r = i / XO;
+      const int32_t oy = y0 + r, ox = ox0 + xo;
+      if (oy > Lcy || ox > Lcx) continue;
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        int par[3];
+        map_parity(NSP, k, par);
+        const int32_t e0 = NSP == 3 ? (par[0] ? Lcz : Lcz + 1) : 1, e1 = par[1] ? Lcy : Lcy + 1,
+                      e2 = par[2] ? Lcx : Lcx + 1;
+        if (oz >= e0 || oy >= e1 || ox >= e2) continue;
+        Contrib cb[4];
+        const int nc = map_contribs(NSP, k, cb);
+        uint32_t sum = 0, cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j >= nc) break;
+          const int32_t z = oz - cb[j].dz, y = oy - cb[j].dy, x = ox - cb[j].dx;
+          if (z >= 0 && z < cz && y >= 0 && y < Lcy && x >= 0 && x < Lcx) {
+            sum += at(z, r + 1 - cb[j].dy, x);
+            ++cnt;
+          }
+        }
+        ((T*)outs.p[k])[((b * e0 + oz) * e1 + oy) * e2 + ox] = (T)(k == center_map(NSP) ? sum : sum >> (cnt >> 1));
+      }
+    }
+    if (!more) break;  // uniform
+    __syncthreads();
+    put(oz + 1);
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Mean predictor on a padded lowres window (tests/volume/test_encode_decode.py:46-53):
 // cell mean = astype(T)(f32 sum of the (2p+2)^d neighbourhood / N), then the map aggregation.
@@ -1092,6 +1202,26 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     using T = decltype(tag);
     T* cm = (T*)outs.p[center_map(nsp)];
     const bool small = fits32({vol(B, S, C), total});
+    if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
+      if (rows_ok(C, {vol(B, S, C), total}) && padding <= 1) {
+        const int32_t XO = (int32_t)std::min<int64_t>(cells.e[2] + 1, 64);
+        const int32_t YB = std::max(1, std::min(8, kThreads / XO));
+        const int32_t nyb = (int32_t)ceil_div(cells.e[1] + 1, YB), nxb = (int32_t)ceil_div(cells.e[2] + 1, XO);
+        const int32_t RP = XO + 1;
+        const int64_t fz = nsp == 3 ? cells.e[0] + 1 : 1;
+        const int64_t want = ceil_div(4096, B * nyb * nxb);
+        const int32_t ZC = (int32_t)ceil_div(fz, std::max<int64_t>(1, std::min<int64_t>(want, fz)));
+        const int32_t nzc = (int32_t)ceil_div(fz, ZC);
+        const size_t lds = (size_t)2 * (YB + 1) * RP * sizeof(uint32_t);
+        const int64_t nblk = B * nzc * nyb * nxb;
+        if ((int64_t)(YB + 1) * RP > kThreads * kMpCpt) return fail(KMP_ERR_ARG, "mean_predict_maps: tile");
+        auto kern = nsp == 3 ? mean_predict_lds_kernel<T, 3> : mean_predict_lds_kernel<T, 2>;
+        kern<<<(unsigned)nblk, kThreads, lds, (hipStream_t)stream>>>(
+            (const T*)padded_lowres, e32(S), padding, (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2],
+            outs, YB, XO, ZC, nzc, nyb, nxb, RP);
+        return check_launch("mean_predict_maps");
+      }
+    }
     int st = with_index(small, [&](auto itag) {
       using I = decltype(itag);
       cell_mean_map_kernel<T, I><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>(
