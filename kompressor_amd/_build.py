@@ -51,16 +51,33 @@ def build(verbose=True, jobs=None):
     stamp = os.path.join(BUILD, 'objects.txt')  # relink when the set of sources changes too
     listing = '\n'.join(sorted(objs))
     same_set = os.path.exists(stamp) and open(stamp).read() == listing
-    if same_set and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
-        return LIB
-    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB + '.tmp']
+    if not (same_set and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs)):
+        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB + '.tmp']
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(LIB + '.tmp', LIB)
+        with open(stamp, 'w') as f:
+            f.write(listing)
+    _build_capi_example(verbose)
+    return LIB
+
+
+def _build_capi_example(verbose):
+    """tools/capi_example: the C-ABI from a plain C++ host (no Python), linked to the in-tree
+    library by a relative rpath so it runs from any checkout."""
+    root = os.path.dirname(HERE)
+    src = os.path.join(root, 'tools', 'capi_example.cpp')
+    exe = os.path.join(root, 'tools', 'capi_example')
+    if not os.path.exists(src):
+        return
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(LIB)):
+        return
+    cmd = [HIPCC, '-O2', f'--offload-arch={ARCH}', src, '-o', exe, f'-L{HERE}', '-lkompressor_hip',
+           '-Wl,-rpath,$ORIGIN/../kompressor_amd']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + '.tmp', LIB)
-    with open(stamp, 'w') as f:
-        f.write(listing)
-    return LIB
 
 
 if __name__ == '__main__':
