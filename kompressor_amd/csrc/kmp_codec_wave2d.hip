@@ -241,6 +241,163 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   }
 }
 
+// uint8 form of the mean kernel (BASELINE config C2), SWAR: the lane's 8 cells travel as 4 words
+// of two 16-bit lanes each, so every node / mean / prediction / residual step is one 32-bit op
+// for two cells (node pair sums <= 510, means <= 255: no carry between the halves; residuals add
+// 256 per half before subtracting, so no borrow).  Bytes are split / merged with v_perm.  The
+// arithmetic is the generic kernel's above, element for element; the SQ counters showed that
+// kernel's VALU busy 67 % of its cycles at C2.
+__device__ __forceinline__ uint32_t lo_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c02u); }
+__device__ __forceinline__ uint32_t pack_pairs(uint32_t a, uint32_t b) {  // 16-bit-lane bytes -> 4 bytes
+  return __builtin_amdgcn_perm(b, a, 0x06040200u);
+}
+__device__ __forceinline__ uint32_t shift_pairs(uint32_t hi, uint32_t lo) {  // {lo.hi16, hi.lo16}
+  return __builtin_amdgcn_alignbit(hi, lo, 16);
+}
+
+template <bool DEC>
+__global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
+  constexpr int VX = 8;
+  constexpr uint32_t B8 = 0x00ff00ffu;
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+
+  const int lane = threadIdx.x & 63;
+  const int wv_ = threadIdx.x >> 6;
+  const int tx = lane % a.txn;
+  const int r = lane / a.txn;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int grp = blk % a.ngrp;
+  const int64_t b = blk / a.ngrp;
+  const int Y0 = (grp * a.nwv + wv_) * a.rows;
+  if (Y0 >= a.Ey) return;  // whole idle wave
+  const int Y = Y0 + r;
+  const bool live = Y < a.Ey;
+  const int Yc = live ? Y : a.Ey - 1;
+  const bool first = r == 0;
+  const bool last = r == a.rows - 1 || Y == a.Ey - 1;
+  const bool vy1 = Y < a.Lcy;
+  const bool vy0 = Y >= 1;
+  const bool need_halo = live && ((first && Y0 >= 1) || (last && vy1));
+  const int yh = first ? (Y0 >= 1 ? Y0 - 1 : 0) : lsrc(Yc + 1, a.Ly, a.Ey);
+  const bool xlast = tx == a.txn - 1;
+
+  const int64_t himg = (int64_t)a.H * a.W;
+  const int hx = 2 * X;
+  const uint8_t* hin = DEC ? nullptr : (const uint8_t*)a.hi_in + b * himg;
+  uint8_t* hout = DEC ? (uint8_t*)a.hi_out + b * himg : nullptr;
+  const uint8_t* lin = DEC ? (const uint8_t*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
+  const int64_t m_lr = (b * a.Lcy + Yc) * a.Ex + X;
+  const int64_t m_ud = (b * a.Ey + Yc) * a.Ex + X;
+
+  V own{}, halo{};
+  uint4 o0 = make_uint4(0, 0, 0, 0);
+  uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
+  if constexpr (DEC) {
+    if (live) own = ld8c(lin + Yc * a.Ex + X);
+    if (need_halo) halo = ld8c(lin + yh * a.Ex + X);
+    if (live && vy1) mv[0] = ld8((const uint8_t*)a.maps.p[0] + m_lr);
+    if (live) mv[1] = ld8((const uint8_t*)a.maps.p[1] + m_ud);
+    if (live && vy1) mv[2] = ld8((const uint8_t*)a.maps.p[2] + m_lr);
+  } else {
+    if (live) own = ld16c(hin + 2 * Yc * a.W + hx);
+    if (need_halo) halo = ld16c(hin + 2 * yh * a.W + hx);
+    if (live && vy1) o0 = ld16(hin + (2 * Yc + 1) * a.W + hx);
+  }
+
+  // nodes as pairs: N[k] = {n[2k], n[2k+1]}
+  uint32_t N[4], NH[4], XO[4] = {0, 0, 0, 0};
+  if constexpr (DEC) {
+    N[0] = lo_pair(own.x); N[1] = hi_pair(own.x); N[2] = lo_pair(own.y); N[3] = hi_pair(own.y);
+    NH[0] = lo_pair(halo.x); NH[1] = hi_pair(halo.x); NH[2] = lo_pair(halo.y); NH[3] = hi_pair(halo.y);
+  } else {
+    const uint32_t w[4] = {own.x, own.y, own.z, own.w}, h[4] = {halo.x, halo.y, halo.z, halo.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      N[k] = w[k] & B8;
+      XO[k] = (w[k] >> 8) & B8;  // row 2Y odd x: the UD map's ground truth
+      NH[k] = h[k] & B8;
+    }
+  }
+  uint32_t nx1 = shdn(N[0], 1), nhx1 = shdn(NH[0], 1);  // node X+8 (low half)
+  if (xlast) {  // the mirrored node Ex-1 (even pad), or no cell at all (odd)
+    nx1 = N[3] >> 16;
+    nhx1 = NH[3] >> 16;
+  }
+  uint32_t M1[4], M0[4];  // cell means of rows Y / Y-1, cells X+2k, X+2k+1
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t h = N[k] + shift_pairs(k < 3 ? N[k + 1] : nx1, N[k]);
+    const uint32_t hh = NH[k] + shift_pairs(k < 3 ? NH[k + 1] : nhx1, NH[k]);
+    const uint32_t below = shdn(h, a.txn);
+    M1[k] = ((h + (last ? hh : below)) >> 2) & B8;
+    const uint32_t above = shup(M1[k], a.txn);
+    M0[k] = first ? ((hh + h) >> 2) & B8 : above;
+  }
+  uint32_t m1l = shup(M1[3], 1) >> 16;  // cell X-1 (the UD prediction needs no left cell)
+  if (!live || Y < a.ybeg || Y >= a.yend) return;
+
+  // validity of cells X-1 .. X+7 (vx[q] = cell X-1+q) as per-half masks
+  bool vx[VX + 1];
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  uint32_t VM[4], BM[4];  // VM: cells X+2k, X+2k+1 valid; BM: both neighbours of the LR pair valid
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    VM[k] = (vx[2 * k + 1] ? 0x0000ffffu : 0u) | (vx[2 * k + 2] ? 0xffff0000u : 0u);
+    BM[k] = (vx[2 * k] && vx[2 * k + 1] ? 0x0000ffffu : 0u) | (vx[2 * k + 1] && vx[2 * k + 2] ? 0xffff0000u : 0u);
+  }
+  m1l = (vy1 && vx[0]) ? m1l : 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    M1[k] = vy1 ? (M1[k] & VM[k]) : 0u;
+    M0[k] = vy0 ? (M0[k] & VM[k]) : 0u;
+  }
+  const bool ud2 = vy0 && vy1;
+  uint32_t PL[4], PU[4];  // LR, UD predictions; C is M1
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t left = shift_pairs(M1[k], k == 0 ? m1l << 16 : M1[k - 1]);  // cells X+2k-1, X+2k
+    const uint32_t sl = left + M1[k];
+    PL[k] = (((sl >> 1) & 0x7fff7fffu) & BM[k]) | (sl & ~BM[k]);
+    const uint32_t su = M0[k] + M1[k];
+    PU[k] = ud2 ? (su >> 1) & 0x7fff7fffu : su;
+  }
+  if constexpr (!DEC) {
+    const uint32_t o[4] = {o0.x, o0.y, o0.z, o0.w};
+    uint32_t rl[4], ru[4], rc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      rl[k] = ((o[k] & B8) + 0x01000100u - PL[k]) & B8;          // LR (1,0): row 2Y+1, even x
+      ru[k] = (XO[k] + 0x01000100u - PU[k]) & B8;                // UD (0,1): row 2Y, odd x
+      rc[k] = (((o[k] >> 8) & B8) + 0x01000100u - M1[k]) & B8;   // C  (1,1): row 2Y+1, odd x
+    }
+    st8((uint8_t*)a.lo_out + m_ud, make_uint2(pack_pairs(N[0], N[1]), pack_pairs(N[2], N[3])));
+    if (vy1) st8((uint8_t*)a.maps.p[0] + m_lr, make_uint2(pack_pairs(rl[0], rl[1]), pack_pairs(rl[2], rl[3])));
+    st8((uint8_t*)a.maps.p[1] + m_ud, make_uint2(pack_pairs(ru[0], ru[1]), pack_pairs(ru[2], ru[3])));
+    if (vy1) st8((uint8_t*)a.maps.p[2] + m_lr, make_uint2(pack_pairs(rc[0], rc[1]), pack_pairs(rc[2], rc[3])));
+  } else {
+    const uint32_t el[4] = {lo_pair(mv[0].x), hi_pair(mv[0].x), lo_pair(mv[0].y), hi_pair(mv[0].y)};
+    const uint32_t eu[4] = {lo_pair(mv[1].x), hi_pair(mv[1].x), lo_pair(mv[1].y), hi_pair(mv[1].y)};
+    const uint32_t ec[4] = {lo_pair(mv[2].x), hi_pair(mv[2].x), lo_pair(mv[2].y), hi_pair(mv[2].y)};
+    uint32_t r0[4], r1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t dl = (PL[k] + el[k]) & B8, du = (PU[k] + eu[k]) & B8, dc = (M1[k] + ec[k]) & B8;
+      r0[k] = N[k] | (du << 8);  // row 2Y:   lowres | UD
+      r1[k] = dl | (dc << 8);    // row 2Y+1: LR | C
+    }
+    uint8_t* h0 = hout + 2 * Yc * a.W + hx;
+    st16(h0, make_uint4(r0[0], r0[1], r0[2], r0[3]));
+    if (vy1) st16(h0 + a.W, make_uint4(r1[0], r1[1], r1[2], r1[3]));
+  }
+}
+
 }  // namespace w2
 
 static int w2_env(const char* name, int dflt) {
@@ -294,6 +451,10 @@ static void launch_wave2d(bool one, bool lin, dim3 grid, dim3 block, hipStream_t
     else w2::wave2d_kernel<T, DEC, true, false><<<grid, block, 0, s>>>(a);
   } else {
     if (lin) w2::wave2d_kernel<T, DEC, false, true><<<grid, block, 0, s>>>(a);
+    // SWAR u8 form: decode 24.0 vs 24.8 us at C2 on one box; encode 26.2 vs 25.4 (kept behind a
+    // knob: the encode is bound by its row loads, not VALU) -- profiles/round1/ab_wave2d_swar.log
+    else if (std::is_same<T, uint8_t>::value && !w2_env("KMP_DISABLE_SWAR", 0) && (DEC || w2_env("KMP_W2_SWAR_ENC", 0)))
+      w2::wave2d_u8_kernel<DEC><<<grid, block, 0, s>>>(a);
     else w2::wave2d_kernel<T, DEC, false, false><<<grid, block, 0, s>>>(a);
   }
 }

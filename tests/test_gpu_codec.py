@@ -380,6 +380,40 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(7, 9), padding=p), x)
 
 
+@pytest.mark.parametrize('shape', [
+    (8, 256, 256, 1),      # C2 geometry: 16 lanes per row, 4 rows per wave
+    (3, 35, 64, 1),        # odd height: the last cell row is missing, Ey = 18, 16 rows per wave
+    (2, 31, 128, 1),       # odd height, 8 lanes per row
+    (4, 18, 32, 1),        # 2 lanes per row, Ey = 9 < 32 rows per wave
+    (2, 9, 16, 1),         # one lane per row, Ey = 5 < rows
+    (1, 40, 1024, 1),      # 64 lanes per row: the one-row wave (generic kernel only)
+])
+@pytest.mark.parametrize('mode', ['swar_dec', 'swar_both', 'generic'])
+def test_wave2d_u8_p0_matches_oracle(kom, shape, mode, monkeypatch):
+    """The p = 0 uint8 image kernels of kmp_codec_wave2d.hip -- the SWAR form (decode by default,
+    encode behind KMP_W2_SWAR_ENC) and the generic per-cell form (KMP_DISABLE_SWAR) -- against
+    the oracle, whole-image and chunked."""
+    if mode == 'swar_both':
+        monkeypatch.setenv('KMP_W2_SWAR_ENC', '1')
+    elif mode == 'generic':
+        monkeypatch.setenv('KMP_DISABLE_SWAR', '1')
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = kom.image, oracle.image
+    x = np.random.default_rng(13).integers(0, 256, size=shape, dtype=np.int64).astype(np.uint8)
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(0, 2), ons.encode_values_uint8, x)
+    pred = kom.MeanPredictor(0, 2)
+    lo, (maps, dims) = ns.encode(pred, ns.encode_values_uint8, x)
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    assert np.array_equal(ns.decode(pred, ns.decode_values_uint8, lo, (maps, dims)), x)
+    lo2, (maps2, _) = ns.encode_chunks(pred, ns.encode_values_uint8, x, chunk=5)
+    assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
+    assert np.array_equal(ns.decode_chunks(pred, ns.decode_values_uint8, lo, (maps, dims), chunk=(7, 9)), x)
+
+
 @pytest.mark.parametrize('shape,dtype', [
     ((4, 16, 16, 16, 1), np.uint32),
     ((8, 9, 10, 32, 1), np.uint32),        # odd depth, 8 rows per wave
