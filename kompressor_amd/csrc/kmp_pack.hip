@@ -6,24 +6,22 @@
 // small signed values modulo 2^W, so each sample is zigzag-mapped (z = (s << 1) ^ (s >> (W-1)) of
 // its signed W-bit reading: 0, -1, 1, -2 ... -> 0, 1, 2, 3 ...), and every block of 64 samples is
 // stored as `width` 64-bit bit-planes, width = the bit length of the block's largest z (0 for an
-// all-zero block).  On a 64-lane wavefront one block is one wave, and bit-plane i of the block is
-// exactly ``ballot((z >> i) & 1)``: packing is `width` ballots, unpacking `width` uniform words
-// read by every lane -- no cross-lane bit shuffling at all.
+// all-zero block).  Plane b of a block is the 64-bit word whose bit s is bit b of sample s.
 //
-// Launches: widths -> per-chunk exclusive scan of the widths (4096 blocks per workgroup) -> scan
+// Launches: widths -> per-chunk exclusive scan of the widths (kChunk blocks per workgroup) -> scan
 // of the chunk sums (one workgroup) -> pack / unpack.  The payload offset of block b, in 64-bit
-// words, is chunk_base[b / 4096] + local[b].  Every kernel moves the samples as one 16-byte
-// vector per lane: a wave covers SPL = 128 / W blocks per step (16 B = SPL samples per lane), so
-// it has one load in flight per SPL blocks instead of one 2-byte load per block; pack / unpack
-// turn that layout into one-sample-per-lane (the ballot layout) through 1 KB of LDS per wave.
+// words, is chunk_base[b / kChunk] + local[b].  Every kernel gives a lane 8 consecutive samples
+// (one 8 / 16 / 32-byte load), so a wave step covers 8 blocks; pack / unpack build the planes with
+// register bit transposes and a cross-lane byte transpose (see ``xtr8``), no LDS, no ballots --
+// the ballot-per-plane form was VALU-bound at 7 instructions per plane.
 #include "kmp_common.h"
 
 namespace kmp {
 namespace pk {
 
 constexpr int kBlock = 64;         // samples per block == lanes per wave
-constexpr int kChunk = 4096;       // blocks per scan chunk
-constexpr int kScanThreads = 256;  // 16 blocks per thread
+constexpr int kChunk = 1024;       // blocks per scan chunk (256 chunks for a 32 MiB u16 map)
+constexpr int kScanThreads = 256;  // 4 blocks per thread
 constexpr int kPackHeadMax = 128;  // header bytes a kmp_pack_header call can write
 
 template <int W>
@@ -56,49 +54,174 @@ __device__ __forceinline__ void store_sample(void* x, int64_t i, uint32_t v) {
   else ((uint32_t*)x)[i] = v;
 }
 
-// 16 bytes of samples per lane: lanes g*LPB .. g*LPB+LPB-1 of a wave step hold block g (SPL blocks)
+// ---- lane layout: 8 consecutive samples per lane, 8 lanes per block, 8 blocks per wave step ----
+// A lane's 8 samples are W/4 32-bit words (2, 4 or 8).  Planes are formed without ballots: the
+// lane's samples are bit-transposed in registers (8x8 bit transposes, one per sample byte), which
+// gives, per 8-plane group p, the byte of planes 8p .. 8p+7 this lane contributes (bit k = its
+// sample k); an 8x8 BYTE transpose across the block's 8 lanes (DPP) then leaves lane j holding the
+// whole 64-bit plane 8p+j.  Zigzag is applied in the plane domain (z-plane 0 = the sign plane,
+// z-plane b = s-plane b-1 ^ sign plane).  About 12 VALU instructions per block for 16-bit samples,
+// against ~80 for one ballot per plane.
 template <int W>
-struct Lay {
-  static constexpr int SPL = 128 / W;       // samples per lane == blocks per wave step
-  static constexpr int LPB = kBlock / SPL;  // lanes per block
+struct Sw {
+  static constexpr int NW = W / 4;  // 32-bit words per lane (8 samples)
+  static constexpr int NP = W / 8;  // 8-plane groups (64-bit words as lo / hi)
 };
+typedef uint32_t u32x2a1 __attribute__((ext_vector_type(2), aligned(1)));
 typedef uint32_t u32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
 
 template <int W>
-__device__ __forceinline__ u32x4v load16(const void* x, int64_t n, int64_t i0) {  // samples i0 .. i0+SPL-1
-  constexpr int SPL = Lay<W>::SPL;
-  if (i0 + SPL <= n) return *(const u32x4a1*)((const char*)x + i0 * (W / 8));
-  u32x4v v = {0u, 0u, 0u, 0u};
-  for (int e = 0; e < SPL; ++e) {
-    if (i0 + e >= n) break;
-    const uint32_t s = load_sample<W>(x, i0 + e);
-    v[(e * W) / 32] |= s << ((e * W) % 32);
+__device__ __forceinline__ void load8s(const void* x, int64_t n, int64_t i0, uint32_t (&w)[Sw<W>::NW]) {
+  const char* p = (const char*)x + i0 * (W / 8);
+  if (i0 + 8 <= n) {
+    if constexpr (W == 8) {
+      const u32x2a1 v = *(const u32x2a1*)p;
+      w[0] = v[0]; w[1] = v[1];
+    } else {
+#pragma unroll
+      for (int q = 0; q < W / 16; ++q) {
+        const u32x4a1 v = *(const u32x4a1*)(p + 16 * q);
+        w[4 * q] = v[0]; w[4 * q + 1] = v[1]; w[4 * q + 2] = v[2]; w[4 * q + 3] = v[3];
+      }
+    }
+    return;
   }
-  return v;
+#pragma unroll
+  for (int k = 0; k < Sw<W>::NW; ++k) w[k] = 0u;
+  for (int e = 0; e < 8; ++e) {
+    if (i0 + e >= n) break;
+    w[(e * W) / 32] |= load_sample<W>(x, i0 + e) << ((e * W) % 32);
+  }
 }
 template <int W>
-__device__ __forceinline__ uint32_t elem(const u32x4v& v, int e) {
-  if constexpr (W == 32) return v[e];
-  else return (v[(e * W) / 32] >> ((e * W) % 32)) & ((1u << W) - 1u);
+__device__ __forceinline__ void store8s(void* x, int64_t n, int64_t i0, const uint32_t (&w)[Sw<W>::NW]) {
+  char* p = (char*)x + i0 * (W / 8);
+  if (i0 + 8 <= n) {
+    if constexpr (W == 8) {
+      *(u32x2a1*)p = u32x2a1{w[0], w[1]};
+    } else {
+#pragma unroll
+      for (int q = 0; q < W / 16; ++q) *(u32x4a1*)(p + 16 * q) = u32x4a1{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+    }
+    return;
+  }
+  for (int e = 0; e < 8; ++e) {
+    if (i0 + e >= n) break;
+    const uint32_t v = W == 32 ? w[e] : (w[(e * W) / 32] >> ((e * W) % 32)) & ((1u << (W & 31)) - 1u);
+    store_sample<W>(x, i0 + e, v);
+  }
 }
 
-// wave step: widths of SPL consecutive blocks (OR within the lane, then across its LPB lanes)
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {  // bytes 0-3 lo, 4-7 hi
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// 8x8 bit transpose of the 64-bit (lo, hi): bit 8r + c <-> bit 8c + r
+__device__ __forceinline__ void tr8x8(uint32_t& lo, uint32_t& hi) {
+  uint32_t t;
+  t = (lo ^ (lo >> 7)) & 0x00AA00AAu; lo ^= t ^ (t << 7);
+  t = (hi ^ (hi >> 7)) & 0x00AA00AAu; hi ^= t ^ (t << 7);
+  t = (lo ^ (lo >> 14)) & 0x0000CCCCu; lo ^= t ^ (t << 14);
+  t = (hi ^ (hi >> 14)) & 0x0000CCCCu; hi ^= t ^ (t << 14);
+  t = (lo ^ (hi << 4)) & 0xF0F0F0F0u; lo ^= t; hi ^= t >> 4;
+}
+
+// samples -> X[p] (byte k = byte p of sample k) and back
+template <int W>
+__device__ __forceinline__ void gather_bytes(const uint32_t (&w)[Sw<W>::NW], uint32_t (&X)[Sw<W>::NP][2]) {
+  if constexpr (W == 8) {
+    X[0][0] = w[0]; X[0][1] = w[1];
+  } else if constexpr (W == 16) {
+    X[0][0] = perm(w[1], w[0], 0x06040200u); X[0][1] = perm(w[3], w[2], 0x06040200u);
+    X[1][0] = perm(w[1], w[0], 0x07050301u); X[1][1] = perm(w[3], w[2], 0x07050301u);
+  } else {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        X[p][h] = perm(w[4 * h + 1], w[4 * h], 0x0c0c0000u | ((4u + p) << 8) | p) |
+                  perm(w[4 * h + 3], w[4 * h + 2], ((4u + p) << 24) | ((uint32_t)p << 16) | 0x0c0cu);
+  }
+}
+template <int W>
+__device__ __forceinline__ void scatter_bytes(const uint32_t (&X)[Sw<W>::NP][2], uint32_t (&w)[Sw<W>::NW]) {
+  if constexpr (W == 8) {
+    w[0] = X[0][0]; w[1] = X[0][1];
+  } else if constexpr (W == 16) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      w[2 * h] = perm(X[1][h], X[0][h], 0x05010400u);
+      w[2 * h + 1] = perm(X[1][h], X[0][h], 0x07030602u);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int h = k >> 2, b = k & 3;
+      w[k] = perm(X[1][h], X[0][h], 0x0c0c0000u | ((4u + b) << 8) | b) |
+             perm(X[3][h], X[2][h], ((4u + b) << 24) | ((uint32_t)b << 16) | 0x0c0cu);
+    }
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+// 8x8 BYTE transpose across lanes j = lane & 7 (row j = the lane's (lo, hi)): afterwards lane j
+// holds column j.  Three exchange stages (lane distance 4, 2, 1), each swapping the off-diagonal
+// sub-blocks: lanes with bit d clear keep columns with bit d clear and take the partner's.
+__device__ __forceinline__ void xtr8(uint32_t& lo, uint32_t& hi, int j) {
+  {  // d = 4: 32-bit halves (row_shl:4 reads lane l+4, row_shr:4 lane l-4; both stay in the 8)
+    const uint32_t up = dpp<0x104>(lo), dn = dpp<0x114>(hi);
+    if (j & 4) lo = dn;
+    else hi = up;
+  }
+  {  // d = 2: 16-bit units (quad_perm [2,3,0,1])
+    const bool odd = j & 2;
+    const uint32_t recv = dpp<0x4E>(perm(hi, lo, odd ? 0x05040100u : 0x07060302u));
+    lo = perm(recv, lo, odd ? 0x03020504u : 0x05040100u);
+    hi = perm(recv, hi, odd ? 0x03020706u : 0x07060100u);
+  }
+  {  // d = 1: bytes (quad_perm [1,0,3,2])
+    const bool odd = j & 1;
+    const uint32_t recv = dpp<0xB1>(perm(hi, lo, odd ? 0x06040200u : 0x07050301u));
+    lo = perm(recv, lo, odd ? 0x03050104u : 0x05020400u);
+    hi = perm(recv, hi, odd ? 0x03070106u : 0x07020600u);
+  }
+}
+
+// per block OR of the zigzag samples -> width; lane 8g+0 writes block g's
 template <int W>
 __global__ void __launch_bounds__(256) widths_kernel(const void* __restrict__ x, int64_t n, uint8_t* __restrict__ widths,
                                                    int64_t nb) {
-  constexpr int SPL = Lay<W>::SPL, LPB = Lay<W>::LPB;
   const int lane = threadIdx.x & 63;
-  const int64_t nstep = (nb + SPL - 1) / SPL;
+  const int64_t nstep = (nb + 7) / 8;
   for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
        st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const u32x4v v = load16<W>(x, n, st * SPL * kBlock + (int64_t)lane * SPL);
-    uint32_t o = 0;
+    uint32_t w[Sw<W>::NW];
+    load8s<W>(x, n, st * 512 + (int64_t)lane * 8, w);
+    // OR of the zigzag samples without forming them: z = ((s ^ m) << 1) | (m & 1), m = the sign
+    // replicated, so OR z = (OR (s ^ m)) << 1 | (any sample negative)
+    uint32_t acc = 0, neg = 0;
 #pragma unroll
-    for (int e = 0; e < SPL; ++e) o |= zigzag<W>(elem<W>(v, e));
-#pragma unroll
-    for (int d = 1; d < LPB; d <<= 1) o |= (uint32_t)__shfl_xor((int)o, d, 64);
-    const int64_t blk = st * SPL + lane / LPB;
-    if (lane % LPB == 0 && blk < nb) widths[blk] = (uint8_t)(o ? 32 - __clz(o) : 0);
+    for (int k = 0; k < Sw<W>::NW; ++k) {
+      uint32_t m;
+      if constexpr (W == 8) m = perm(w[k], w[k] << 8, 0x0b090a08u);  // sign bits 7 / 15 / 23 / 31 per byte
+      else if constexpr (W == 16) m = (uint32_t)((int32_t)(w[k] << 16) >> 31 & 0xffff) | (uint32_t)((int32_t)w[k] >> 31 << 16);
+      else m = (uint32_t)((int32_t)w[k] >> 31);
+      acc |= w[k] ^ m;
+      neg |= m;
+    }
+    if constexpr (W == 8) acc |= (acc >> 16) | (acc >> 8) | (acc >> 24);
+    else if constexpr (W == 16) acc |= acc >> 16;
+    uint32_t o = ((acc & ((W == 32) ? 0xffffffffu : ((1u << (W & 31)) - 1u))) << 1) | (neg ? 1u : 0u);
+    o |= dpp<0xB1>(o);
+    o |= dpp<0x4E>(o);
+    const uint32_t up = dpp<0x104>(o), dn = dpp<0x114>(o);  // both in full exec: DPP reads of lanes
+    o |= (lane & 4) ? dn : up;                                 // masked off by a branch return ``old``
+    const int64_t blk = st * 8 + (lane >> 3);
+    if ((lane & 7) == 0 && blk < nb) widths[blk] = (uint8_t)(o ? 32 - __clz(o) : 0);
   }
 }
 
@@ -156,109 +279,87 @@ __global__ void __launch_bounds__(1024) scan_chunks_kernel(const uint64_t* __res
   if (threadIdx.x == 0) *total = carry;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// wave step: SPL blocks; samples land in LDS as 16 B per lane and are re-read one per lane per
-// block; lane j < SPL fetches block j's width and offset, broadcast with readlane
+// wave step: 8 blocks; lane j of block g stores planes 8p + j < width, contiguous per block
 template <int W>
 __global__ void __launch_bounds__(256) pack_kernel(const void* __restrict__ x, int64_t n,
                                                  const uint8_t* __restrict__ widths, const uint32_t* __restrict__ local,
                                                  const uint64_t* __restrict__ cbase, int64_t nb,
                                                  uint64_t* __restrict__ payload) {
-  constexpr int SPL = Lay<W>::SPL;
-  __shared__ u32x4v stage[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t nstep = (nb + SPL - 1) / SPL;
+  constexpr int NP = Sw<W>::NP;
+  const int lane = threadIdx.x & 63, j = lane & 7;
+  const int64_t nstep = (nb + 7) / 8;
   for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
        st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int64_t blk0 = st * SPL;
-    const u32x4v v = load16<W>(x, n, blk0 * kBlock + (int64_t)lane * SPL);
-    uint32_t wj = 0;
-    uint64_t oj = 0;
-    if (lane < SPL && blk0 + lane < nb) {
-      wj = widths[blk0 + lane];
-      oj = cbase[(blk0 + lane) / kChunk] + local[blk0 + lane];
+    const int64_t blk = st * 8 + (lane >> 3);
+    uint32_t w[Sw<W>::NW];
+    load8s<W>(x, n, st * 512 + (int64_t)lane * 8, w);
+    int wd = 0;
+    uint64_t off = 0;
+    if (blk < nb) {
+      wd = widths[blk];
+      off = cbase[blk / kChunk] + local[blk];
     }
-    stage[wv][lane] = v;
-    wave_lds_sync();
-    const unsigned char* sb = (const unsigned char*)stage[wv];
-    for (int g = 0; g < SPL; ++g) {
-      if (blk0 + g >= nb) break;  // uniform
-      const int w = (int)__builtin_amdgcn_readlane(wj, g);
-      const uint64_t off = readlane64(oj, g);
-      uint32_t smp;
-      if constexpr (W == 8) smp = sb[g * 64 + lane];
-      else if constexpr (W == 16) smp = ((const uint16_t*)sb)[g * 64 + lane];
-      else smp = ((const uint32_t*)sb)[g * 64 + lane];
-      const uint32_t z = zigzag<W>(smp);
-      uint64_t mine = 0;
-      for (int b = 0; b < w; ++b) {  // bit-plane b of the block, kept by lane b
-        const uint64_t plane = __ballot((z >> b) & 1u);
-        mine = lane == b ? plane : mine;
-      }
-      if (lane < w) payload[off + lane] = mine;
+    uint32_t X[NP][2];
+    gather_bytes<W>(w, X);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) tr8x8(X[p][0], X[p][1]);  // byte b of X[p]: s-plane 8p + b
+    // zigzag on planes: z-plane 0 = sign plane (s-plane W-1), z-plane b = s-plane b-1 ^ sign
+    const uint32_t sg = perm(X[NP - 1][1], X[NP - 1][1], 0x07070707u);
+    uint32_t Z[NP][2];
+#pragma unroll
+    for (int i = 2 * NP - 1; i >= 0; --i) {
+      const uint32_t cur = X[i >> 1][i & 1];
+      const uint32_t prev = i ? X[(i - 1) >> 1][(i - 1) & 1] : 0u;
+      Z[i >> 1][i & 1] = __builtin_amdgcn_alignbit(cur, prev, 24) ^ sg;
     }
-    wave_lds_sync();
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      xtr8(Z[p][0], Z[p][1], j);
+      if (8 * p + j < wd) payload[off + 8 * p + j] = ((uint64_t)Z[p][1] << 32) | Z[p][0];
+    }
   }
 }
 
-// wave step: SPL blocks; every block's planes are loaded up front (lane b holds plane b), each
-// sample is rebuilt from readlane-broadcast planes into LDS, then stored as 16 B per lane
+// wave step: 8 blocks; the inverse of pack_kernel (both transposes are their own inverses)
 template <int W>
 __global__ void __launch_bounds__(256) unpack_kernel(const uint64_t* __restrict__ payload, int64_t n,
                                                    const uint8_t* __restrict__ widths,
                                                    const uint32_t* __restrict__ local,
                                                    const uint64_t* __restrict__ cbase, int64_t nb, void* __restrict__ out) {
-  constexpr int SPL = Lay<W>::SPL;
-  __shared__ u32x4v stage[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t nstep = (nb + SPL - 1) / SPL;
+  constexpr int NP = Sw<W>::NP;
+  const int lane = threadIdx.x & 63, j = lane & 7;
+  const int64_t nstep = (nb + 7) / 8;
   for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
        st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int64_t blk0 = st * SPL;
-    uint32_t wj = 0;
-    uint64_t oj = 0;
-    if (lane < SPL && blk0 + lane < nb) {
-      wj = widths[blk0 + lane];
-      oj = cbase[(blk0 + lane) / kChunk] + local[blk0 + lane];
+    const int64_t blk = st * 8 + (lane >> 3);
+    int wd = 0;
+    uint64_t off = 0;
+    if (blk < nb) {
+      wd = widths[blk];
+      off = cbase[blk / kChunk] + local[blk];
     }
-    uint64_t mine[SPL];
+    uint32_t Z[NP][2];
 #pragma unroll
-    for (int g = 0; g < SPL; ++g) {
-      const int w = (int)__builtin_amdgcn_readlane(wj, g);  // 0 past the last block
-      mine[g] = lane < w ? payload[readlane64(oj, g) + lane] : 0ull;
+    for (int p = 0; p < NP; ++p) {
+      const uint64_t v = 8 * p + j < wd ? payload[off + 8 * p + j] : 0ull;
+      Z[p][0] = (uint32_t)v;
+      Z[p][1] = (uint32_t)(v >> 32);
     }
-    unsigned char* sb = (unsigned char*)stage[wv];
 #pragma unroll
-    for (int g = 0; g < SPL; ++g) {
-      const int w = (int)__builtin_amdgcn_readlane(wj, g);
-      uint32_t z = 0;
-      for (int b = 0; b < w; ++b) z |= (uint32_t)(readlane64(mine[g], b) >> lane & 1u) << b;
-      const uint32_t v = unzigzag<W>(z);
-      if constexpr (W == 8) sb[g * 64 + lane] = (uint8_t)v;
-      else if constexpr (W == 16) ((uint16_t*)sb)[g * 64 + lane] = (uint16_t)v;
-      else ((uint32_t*)sb)[g * 64 + lane] = v;
+    for (int p = 0; p < NP; ++p) xtr8(Z[p][0], Z[p][1], j);  // byte b of Z[p]: z-plane 8p + b
+    const uint32_t sg = perm(Z[0][0], Z[0][0], 0x00000000u);
+    uint32_t X[NP][2];
+#pragma unroll
+    for (int i = 0; i < 2 * NP; ++i) {
+      const uint32_t cur = Z[i >> 1][i & 1];
+      const uint32_t next = i + 1 < 2 * NP ? Z[(i + 1) >> 1][(i + 1) & 1] : 0u;
+      X[i >> 1][i & 1] = __builtin_amdgcn_alignbit(next, cur, 8) ^ sg;
     }
-    wave_lds_sync();
-    const u32x4v v = stage[wv][lane];
-    const int64_t i0 = blk0 * kBlock + (int64_t)lane * SPL;
-    if (i0 + SPL <= n) {
-      *(u32x4a1*)((char*)out + i0 * (W / 8)) = v;
-    } else {
-      for (int e = 0; e < SPL; ++e) {
-        if (i0 + e >= n) break;
-        store_sample<W>(out, i0 + e, elem<W>(v, e));
-      }
-    }
-    wave_lds_sync();
+#pragma unroll
+    for (int p = 0; p < NP; ++p) tr8x8(X[p][0], X[p][1]);
+    uint32_t w[Sw<W>::NW];
+    scatter_bytes<W>(X, w);
+    store8s<W>(out, n, st * 512 + (int64_t)lane * 8, w);
   }
 }
 
@@ -276,7 +377,7 @@ __global__ void __launch_bounds__(128) header_kernel(uint8_t* __restrict__ dst, 
 
 template <int W>
 static inline unsigned waves_grid(int64_t nb) {
-  int64_t g = ceil_div(ceil_div(nb, (int64_t)Lay<W>::SPL), 4);  // a wave step = SPL blocks, 4 waves per workgroup
+  int64_t g = ceil_div(ceil_div(nb, (int64_t)8), 4);  // a wave step = 8 blocks, 4 waves per workgroup
   return (unsigned)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
 }
 

@@ -44,7 +44,7 @@ def test_spec_round_trip(dtype, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32, np.float32])
-@pytest.mark.parametrize('shape', [(1,), (64,), (65,), (3, 17, 19), (2, 4096 * 64 + 5)])
+@pytest.mark.parametrize('shape', [(1,), (64,), (65,), (513,), (3, 17, 19), (2, 4096 * 64 + 5), (3 * 1024 * 64 + 8 * 64 + 17,)])
 def test_pack_matches_spec(kom, dtype, shape):
     rng = np.random.default_rng(sum(shape))
     if dtype == np.float32:

@@ -203,6 +203,33 @@ def main():
         emit('packing:pack', f'bit-plane pack of a 32 MiB coded map (whole volume ratio {ratio}x)',
              m.numel() * 2 + blob.numel(), tp)
         emit('packing:unpack', 'bit-plane unpack of the same map', m.numel() * 2 + blob.numel(), tu)
+        # the device chains alone (C-ABI on preallocated buffers, no header and no host sync):
+        # widths + scan + pack, and scan + unpack
+        from kompressor_amd import _device as kdev
+        from kompressor_amd._lib import lib as klib
+        n, code = m.numel(), kdev.dtype_code(m)
+        nb = int(klib.kmp_pack_blocks(n))
+        ws = torch.empty(int(klib.kmp_pack_workspace_bytes(n)), dtype=torch.uint8, device='cuda')
+        wd = torch.empty(max(nb, 1), dtype=torch.uint8, device='cuda')
+        pay = torch.empty(nb * 64 * 2, dtype=torch.uint8, device='cuda')
+        out = torch.empty_like(m)
+
+        def pack_dev():
+            klib.kmp_pack_plan(code, m.data_ptr(), n, wd.data_ptr(), ws.data_ptr(), kdev.stream())
+            klib.kmp_pack(code, m.data_ptr(), n, wd.data_ptr(), ws.data_ptr(), pay.data_ptr(), kdev.stream())
+
+        def unpack_dev():
+            klib.kmp_unpack_plan(wd.data_ptr(), n, ws.data_ptr(), kdev.stream())
+            klib.kmp_unpack(code, pay.data_ptr(), n, wd.data_ptr(), ws.data_ptr(), out.data_ptr(), kdev.stream())
+
+        pack_dev()
+        unpack_dev()
+        torch.cuda.synchronize()
+        assert torch.equal(out, m)
+        emit('packing:pack_device', 'widths + scan + pack kernels of the same map (no header, no host sync)',
+             m.numel() * 2 + blob.numel(), gpu_time(pack_dev, args.reps))
+        emit('packing:unpack_device', 'scan + unpack kernels of the same map', m.numel() * 2 + blob.numel(),
+             gpu_time(unpack_dev, args.reps))
         del tiles, lo, maps
 
     # geometry primitives (volume/utils.py) on the C3 tile batch
