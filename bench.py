@@ -126,11 +126,13 @@ def e2e_leg(kom, host, predictor, ndim, chunk, reps=3):
             'note': 'raw bytes / (t_enc + t_dec), each direction timed from pinned host input to pinned host output'}
 
 
-def kernel_name(ndim, padding):
+def kernel_name(ndim, padding, direction='encode', u8=False):
     # the one-pass kernel the C layer dispatches for this workload (kmp_codec_*.hip)
     if ndim == 3:
         return 'wave3d_plane_kernel' if padding == 0 else 'fast3d_kernel'
-    return 'wave2d_kernel' if padding == 0 else 'fast2d_kernel'
+    if padding == 0:
+        return 'wave2d_u8_kernel' if (u8 and direction == 'decode') else 'wave2d_kernel'
+    return 'wave2dp_kernel'
 
 
 def load_traffic(workload, padding, kernel):
@@ -333,7 +335,7 @@ def main():
                        'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
             'launch': 'hipGraph replay (one graph per direction)' if args.graph else 'eager (one ctypes launch per direction)',
-            'roofline': {'bound': 'hbm', 'kernel': f'{kernel_name(ndim, args.padding)} {dominant}',
+            'roofline': {'bound': 'hbm', 'kernel': f'{kernel_name(ndim, args.padding, dominant, spec["dtype"] == np.uint8)} {dominant}',
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),
                          'traffic': traffic, 'algorithmic_bytes_per_launch': algo},

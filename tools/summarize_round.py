@@ -29,7 +29,7 @@ def pmc(kind):
         shutil.copy(f[0], os.path.join(dst, f'{tag}_pmc_{ctr}{kind}.csv'))
         for r in csv.DictReader(open(f[0])):
             if 'kmp' in r['Kernel_Name']:
-                direction = 'decode' if ', true' in r['Kernel_Name'] else 'encode'
+                direction = 'decode' if (', true' in r['Kernel_Name'] or '<true>' in r['Kernel_Name']) else 'encode'
                 vals[(direction, r['Counter_Name'])].append(float(r['Counter_Value']))
     out = {}
     for d in ('encode', 'decode'):
