@@ -14,6 +14,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 BUILD = os.path.join(HERE, 'build')
 LIB = os.path.join(HERE, 'libkompressor_hip.so')
+# the debug variant: device bounds checks (KMP_DCHECK / KMP_SPAN in kmp_common.h) compiled in;
+# loaded instead of the release library when KMP_DEBUG=1 (kompressor_amd/_lib.py)
+BUILD_DEBUG = os.path.join(HERE, 'build_debug')
+LIB_DEBUG = os.path.join(HERE, 'libkompressor_hip_debug.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wall', '-Wno-unused-function',
@@ -30,37 +34,40 @@ def _headers_mtime():
     return max(os.path.getmtime(h) for h in hs)
 
 
-def _compile(src, hdr_mtime, verbose):
-    obj = os.path.join(BUILD, os.path.basename(src).replace('.hip', '.o'))
+def _compile(src, hdr_mtime, verbose, debug=False):
+    obj = os.path.join(BUILD_DEBUG if debug else BUILD, os.path.basename(src).replace('.hip', '.o'))
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
         return obj
-    cmd = [HIPCC, *FLAGS, '-c', src, '-o', obj]
+    cmd = [HIPCC, *FLAGS, *(['-DKMP_DEBUG'] if debug else []), '-c', src, '-o', obj]
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     return obj
 
 
-def build(verbose=True, jobs=None):
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose=True, jobs=None, debug=False):
+    """Compile and link the release library (``debug=False``) or the bounds-checked debug variant."""
+    bdir, lib = (BUILD_DEBUG, LIB_DEBUG) if debug else (BUILD, LIB)
+    os.makedirs(bdir, exist_ok=True)
     hdr = _headers_mtime()
     srcs = sources()
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
-    stamp = os.path.join(BUILD, 'objects.txt')  # relink when the set of sources changes too
+        objs = list(ex.map(lambda s: _compile(s, hdr, verbose, debug), srcs))
+    stamp = os.path.join(bdir, 'objects.txt')  # relink when the set of sources changes too
     listing = '\n'.join(sorted(objs))
     same_set = os.path.exists(stamp) and open(stamp).read() == listing
-    if not (same_set and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs)):
-        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB + '.tmp']
+    if not (same_set and os.path.exists(lib) and os.path.getmtime(lib) >= max(os.path.getmtime(o) for o in objs)):
+        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', lib + '.tmp']
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        os.replace(LIB + '.tmp', LIB)
+        os.replace(lib + '.tmp', lib)
         with open(stamp, 'w') as f:
             f.write(listing)
-    _build_capi_example(verbose)
-    return LIB
+    if not debug:
+        _build_capi_example(verbose)
+    return lib
 
 
 def _build_capi_example(verbose):
@@ -81,4 +88,4 @@ def _build_capi_example(verbose):
 
 
 if __name__ == '__main__':
-    print(build(verbose='-q' not in sys.argv))
+    print(build(verbose='-q' not in sys.argv, debug=os.environ.get('KMP_DEBUG', '0') != '0' or '--debug' in sys.argv))

@@ -17,7 +17,9 @@ import numpy as np
 import torch  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('KOMPRESSOR_HIP_LIB', os.path.join(HERE, 'libkompressor_hip.so'))
+# KMP_DEBUG=1 loads the variant with device bounds checks (kompressor_amd/_build.py --debug)
+_DEFAULT_LIB = 'libkompressor_hip_debug.so' if os.environ.get('KMP_DEBUG', '0') != '0' else 'libkompressor_hip.so'
+LIB_PATH = os.environ.get('KOMPRESSOR_HIP_LIB', os.path.join(HERE, _DEFAULT_LIB))
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f'kompressor_amd: {LIB_PATH} is missing -- build it with '

@@ -414,24 +414,20 @@ def encoded_shapes(shape, nsp):
     return lo, maps, dims
 
 
-_HOST_PTRS = {}
-
-
 def _ptr(t):
     """Device address of ``t``: its data pointer for a device tensor; for a pinned host tensor the
     device mapping of the page-locked buffer (zero-copy: the kernel reads / writes host memory
-    over the host link directly, ``kmp_host_device_pointer``)."""
+    over the host link directly, ``kmp_host_device_pointer``).  The mapping is looked up on every
+    call (about a microsecond): a cache keyed by host address would hand out a stale mapping once
+    a freed pinned buffer's address is reused."""
     if t.is_cuda:
         return t.data_ptr()
     if not t.is_pinned():
         raise TypeError('fused kernels take device tensors or pinned host tensors')
     base = t.untyped_storage().data_ptr()
-    dbase = _HOST_PTRS.get(base)
-    if dbase is None:
-        out = ctypes.c_void_p()
-        check(lib.kmp_host_device_pointer(ctypes.c_void_p(base), ctypes.byref(out)), 'host_device_pointer')
-        dbase = _HOST_PTRS[base] = out.value
-    return dbase + (t.data_ptr() - base)
+    out = ctypes.c_void_p()
+    check(lib.kmp_host_device_pointer(ctypes.c_void_p(base), ctypes.byref(out)), 'host_device_pointer')
+    return out.value + (t.data_ptr() - base)
 
 
 def _ptrs(tensors):
@@ -675,18 +671,29 @@ def fused_chunk_regions(chunk_list, E, nsp):
 _REGION_CACHE = {}
 
 
+def _covers(regions, E):
+    """True when the union of the boxes ``regions`` covers the frame ``[0, E)``.  Checked on the
+    grid the boxes' own edges cut the frame into (a few cells per window per axis), not on a dense
+    per-element mask -- a 2048^3 volume's lowres frame would be a 1 GB mask."""
+    cuts = [sorted({0, int(e)} | {min(max(int(v), 0), int(e)) for r in regions for v in r[a]})
+            for a, e in enumerate(E)]
+    grid = np.zeros(tuple(max(len(c) - 1, 0) for c in cuts), dtype=bool)
+    for r in regions:
+        grid[tuple(slice(int(np.searchsorted(c, min(max(a, 0), e))), int(np.searchsorted(c, min(max(b, 0), e))))
+                   for (a, b), c, e in zip(r, cuts, E))] = True
+    return bool(grid.all())
+
+
 def _chunk_regions(boxes, E):
-    regions, full = [], np.zeros(tuple(E), dtype=bool)
+    regions = []
     done = np.zeros(E[0], dtype=bool)  # leading-axis planes written by a full-slab launch
     k = 0
     while k < len(boxes):
         lead = boxes[k][0]
         j = k
-        cross = np.zeros(tuple(E[1:]), dtype=bool)
         while j < len(boxes) and boxes[j][0] == lead:
-            cross[tuple(slice(a, b) for a, b in boxes[j][1:])] = True
             j += 1
-        if cross.all():
+        if _covers([b[1:] for b in boxes[k:j]], E[1:]):
             # overlapping windows (yield_chunks steps by chunk - 3) rewrite planes an earlier slab
             # already wrote with identical values: launch only the planes not yet written
             a = lead[0]
@@ -703,9 +710,7 @@ def _chunk_regions(boxes, E):
         else:
             regions.extend(boxes[k:j])
         k = j
-    for r in regions:
-        full[tuple(slice(a, b) for a, b in r)] = True
-    return regions, bool(full.all())
+    return regions, _covers(regions, E)
 
 
 def d_process_chunks(predictions_fn, code_fn, lowres, reference_maps, chunk_list, padding, nsp):
@@ -795,13 +800,24 @@ def decode_chunks(predictions_fn, decode_fn, lowres, encoded, chunk, padding, pr
 # Public wrappers for the primitives (numpy or torch in, same kind out)
 # =============================================================================================
 
+def _fresh(out, src):
+    """``out``, or a copy of it when it shares memory with the caller's ``src`` (a zero-width pad or
+    trim returns its input on the device path): the reference is purely functional -- every
+    output is a new array (SURVEY.md §8b "Ownership") -- so a torch caller must never get its own
+    tensor back and see later writes to one through the other."""
+    if isinstance(src, torch.Tensor) and src.is_cuda and out.numel() and src.numel() and \
+            out.untyped_storage().data_ptr() == src.untyped_storage().data_ptr():
+        return out.clone()
+    return out
+
+
 def wrap1(fn):
     def inner(x, *args):
         t, kind = dev.to_device(x)
         out = fn(t, *args)
         if isinstance(out, tuple):
-            return tuple(dev.from_device(o, kind) for o in out)
-        return dev.from_device(out, kind)
+            return tuple(dev.from_device(_fresh(o, x), kind) for o in out)
+        return dev.from_device(_fresh(out, x), kind)
     return inner
 
 
@@ -811,13 +827,17 @@ def highres_from_lowres_and_maps(lowres, maps, nsp):
 
 
 def pad_maps(maps, dims, nsp):
+    maps = list(maps)
     kinds = [dev.to_device(m) for m in maps]
-    return tuple(dev.from_device(o, k) for o, (_, k) in zip(d_pad_maps([t for t, _ in kinds], dims, nsp), kinds))
+    outs = d_pad_maps([t for t, _ in kinds], dims, nsp)
+    return tuple(dev.from_device(_fresh(o, m), k) for o, m, (_, k) in zip(outs, maps, kinds))
 
 
 def trim_maps(maps, dims, nsp):
+    maps = list(maps)
     kinds = [dev.to_device(m) for m in maps]
-    return tuple(dev.from_device(o, k) for o, (_, k) in zip(d_trim_maps([t for t, _ in kinds], dims, nsp), kinds))
+    outs = d_trim_maps([t for t, _ in kinds], dims, nsp)
+    return tuple(dev.from_device(_fresh(o, m), k) for o, m, (_, k) in zip(outs, maps, kinds))
 
 
 def to_numpy(x):

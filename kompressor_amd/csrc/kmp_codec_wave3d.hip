@@ -43,6 +43,7 @@ struct W3 {
   int32_t txn, rows, nwv, nyg;
   int32_t xcd_per;  // > 0: XCD-contiguous block order (blocks per XCD), 0: identity
   int32_t nt_nodes; // plane kernel: 1 = non-temporal node-row loads, 0 = default policy (L2-shared halo)
+  int64_t nB;       // tiles in the batch (debug-build bounds checks only)
 };
 
 // rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row;
@@ -142,6 +143,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       N[t].halo = N[t].dn = uint4{};
       const T* p = hin + 2 * lsrc(q, a.Lz, a.Ez) * hplane;
+      KMP_SPAN((const T*)a.hi_in, p + ho_own, 2 * VX, a.nB * a.D * hplane);
+      KMP_SPAN((const T*)a.hi_in, p + (first ? ho_up : ho_dn), 2 * VX, a.nB * a.D * hplane);
       // own node row: unconditional (row Yc is clamped in bounds; a dead lane's value is unused)
       if (a.nt_nodes) N[t].own = ld16(p + ho_own);
       else N[t].own = ld16c(p + ho_own);
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       // re-read row 2Y / plane 2q; the maps they would feed are not stored there)
       const int r1 = 2 * Yc + 1 < a.H ? a.W : 0, p1 = 2 * q + 1 < a.D ? hplane : 0;
       const T* p = hin + 2 * q * hplane;
+      KMP_SPAN((const T*)a.hi_in, p + p1 + ho_own + r1, 2 * VX, a.nB * a.D * hplane);
       O[u].e1 = ld16(p + ho_own + r1);
       O[u].o0 = ld16(p + p1 + ho_own);
       O[u].o1 = ld16(p + p1 + ho_own + r1);
@@ -178,6 +182,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       N[t].halo = N[t].dn = uint2{};
       const T* p = lin + lsrc(q, a.Lz, a.Ez) * lplane;
+      KMP_SPAN((const T*)a.lo_in, p + lo_own, VX, a.nB * a.Ez * lplane);
+      KMP_SPAN((const T*)a.lo_in, p + (first ? lo_up : lo_dn), VX, a.nB * a.Ez * lplane);
       if (a.nt_nodes) N[t].own = ld8(p + lo_own);
       else N[t].own = ld8c(p + lo_own);
       if constexpr (ONE) {
@@ -198,8 +204,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         int par[3];
         map_parity(3, k, par);
         const int ez = par[0] ? a.Lcz : a.Ez;
-        if (ez > 0 && mplane[k] > 0) O[u].mv[k] = ld8(mbase[k] + (q < ez ? q : ez - 1) * mplane[k]);  // uniform
-        else O[u].mv[k] = uint2{};
+        if (ez > 0 && mplane[k] > 0) {  // uniform
+          KMP_SPAN((const T*)a.maps.p[k], mbase[k] + (q < ez ? q : ez - 1) * mplane[k], VX, a.nB * ez * mplane[k]);
+          O[u].mv[k] = ld8(mbase[k] + (q < ez ? q : ez - 1) * mplane[k]);
+        } else {
+          O[u].mv[k] = uint2{};
+        }
       }
     };
     load_node(0);
@@ -310,12 +320,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         res[5][i] = (el16<T>(Oc.e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
         res[6][i] = (el16<T>(e0, 2 * i + 1) - pred[6][i]) & MASK;     // X  (0,0,1)
       }
+      KMP_SPAN((const T*)a.lo_out, (const T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, VX,
+               a.nB * a.Ez * lplane);
       st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         int par[3];
         map_parity(3, k, par);
-        if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+        if (mok_y[k] && (!par[0] || vz1)) {
+          KMP_SPAN((const T*)a.maps.p[k], mbase[k] + c * mplane[k], VX,
+                   a.nB * (par[0] ? a.Lcz : a.Ez) * mplane[k]);
+          st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+        }
       }
     } else {
       const OR& Oc = O[u];
@@ -327,6 +343,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
         for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(Oc.mv[k], i)) & MASK;
       T* h0 = hout + 2 * c * hplane + ho_own;
+      KMP_SPAN((T*)a.hi_out, h0 + (vz1 ? hplane : 0) + (vy1 ? a.W : 0), 2 * VX, a.nB * a.D * hplane);
       st16(h0, pack16<T, VX>(own, dv[6]));
       if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[5], dv[2]));
       if (vz1) {
@@ -385,6 +402,7 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   const int64_t nblk = B * nslab * nyg;
   a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
   a.nt_nodes = w3_env("KMP_W3_NT_NODES", 0);
+  a.nB = B;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);

@@ -20,6 +20,32 @@ void set_error(const std::string& msg);
 int fail(int status, const std::string& msg);
 int check_launch(const char* what);
 
+// Device-side bounds checks of the debug build (``KMP_DEBUG=1 python kompressor_amd/_build.py``
+// -> libkompressor_hip_debug.so, loaded when KMP_DEBUG=1): a failed check prints the kernel's
+// file:line and the offending access, then traps so the fault is localised to one access instead
+// of surfacing as a memory fault somewhere later.  Compiled out of the release library.
+#ifdef KMP_DEBUG
+#define KMP_DCHECK(cond, ...)                                                               \
+  do {                                                                                     \
+    if (!(cond)) {                                                                         \
+      printf("KMP_DCHECK failed %s:%d: %s -- ", __FILE__, __LINE__, #cond);               \
+      printf(__VA_ARGS__);                                                                 \
+      printf("\n");                                                                        \
+      __builtin_trap();                                                                    \
+    }                                                                                      \
+  } while (0)
+#else
+#define KMP_DCHECK(cond, ...) do { } while (0)
+#endif
+
+// [p, p + cnt) inside the array [base, base + n) (elements); a no-op in the release build
+template <typename T>
+__device__ __forceinline__ void dcheck_span(const T* base, const T* p, int64_t cnt, int64_t n, int line) {
+  KMP_DCHECK(p >= base && p + cnt <= base + n, "line %d: access [%lld, %lld) of an array of %lld elements", line,
+             (long long)(p - base), (long long)(p - base + cnt), (long long)n);
+}
+#define KMP_SPAN(base, p, cnt, n) ::kmp::dcheck_span((base), (p), (int64_t)(cnt), (int64_t)(n), __LINE__)
+
 #define KMP_REQUIRE(cond, msg)                                         \
   do {                                                                 \
     if (!(cond)) return ::kmp::fail(KMP_ERR_ARG, std::string(__func__) + ": " + (msg)); \

@@ -335,8 +335,8 @@ __global__ void __launch_bounds__(256) unpack_kernel(const uint64_t* __restrict_
     int wd = 0;
     uint64_t off = 0;
     if (blk < nb) {
-      wd = widths[blk];
-      off = cbase[blk / kChunk] + local[blk];
+      wd = min((int)widths[blk], W);  // a width past the sample size never steers a read (the host
+      off = cbase[blk / kChunk] + local[blk];  // also rejects such blobs before launching)
     }
     uint32_t Z[NP][2];
 #pragma unroll

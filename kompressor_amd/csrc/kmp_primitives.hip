@@ -946,7 +946,11 @@ using namespace kmp;
 
 extern "C" {
 
-const char* kmp_version(void) { return "kompressor_hip 0.1.0 (gfx950)"; }
+#ifdef KMP_DEBUG
+const char* kmp_version(void) { return "kompressor_hip 0.2.0 (gfx950, debug: device bounds checks)"; }
+#else
+const char* kmp_version(void) { return "kompressor_hip 0.2.0 (gfx950)"; }
+#endif
 const char* kmp_last_error(void) { return g_last_error.c_str(); }
 const char* kmp_last_launch(void) { return g_last_launch; }
 

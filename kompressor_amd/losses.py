@@ -35,18 +35,37 @@ def mean_charbonnier_error(pred, gt, eps):
     return _out(torch.mean(torch.sqrt(torch.square(d) + np.float32(eps) ** 2)), gt)
 
 
-def _diff_mean(x, axis):
-    """Mean of the signed forward difference along ``axis`` in the input dtype (unsigned wraps)."""
-    if isinstance(x, torch.Tensor):
-        a = x.detach().cpu().numpy()
-    else:
-        a = np.asarray(x)
-    return np.float32(np.mean(np.diff(a, axis=axis).astype(np.float32), dtype=np.float32))
+_WRAP_BITS = {torch.uint8: 8, torch.uint16: 16, torch.int8: 8, torch.int16: 16, torch.int32: 32}
+_SIGNED = {torch.int8, torch.int16, torch.int32}
+
+
+def _as_tensor(x):
+    return x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+
+
+def _diff_mean(t, axis):
+    """Mean of the signed forward difference along ``axis`` computed in the input dtype, as
+    ``input[1:] - input[:-1]`` does under jnp (integer types wrap modulo 2^bits), then averaged in
+    float32 -- on the device ``t`` lives on (no host round trip)."""
+    n = t.shape[axis]
+    hi, lo = t.narrow(axis, 1, n - 1), t.narrow(axis, 0, n - 1)
+    bits = _WRAP_BITS.get(t.dtype)
+    if bits is None:  # floating point: the difference in the input dtype
+        d = (hi - lo).to(torch.float32)
+    else:             # integers: exact difference in int64, wrapped to the dtype's range
+        d = hi.to(torch.int32).to(torch.int64) - lo.to(torch.int32).to(torch.int64) if t.dtype == torch.uint16 \
+            else hi.to(torch.int64) - lo.to(torch.int64)
+        d = torch.remainder(d, 1 << bits)
+        if t.dtype in _SIGNED:
+            d = torch.where(d >= (1 << (bits - 1)), d - (1 << bits), d)
+        d = d.to(torch.float32)
+    return torch.mean(d)
 
 
 def total_variation(inputs, axes):
-    terms = [_diff_mean(inputs, a) for a in axes]
-    value = np.float32(sum(terms, np.float32(0)) / np.float32(len(axes)))
-    if isinstance(inputs, torch.Tensor):
-        return torch.tensor(value, dtype=torch.float32)
-    return value
+    """Mean over ``axes`` of the mean signed forward difference (volume/losses.py:30-35,
+    image/losses.py:30-34): ``(mean(dz) + mean(dy) + mean(dx)) / 3`` in 3D, ``/ 2`` in 2D."""
+    t = _as_tensor(inputs)
+    terms = [_diff_mean(t, a) for a in axes]
+    value = (sum(terms[1:], terms[0]) / np.float32(len(axes))).to(torch.float32)
+    return _out(value, inputs)

@@ -66,29 +66,56 @@ def _pack_device(t):
     return out[:poff + 8 * words]
 
 
+_SAMPLE_BITS = {1: 8, 2: 16, 4: 32}
+
+
 def _parse_array(b):
-    """(dtype code, shape, n, nb, widths offset, payload offset, total bytes) of an array blob:
-    one device-to-host read of the header."""
+    """(dtype code, shape, n, nb, widths offset, payload offset, total bytes, words) of an array
+    blob: one device-to-host read of the header.  Every header field is checked against the others
+    before anything is launched, so a corrupt or hostile blob raises ValueError instead of steering
+    a kernel outside its buffers."""
     hb = bytes(b[:min(b.numel(), _HEAD.size + 8 * 8)].cpu().numpy())
     if len(hb) < _HEAD.size:
         raise ValueError('truncated array blob')
     magic, version, code, ndim, _, n, nb, words = _HEAD.unpack(hb[:_HEAD.size])
     if magic != ARRAY_MAGIC or version != VERSION or ndim > 8:
         raise ValueError(f'not a kompressor_amd array blob (magic {magic!r}, version {version})')
+    if code not in dev.CODE_TO_TORCH:
+        raise ValueError(f'array blob has an unknown dtype code {code}')
+    if len(hb) < _HEAD.size + 8 * ndim:
+        raise ValueError('truncated array blob')
     shape = struct.unpack(f'<{ndim}q', hb[_HEAD.size:_HEAD.size + 8 * ndim])
+    if any(s < 0 for s in shape) or n != dev.prod(shape):
+        raise ValueError(f'array blob sample count {n} does not match its shape {shape}')
+    if nb != int(lib.kmp_pack_blocks(n)):
+        raise ValueError(f'array blob has {nb} blocks, {n} samples need {int(lib.kmp_pack_blocks(n))}')
+    bits = _SAMPLE_BITS[torch.empty(0, dtype=dev.CODE_TO_TORCH[code]).element_size()]
+    if words < 0 or words > nb * bits:
+        raise ValueError(f'array blob payload of {words} words exceeds {nb} blocks of {bits} planes')
     woff = _HEAD.size + 8 * ndim
     poff = woff + _pad8(nb)
-    return code, shape, n, nb, woff, poff, poff + 8 * words
+    return code, shape, n, nb, woff, poff, poff + 8 * words, words
 
 
 def _unpack_device(b):
-    code, shape, n, nb, woff, poff, total = _parse_array(b)
+    code, shape, n, nb, woff, poff, total, words = _parse_array(b)
     if b.numel() < total:
         raise ValueError(f'truncated array blob ({b.numel()} < {total} bytes)')
-    widths = b[woff:woff + max(nb, 1)]
-    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
     out = dev.empty(shape, dev.CODE_TO_TORCH[code])
+    if n == 0:
+        return out
+    widths = b[woff:woff + nb]
+    bits = _SAMPLE_BITS[out.element_size()]
+    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
     check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
+    # the widths must fit the sample type and add up to the header's payload length (the unpack
+    # kernel derives every block's payload offset from them): one synchronisation for both
+    off = int(lib.kmp_pack_total_offset(n))
+    scanned = ws[off:off + 8].view(torch.int64)
+    wmax, total_words = torch.cat([widths.max().to(torch.int64).reshape(1), scanned]).tolist()
+    if wmax > bits or total_words != words:
+        raise ValueError(f'array blob block widths are inconsistent (max {wmax} of {bits} bits, '
+                         f'{total_words} payload words, header says {words})')
     check(lib.kmp_unpack(code, b.data_ptr() + poff, n, widths.data_ptr(), ws.data_ptr(), out.data_ptr(),
                          dev.stream()), 'unpack')
     return out

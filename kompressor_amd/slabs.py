@@ -157,6 +157,16 @@ def _with_halo(x, own, need, ranges, needs, group):
     world, rank = world_and_rank(group)
     if world == 1:
         return x
+    # every rank evaluates the same global decision before any p2p call, so a slab thinner than
+    # a neighbour's halo makes ALL ranks raise together instead of one raising while its
+    # neighbour blocks forever in a send nobody receives
+    for r in range(world):
+        lo_need = ranges[r][0] - needs[r][0]
+        hi_need = needs[r][1] - ranges[r][1]
+        if (r > 0 and lo_need > ranges[r - 1][1] - ranges[r - 1][0]) or \
+                (r < world - 1 and hi_need > ranges[r + 1][1] - ranges[r + 1][0]):
+            raise AssertionError(f'slab of rank {r - 1 if lo_need > 0 and r > 0 else r + 1} is thinner than the halo '
+                                 f'rank {r} needs: use fewer ranks')
     local, sends, recvs = _exchange(x, own, need, world, rank, group, ranges)
     if rank > 0:  # rank r-1 needs my first planes above its own
         n_up = needs[rank - 1][1] - ranges[rank - 1][1]

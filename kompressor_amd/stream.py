@@ -86,6 +86,23 @@ class TileStream:
         cdt = torch.uint32 if self.dtype == torch.float32 else self.dtype
         return pinned((n, *self.lowres_shape), cdt), [pinned((n, *s), self.map_dtype) for s in self.map_shapes]
 
+    def _check_buffers(self, tiles, host_lowres, host_maps, n, what):
+        """Every host buffer against the shapes :meth:`alloc_encoded` gives for ``n`` tiles --
+        raised before any launch: on the zero-copy path the kernel reads / writes these buffers
+        directly, so a short or mis-shaped one would be overrun in pinned host memory."""
+        cdt = torch.uint32 if self.dtype == torch.float32 else self.dtype
+        want = [((n, *self.tile_shape), cdt, tiles), ((n, *self.lowres_shape), cdt, host_lowres)]
+        host_maps = list(host_maps)
+        if len(host_maps) != len(self.map_shapes):
+            raise AssertionError(f'{what}: expected {len(self.map_shapes)} maps, got {len(host_maps)}')
+        want += [((n, *s), self.map_dtype, m) for s, m in zip(self.map_shapes, host_maps)]
+        for shape, dtype, t in want:
+            if not isinstance(t, torch.Tensor) or tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous():
+                got = (tuple(t.shape), t.dtype, t.is_contiguous()) if isinstance(t, torch.Tensor) else type(t)
+                raise AssertionError(f'{what}: buffer {got} does not match the stream\'s '
+                                     f'{shape} {dtype} (contiguous)')
+        return host_maps
+
     def _chunks(self, n):
         for i, b in enumerate(range(0, n, self.chunk)):
             yield i % self.slots, b, min(n, b + self.chunk)
@@ -96,6 +113,7 @@ class TileStream:
         :meth:`alloc_encoded`).  Returns once every copy is queued; :meth:`synchronize` waits."""
         src = _as_codec_dtype(host_tiles)
         n = int(src.shape[0])
+        host_maps = self._check_buffers(src, host_lowres, host_maps, n, 'TileStream.encode')
         cur = torch.cuda.current_stream()
         for s in self._streams:
             s.wait_stream(cur)
@@ -120,6 +138,7 @@ class TileStream:
         """Decode pinned encoded tiles into the pinned ``host_out`` ``[n, *tile, C...]``."""
         dst = _as_codec_dtype(host_out)
         n = int(host_lowres.shape[0])
+        host_maps = self._check_buffers(dst, host_lowres, host_maps, n, 'TileStream.decode')
         cur = torch.cuda.current_stream()
         for s in self._streams:
             s.wait_stream(cur)

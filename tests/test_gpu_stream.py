@@ -83,3 +83,54 @@ def test_uint32_fused_codec_vs_oracle(kom, p):
     for m, r in zip(maps, ref_maps):
         assert np.array_equal(m, r)
     assert np.array_equal(kom.volume.decode(pred, kom.volume.decode_values_uint32, lo, (maps, dims), padding=p), x)
+
+
+@pytest.mark.parametrize('zero_copy', [True, False])
+def test_c5_chunk_shape_float32(kom, zero_copy):
+    """BASELINE config C5 at its real chunk geometry: a handful of 128^3 float32 chunks streamed
+    through TileStream (zero-copy and the 3-stream copy pipeline), chunk 1 bit-exact against the
+    oracle's uint32 restatement (volume/encode_decode.py:30-85 with the mod-2^32 coder), every
+    chunk round-tripping bit for bit -- NaN / +-0 / +-inf / denormals included."""
+    import oracle
+    from oracle import predictors as OP
+    n = 5
+    rng = np.random.default_rng(128)
+    x = (rng.standard_normal((n, 128, 128, 128, 1), dtype=np.float32) * 100).astype(np.float32)
+    flat = x.reshape(-1)
+    flat[:6] = [np.nan, -0.0, 0.0, np.inf, -np.inf, np.float32(1e-40)]
+    ts = kom.stream.TileStream(kom.MeanPredictor(0, 3), x.shape[1:], torch.float32, 2, 3, 3, zero_copy=zero_copy)
+    assert ts.zero_copy == zero_copy
+    src = _pinned_from(x)
+    lo, maps = ts.alloc_encoded(n)
+    ts.encode(src, lo, maps)
+    ts.synchronize()
+    bits = x[1:2].view(np.uint32)
+    ref_lo, (ref_maps, _) = oracle.volume.encode(OP.mean_predictions_fn(0, 3), oracle.volume.encode_values_uint32, bits)
+    assert np.array_equal(lo[1:2].numpy(), ref_lo)
+    for m, r in zip(maps, ref_maps):
+        assert np.array_equal(m[1:2].numpy(), r)
+    out = torch.empty_like(src).pin_memory()
+    ts.decode(lo, maps, out)
+    ts.synchronize()
+    assert np.array_equal(out.numpy().view(np.uint32), x.view(np.uint32))
+
+
+def test_stream_rejects_mismatched_host_buffers(kom):
+    """on the zero-copy path the kernel writes the caller's pinned buffers
+    directly, so buffers that do not match the stream's shapes raise before any launch."""
+    shape = (4, 16, 16, 16, 1)
+    ts = kom.stream.TileStream(kom.MeanPredictor(0, 3), shape[1:], torch.uint16, 2, 2, 3, zero_copy=True)
+    src = _pinned_from(np.zeros(shape, np.uint16))
+    lo, maps = ts.alloc_encoded(shape[0])
+    short_lo, short_maps = ts.alloc_encoded(shape[0] - 1)
+    with pytest.raises(AssertionError):
+        ts.encode(src, short_lo, maps)
+    with pytest.raises(AssertionError):
+        ts.encode(src, lo, short_maps)
+    with pytest.raises(AssertionError):
+        ts.encode(src, lo, maps[:-1])
+    out_bad = torch.empty((shape[0], 16, 16, 15, 1), dtype=torch.uint16, pin_memory=True)
+    ts.encode(src, lo, maps)
+    ts.synchronize()
+    with pytest.raises(AssertionError):
+        ts.decode(lo, maps, out_bad)

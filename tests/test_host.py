@@ -22,6 +22,27 @@ def test_library_exports_every_header_symbol():
     assert 'gfx950' in L.version()
 
 
+def test_debug_library_exports_the_same_c_abi():
+    """The KMP_DEBUG=1 variant (device bounds checks compiled in) is built beside the release
+    library and exports the identical C-ABI, so the parity suite can run against either."""
+    import subprocess
+    import sys
+    import kompressor_amd._lib as L
+    path = os.path.join(ROOT, 'kompressor_amd', 'libkompressor_hip_debug.so')
+    if not os.path.exists(path):
+        pytest.skip('debug library not built (__graft_entry__.build() builds it)')
+    # loaded in a child process: the library is chosen when kompressor_amd._lib is imported
+    code = ('import os, sys; os.environ["KMP_DEBUG"] = "1"; sys.path.insert(0, %r); '
+            'import kompressor_amd._lib as L; print(L.LIB_PATH); print(L.version()); '
+            'print([n for n in L.EXPORTED if not hasattr(L.lib, n)])' % ROOT)
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    assert lines[0].endswith('libkompressor_hip_debug.so')
+    assert 'debug' in lines[1] and 'debug' not in L.version()
+    assert lines[2] == '[]'
+
+
 def test_package_imports_and_version():
     import kompressor_amd as kom
     assert isinstance(kom.VERSION, str)  # tests/test_import_module.py:36-40

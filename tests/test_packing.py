@@ -112,3 +112,33 @@ def test_unpack_rejects_bad_blobs(kom):
         kom.packing.unpack(bad)                # not a container
     with pytest.raises(ValueError):
         kom.packing.unpack(blob[:10])          # shorter than a header
+
+
+def _poke(blob, off, fmt, value):
+    import struct
+    bad = blob.copy()
+    bad[off:off + struct.calcsize(fmt)] = np.frombuffer(struct.pack(fmt, value), np.uint8)
+    return bad
+
+
+@pytest.mark.gpu
+def test_unpack_rejects_inconsistent_headers(kom):
+    """every header field is checked against the others before a kernel runs --
+    a sample count that disagrees with the shape, a wrong block count, an unknown dtype, a block
+    width past the sample size, a payload word count that the widths do not add up to."""
+    x = (np.arange(1000) % 7).astype(np.uint16)
+    blob = kom.packing.pack(x)
+    head = 40 + 8 * x.ndim
+    cases = [
+        _poke(blob, 16, '<q', 1 << 20),   # n past prod(shape): the kernel would write past `out`
+        _poke(blob, 40, '<q', 1 << 20),   # shape past n
+        _poke(blob, 24, '<q', 3),         # nblocks too small for n
+        _poke(blob, 6, '<H', 99),         # unknown dtype code (ValueError, not KeyError)
+        _poke(blob, 32, '<q', 1),         # words smaller than the widths add up to
+        _poke(blob, head, '<B', 200),     # a block width past 16 bits
+        _poke(blob, head, '<B', 16),      # a legal width whose sum no longer matches words
+    ]
+    for bad in cases:
+        with pytest.raises(ValueError):
+            kom.packing.unpack(bad)
+    assert np.array_equal(kom.packing.unpack(blob), x)

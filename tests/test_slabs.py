@@ -56,6 +56,16 @@ def _worker(rank, world, port, cases, q):
             ok.append(torch.equal(llocal, lo[:, la:lb]))
             # reassembly of the per-rank planes
             ok.append(torch.equal(slabs.gather_planes(vol[:, h0:h1].clone(), depth), vol))
+        # a slab thinner than the halo makes EVERY rank raise (none is left blocked in
+        # a send): depth 13 -> 7 node planes, one or two per rank, against a (1 + p) = 3-plane halo
+        depth = 13
+        vol = torch.zeros((1, depth, 6, 4, 1), dtype=torch.uint16)
+        (z0, z1), (h0, h1) = slabs.slab_planes(depth, rank, world)
+        try:
+            slabs.encode_halo_exchange(vol[:, h0:h1].clone(), depth, 2)
+            ok.append(world < 3)  # with 2 ranks the slabs are thick enough
+        except AssertionError:
+            ok.append(world >= 3)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
