@@ -7,8 +7,10 @@ One step = one fused encode pass + one fused decode pass over the whole batch (v
 512^3 uint16 volume as 512 tiles of 64^3, BASELINE config C3; image: 1024 tiles of 256^2
 uint8, config C2), inputs resident in HBM.  Multi-GPU (torchrun, one rank per GPU): every rank
 codes its own 512-tile volume -- tiles are independent, so the path shards with no data-path
-collective ("scaling": "weak"); the C4 reassembly all-gather is timed separately and reported
-under "c4_reassembly", never in "value".  Rank 0 prints ONE JSON line.
+collective ("scaling": "weak"; ``value`` = bytes coded by all ranks / wall time, the whole-job
+aggregate, ``value_per_gpu`` = value / N).  Config C4 proper -- ONE volume, 512/N tiles per rank,
+then the RCCL all-gather that reassembles it -- is measured beside it under "c4" (codec and
+all-gather timed separately), never in ``value``.  Rank 0 prints ONE JSON line.
 """
 
 import argparse
@@ -49,7 +51,8 @@ def parse():
     ap.add_argument('--padding', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument("--graph", action="store_true", help="replay each direction from a hipGraph instead of eager ctypes launches")
-    ap.add_argument('--cpu-tiles', type=int, default=0, help='tiles in the CPU baseline sample (0 = all)')
+    ap.add_argument('--cpu-tiles', type=int, default=0,
+                    help='tiles in the 1-thread numpy CPU sample (0 = 64 volume tiles / 256 images)')
     ap.add_argument('--e2e-chunk', type=int, default=32, help='tiles per H2D/D2H copy in the end-to-end leg')
     ap.add_argument('--no-e2e', action='store_true', help='skip the pinned-host end-to-end leg')
     ap.add_argument('--stream-tiles', type=int, default=0, help='stream workload: chunks per GPU (0 = 512)')
@@ -65,33 +68,59 @@ def synthetic(spec, seed):
     return rng.integers(0, int(info.max) + 1, size=spec['shape'], dtype=np.int64).astype(spec['dtype'])
 
 
-def cpu_baseline(spec, host, padding, ntiles):
-    """The oracle (numpy op-for-op restatement of the reference's JAX path, 1 thread) on a
-    bounded sample of the same workload: 1 warm-up on 4 tiles, then the median of 2 timed
-    encode+decode rounds over ``ntiles`` tiles."""
-    from oracle import volume as OV, image as OI, predictors as OP
-    ns = OV if spec['ndim'] == 3 else OI
+def _median_rate(fn, nbytes, reps=5):
+    """1 warm-up, then the median of ``reps`` timed runs of ``fn`` -> (GB/s, median seconds)."""
+    fn()
+    times = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t)
+    t = float(np.median(times))
+    return nbytes / t / 1e9, t
+
+
+def cpu_baseline(spec, host, padding, ntiles_numpy=0, ntiles_torch=0):
+    """The reference path on the host cores, on a bounded sample of the same workload
+    (BASELINE.md §2): 1 warm-up + the median of 5 encode+decode rounds of
+      * the multithreaded torch-CPU restatement (oracle/torch_cpu.py: the reference's op sequence
+        with its materialised features / predictions, every op a torch CPU kernel on
+        torch.get_num_threads() threads) -- the headline ``value``;
+      * the 1-thread numpy op-for-op restatement (oracle/volume.py, oracle/image.py) beside it.
+    Both round trips are checked lossless."""
+    from oracle import volume as OV, image as OI, predictors as OP, torch_cpu as TC
+    ndim = spec['ndim']
+    ns = OV if ndim == 3 else OI
     enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if spec['dtype'] == np.uint16 else \
                (ns.encode_values_uint8, ns.decode_values_uint8)
-    pf = OP.mean_predictions_fn(padding, spec['ndim'])
-    sample = host[:ntiles]
+    pf = OP.mean_predictions_fn(padding, ndim)
+    n = host.shape[0]
+    nn = min(n, ntiles_numpy or (64 if ndim == 3 else 256))
+    nt = min(n, ntiles_torch or n)
+    out = {}
 
-    def rnd(x):
-        lo, (maps, dims) = ns.encode(pf, enc, x, padding=padding)
-        return ns.decode(pf, dec, lo, (maps, dims), padding=padding)
+    def numpy_round():
+        lo, (maps, dims) = ns.encode(pf, enc, host[:nn], padding=padding)
+        out['np'] = ns.decode(pf, dec, lo, (maps, dims), padding=padding)
 
-    rnd(host[:4])
-    times = []
-    for _ in range(2):
-        t = time.perf_counter()
-        out = rnd(sample)
-        times.append(time.perf_counter() - t)
-    assert np.array_equal(out, sample), 'oracle round trip failed'
-    t = float(np.median(times))
-    return {'value': round(sample.nbytes / t / 1e9, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{ntiles} of {host.shape[0]} tiles, numpy restatement of the reference path '
-                      f'(oracle/, materialised features/predictions, 1 thread; host has '
-                      f'{len(os.sched_getaffinity(0))} cores), median of 2 after warm-up, {t:.2f} s/round'}
+    def torch_round():
+        lo, e = TC.encode(host[:nt], padding, ndim)
+        out['torch'] = TC.decode(lo, e, padding, ndim)
+
+    threads = torch.get_num_threads()
+    r_t, t_t = _median_rate(torch_round, host[:nt].nbytes)
+    assert np.array_equal(out['torch'], host[:nt]), 'torch-CPU round trip failed'
+    r_n, t_n = _median_rate(numpy_round, host[:nn].nbytes)
+    assert np.array_equal(out['np'], host[:nn]), 'oracle round trip failed'
+    unit = 'tiles' if ndim == 3 else 'images'
+    return {'value': round(r_t, 4), 'unit': 'GB/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{nt} of {n} {unit}: torch-CPU restatement of the reference path (oracle/torch_cpu.py, '
+                      f'materialised features / predictions like the JAX path) on {threads} threads '
+                      f'(torch.get_num_threads(); the host exposes {len(os.sched_getaffinity(0))} cores), '
+                      f'1 warm-up + median of 5 encode+decode rounds, {t_t:.3f} s/round',
+            'single_thread_numpy': {'value': round(r_n, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
+                                    'sample': f'{nn} of {n} {unit}: numpy op-for-op restatement (oracle/), '
+                                              f'1 thread, 1 warm-up + median of 5, {t_n:.3f} s/round'}}
 
 
 def e2e_leg(kom, host, predictor, ndim, chunk, reps=3):
@@ -214,10 +243,12 @@ def direction_times(run_enc, run_dec, n, dist):
     return t_enc, t_dec
 
 
-def c4_reassembly(kom, hi, predictor, ndim, dist, world, ws):
-    """BASELINE config C4: ONE volume's tiles sharded over the ranks (kompressor_amd.shard), each
-    rank codes its shard, then one RCCL all-gather reassembles the decoded tiles everywhere.
-    Timed as a whole, separately from ``value``."""
+def c4_strong(kom, hi, predictor, ndim, dist, world, ws, reps=10):
+    """BASELINE config C4 as SURVEY.md §8d defines it: ONE 512^3 volume (rank 0's, broadcast),
+    its 512 tiles sharded 512/N per rank (kompressor_amd.shard), each rank codes its shard, then
+    one RCCL all-gather reassembles the decoded volume on every rank.  Codec and all-gather are
+    timed separately (barrier + synchronize around each, max over ranks, median of ``reps``);
+    reported beside ``value``, never in it."""
     from kompressor_amd import _nd
     hi = hi.clone()
     dist.broadcast(hi.view(torch.uint8), 0)   # every rank holds the same volume (rank 0's)
@@ -226,23 +257,37 @@ def c4_reassembly(kom, hi, predictor, ndim, dist, world, ws):
     coder = _nd.NATURAL_CODER[hi.dtype]
     lo_s, maps_s, dims_s = _nd._alloc_encoded(shard, coder, ndim)
     rec_s = torch.empty_like(shard)
-    times = []
-    for i in range(6):
-        dist.barrier()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
+
+    def codec():
         _nd.fused_encode_into(shard, predictor, coder, lo_s, maps_s, ndim, workspace=ws)
         _nd.fused_decode_into(lo_s, maps_s, dims_s, predictor, coder, rec_s, ndim, workspace=ws)
-        full = kom.shard.all_gather_tiles(rec_s, n)
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t)
+
+    def timed(fn):
+        ts = []
+        for i in range(reps + 2):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ts.append(time.perf_counter() - t)
+        tt = torch.tensor([float(np.median(ts))], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return tt.item(), r
+
+    t_codec, _ = timed(codec)
+    t_ag, full = timed(lambda: kom.shard.all_gather_tiles(rec_s, n))
     assert torch.equal(full, hi), 'C4 reassembled volume differs from the input'
-    tt = torch.tensor([float(np.median(times[1:]))], dtype=torch.float64, device='cuda')
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     raw = hi.numel() * hi.element_size()
-    return {'tiles_per_rank': int(shard.shape[0]), 'ms_codec_plus_allgather': round(tt.item() * 1e3, 4),
-            'volume_GBps': round(raw / tt.item() / 1e9, 2),
-            'collective': ('all_gather_into_tensor (RCCL) of per-rank decoded tile slabs'
+    recv = raw - shard.numel() * shard.element_size()
+    return {'tiles_per_rank': int(shard.shape[0]), 'ms_codec': round(t_codec * 1e3, 4),
+            'ms_allgather': round(t_ag * 1e3, 4),
+            'volume_GBps_codec': round(raw / t_codec / 1e9, 2),
+            'volume_GBps_with_reassembly': round(raw / (t_codec + t_ag) / 1e9, 2),
+            'allgather_GBps_received_per_rank': round(recv / t_ag / 1e9, 2),
+            'scaling': 'strong (one 512^3 volume split over the ranks)',
+            'collective': ('all_gather_into_tensor (RCCL over xGMI) of per-rank decoded tile slabs'
                            if dist.get_backend() == 'nccl' else f'all_gather ({dist.get_backend()}) of per-rank decoded tile slabs')}
 
 
@@ -314,7 +359,7 @@ def main():
     achieved = algo / t_dom / 1e9
     traffic = load_traffic(args.workload, args.padding, dominant)
 
-    c4 = c4_reassembly(kom, hi, predictor, ndim, dist, world, ws) if dist else None
+    c4 = c4_strong(kom, hi, predictor, ndim, dist, world, ws) if dist else None
 
     e2e = None
     if world == 1 and not args.no_e2e:
@@ -322,17 +367,20 @@ def main():
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(spec, host, args.padding, args.cpu_tiles or spec['shape'][0])
+        base = cpu_baseline(spec, host, args.padding, args.cpu_tiles)
 
     if rank == 0:
         line = {
             'metric': spec['metric'], 'value': round(value, 3), 'unit': 'GB/s', 'n_gpus': world,
+            'value_per_gpu': round(value / world, 3),
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 5),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'u16' if spec['dtype'] == np.uint16 else 'u8', 'data': 'synthetic (default_rng uniform)',
             'config': {'workload': spec['name'], 'global_batch': spec['shape'][0] * world,
                        'tile': list(spec['shape'][1:-1]), 'predictor': f'MeanPredictor(padding={args.padding})',
-                       'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU'},
+                       'parallelism': f'tiles sharded, dp{world}' if world > 1 else 'single GPU',
+                       'value_is': 'whole-job aggregate: raw highres bytes coded by all ranks / wall time '
+                                   '(weak scaling: every rank codes its own full batch; value_per_gpu = value / n_gpus)'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
             'launch': 'hipGraph replay (one graph per direction)' if args.graph else 'eager (one ctypes launch per direction)',
             'roofline': {'bound': 'hbm', 'kernel': f'{kernel_name(ndim, args.padding, dominant, spec["dtype"] == np.uint8)} {dominant}',
@@ -344,7 +392,7 @@ def main():
         if e2e:
             line['e2e_host'] = e2e
         if c4:
-            line['c4_reassembly'] = c4
+            line['c4'] = c4
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -428,20 +476,36 @@ def main_stream(args):
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import volume as OV, predictors as OP
-        sample = src[:2].numpy().view(np.uint32)
+        # the same two restatements as the C3 / C2 lines, on the uint32 bit patterns
+        from oracle import volume as OV, predictors as OP, torch_cpu as TC
+        host32 = src.numpy().view(np.uint32)
         pf = OP.mean_predictions_fn(args.padding, 3)
-        t = time.perf_counter()
-        lo_o, enc_o = OV.encode(pf, OV.encode_values_uint32, sample, padding=args.padding)
-        back = OV.decode(pf, OV.decode_values_uint32, lo_o, enc_o, padding=args.padding)
-        t = time.perf_counter() - t
-        assert np.array_equal(back, sample)
-        base = {'value': round(sample.nbytes / t / 1e9, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
-                'sample': f'2 of {n} chunks of 128^3, numpy restatement (oracle/, uint32 bit-cast, 1 thread), '
-                          f'{t:.2f} s'}
+        nn, nt = min(n, 2), min(n, 8)
+        out = {}
+
+        def numpy_round():
+            lo_o, enc_o = OV.encode(pf, OV.encode_values_uint32, host32[:nn], padding=args.padding)
+            out['np'] = OV.decode(pf, OV.decode_values_uint32, lo_o, enc_o, padding=args.padding)
+
+        def torch_round():
+            lo_t, enc_t = TC.encode(host32[:nt], args.padding, 3)
+            out['torch'] = TC.decode(lo_t, enc_t, args.padding, 3)
+
+        r_t, t_t = _median_rate(torch_round, host32[:nt].nbytes)
+        assert np.array_equal(out['torch'], host32[:nt])
+        r_n, t_n = _median_rate(numpy_round, host32[:nn].nbytes)
+        assert np.array_equal(out['np'], host32[:nn])
+        threads = torch.get_num_threads()
+        base = {'value': round(r_t, 4), 'unit': 'GB/s', 'cores': threads, 'kind': 'port',
+                'sample': f'{nt} of {n} chunks of 128^3: torch-CPU restatement (oracle/torch_cpu.py, uint32 '
+                          f'bit-cast) on {threads} threads, 1 warm-up + median of 5, {t_t:.3f} s/round',
+                'single_thread_numpy': {'value': round(r_n, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
+                                        'sample': f'{nn} of {n} chunks, numpy restatement (oracle/), 1 thread, '
+                                                  f'1 warm-up + median of 5, {t_n:.3f} s/round'}}
     if rank == 0:
         line = {
             'metric': spec['metric'], 'value': round(raw * world * args.steps / elapsed / 1e9, 3), 'unit': 'GB/s',
+            'value_per_gpu': round(raw * args.steps / elapsed / 1e9, 3),
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'u32 (float32 bit-cast)', 'data': 'synthetic (standard normal float32)',

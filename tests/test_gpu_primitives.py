@@ -131,3 +131,23 @@ def test_mean_predictor_callable(kom, ndim, padding):
     want = oracle.predictors.mean_predictions_fn(padding, ndim)(window)
     for a, b in zip(got, want):
         _eq(a, b)
+
+
+@pytest.mark.gpu
+def test_zero_width_pads_and_trims_return_fresh_tensors(kom):
+    """SURVEY.md §8b "Ownership": every output is a new array, as under JAX -- a zero-width pad or
+    trim of a CUDA tensor must not hand the caller's own tensor back (writing the output would
+    silently change the input)."""
+    import torch
+    for ns, shape in ((kom.volume, (2, 5, 6, 7, 1)), (kom.image, (2, 6, 7, 1))):
+        n = len(shape) - 2
+        x = torch.arange(int(np.prod(shape)), dtype=torch.int32).reshape(shape).to(torch.uint16).cuda()
+        keep = x.clone()
+        outs = [ns.pad_neighborhood(x, 0), ns.utils.trim(x, (0,) * n), ns.utils.pad_lowres(x, (0,) * n),
+                ns.utils.pad_map(x, (0,) * n)]
+        outs += list(ns.utils.pad_maps([x, x], (0,) * n)) + list(ns.utils.trim_maps([x, x], (0,) * n))
+        for o in outs:
+            assert torch.equal(o, keep)
+            assert o.untyped_storage().data_ptr() != x.untyped_storage().data_ptr()
+            o.view(torch.int16).fill_(7)
+            assert torch.equal(x, keep), 'writing an output changed the input'

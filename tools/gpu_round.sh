@@ -12,7 +12,7 @@ step() { local name=$1; shift; timeout -k 10 "$@" > $O/$name.log 2>&1; local rc=
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread && \
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" && \
 step bench 400 python bench.py && \
-step bench_image 300 python bench.py --workload image --no-cpu-baseline && \
+step bench_image 300 python bench.py --workload image && \
 step bench_stream 400 python bench.py --workload stream && \
 step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu-baseline --no-e2e && \
 step prof_image 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_image -o run -- python3 bench.py --workload image --no-cpu-baseline --no-e2e && \
