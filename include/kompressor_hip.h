@@ -252,6 +252,24 @@ int kmp_unpack_plan(const uint8_t* widths, int64_t n, void* workspace, kmp_strea
 int kmp_unpack(int32_t dtype, const uint64_t* payload, int64_t n, const uint8_t* widths, const void* workspace,
                void* out, kmp_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Block-adaptive Rice entropy coding of coded maps (kmp_rice.hip; SURVEY.md §8f f-3 -- no      */
+/* reference counterpart, volume/encode_decode.py:56 returns the residuals unreduced; format    */
+/* spec: oracle/rice.py).  n samples of ``dtype`` (8/16/32-bit), zigzag-mapped, blocks of 64:     */
+/* params[b] = Rice k + 1 (0 = all-zero block), bw[b] = the block's 32-bit payload words.         */
+/* ``workspace`` holds kmp_pack_workspace_bytes(n) bytes; the payload word count lands at         */
+/* kmp_pack_total_offset(n) (uint64) like kmp_pack_plan's.                                        */
+/* ---------------------------------------------------------------------------------------- */
+/* params / bw of x, and the block offsets + total payload words into the workspace */
+int kmp_rice_plan(int32_t dtype, const void* x, int64_t n, uint8_t* params, uint8_t* bw, void* workspace,
+                  kmp_stream_t stream);
+/* the payload (4-byte aligned) of x, after kmp_rice_plan on the same workspace */
+int kmp_rice_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* params, const void* workspace,
+                  uint32_t* payload, kmp_stream_t stream);
+/* the samples, after kmp_unpack_plan(bw, n, workspace) (the block offsets from the stored bw) */
+int kmp_rice_unpack(int32_t dtype, const uint32_t* payload, int64_t n, const uint8_t* params, const uint8_t* bw,
+                    const void* workspace, void* out, kmp_stream_t stream);
+
 /* Categorical rank coder utils.py:58-111: ``logits`` float32 [n, L]; x/out of ``dtype`` [n]. */
 int kmp_categorical(int32_t direction, const float* logits, int64_t n, int64_t L, int32_t dtype, const void* x,
                     void* out, kmp_stream_t stream);

@@ -1,0 +1,122 @@
+"""Compressed files (kompressor_amd.container): compress -> file -> decompress is
+lossless for every sample type the codec takes (uint8 images, uint16 volumes, int32, float32 bit
+patterns), with the predictor recorded in the file; the Rice payload is smaller than the
+bit-plane one on structured data; corrupt or foreign files raise ValueError.  The reference has no
+file format (volume/encode_decode.py:56), so the byte layout is the build's own ("parity
+unpinned"; the payload bytes are pinned to oracle/rice.py by tests/test_packing.py)."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT  # noqa: F401
+
+
+def structured(shape, dtype, noise, seed=0):
+    """A smooth field (a few Gaussian blobs + a slow wave) plus Gaussian noise of std ``noise`` --
+    the kind of data a predictive codec is for (random data is incompressible)."""
+    rng = np.random.default_rng(seed)
+    grids = np.meshgrid(*[np.arange(s, dtype=np.float32) for s in shape[1:-1]], indexing='ij')
+    field = np.zeros(shape[1:-1], np.float32)
+    for _ in range(4):
+        c = [rng.uniform(0, s) for s in shape[1:-1]]
+        w = rng.uniform(4, 16)
+        field += rng.uniform(0.3, 1.0) * np.exp(-sum((g - ci) ** 2 for g, ci in zip(grids, c)) / (2 * w * w))
+    field += 0.2 * np.sin(grids[-1] / 7.0) * np.cos(grids[0] / 11.0)
+    hi = 200 if dtype == np.uint8 else 30000
+    out = np.empty(shape, np.float32)
+    for b in range(shape[0]):
+        out[b, ..., 0] = 20 + hi * (field - field.min()) / (np.ptp(field) + 1e-6) + rng.normal(0, noise, shape[1:-1])
+    if dtype == np.float32:
+        return out
+    info = np.iinfo(dtype)
+    return np.clip(np.round(out), info.min, info.max).astype(dtype)
+
+
+CASES = [
+    ('mean0_u16', 3, (4, 64, 64, 64, 1), np.uint16, 2.0),
+    ('mean1_u16_odd', 3, (2, 33, 40, 31, 1), np.uint16, 2.0),
+    ('mean0_u8_img', 2, (16, 256, 256, 1), np.uint8, 1.0),
+    ('mean0_f32', 3, (2, 64, 64, 64, 1), np.float32, 0.5),
+    ('linear0_u16', 3, (2, 32, 32, 32, 1), np.uint16, 2.0),
+]
+
+
+def _predictor(kom, name, ndim):
+    p = 1 if 'mean1' in name else 0
+    if name.startswith('linear'):
+        n, k = 8, 19
+        w = (np.full((n, k), 1.0 / n) + np.random.default_rng(3).standard_normal((n, k)) * 0.01).astype(np.float32)
+        return kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim)
+    return kom.MeanPredictor(p, ndim)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('method', ['rice', 'planes'])
+@pytest.mark.parametrize('name,ndim,shape,dtype,noise', CASES)
+def test_compress_decompress_lossless(kom, tmp_path, name, ndim, shape, dtype, noise, method):
+    x = structured(shape, dtype, noise)
+    pred = _predictor(kom, name, ndim)
+    path = str(tmp_path / f'{name}.kmp')
+    info = kom.container.compress(path, x, pred, method=method)
+    assert info['bytes'] < info['raw_bytes'], info      # structured data shrinks
+    back = kom.container.decompress(path)
+    assert back.dtype == x.dtype and back.shape == x.shape
+    assert np.array_equal(back.view(np.uint8), x.view(np.uint8))
+    # the decoded maps equal the in-memory encode() result exactly (the predictor came from the file)
+    lo, (maps, dims), meta = kom.container.load(path)
+    assert meta['predictor']['kind'] == ('linear' if name.startswith('linear') else 'mean')
+    h = torch.from_numpy(x).cuda()
+    if dtype == np.float32:
+        h = h.view(torch.uint32)
+    ns = kom.volume if ndim == 3 else kom.image
+    enc = {torch.uint16: ns.encode_values_uint16, torch.uint8: ns.encode_values_uint8,
+           torch.uint32: kom.volume.encode_values_uint32}[h.dtype]
+    rlo, (rmaps, rdims) = ns.encode(pred, enc, h, padding=pred.padding)
+    assert tuple(dims) == tuple(rdims) and torch.equal(lo, rlo)
+    assert all(torch.equal(a, b) for a, b in zip(maps, rmaps))
+
+
+@pytest.mark.gpu
+def test_rice_smaller_than_planes_on_structured_volumes(kom, tmp_path):
+    """The entropy coder's point: on structured volumes (smooth field + noise of std 1, 4, 16) the
+    Rice container is clearly smaller than the bit-plane container, and both beat raw storage."""
+    for noise in (1.0, 4.0, 16.0):
+        x = structured((4, 64, 64, 64, 1), np.uint16, noise, seed=int(noise))
+        pred = kom.MeanPredictor(0, 3)
+        r = kom.container.compress(str(tmp_path / 'r.kmp'), x, pred, method='rice')
+        p = kom.container.compress(str(tmp_path / 'p.kmp'), x, pred, method='planes')
+        assert r['bytes'] < 0.93 * p['bytes'], (noise, r, p)
+        assert np.array_equal(kom.container.decompress(str(tmp_path / 'r.kmp')), x)
+
+
+@pytest.mark.gpu
+def test_external_predictor_must_be_passed(kom, tmp_path):
+    inner = kom.MeanPredictor(0, 3)
+
+    def my_predictor(lowres):  # an opaque predictions_fn (a trained network would sit here)
+        return inner(lowres)
+
+    x = structured((2, 32, 32, 32, 1), np.uint16, 2.0)
+    lo, enc = kom.volume.encode(my_predictor, kom.volume.encode_values_uint16, x)
+    path = str(tmp_path / 'ext.kmp')
+    kom.container.save(path, lo, enc, predictor=my_predictor)
+    with pytest.raises(AssertionError, match='external'):
+        kom.container.decompress(path)
+    assert np.array_equal(kom.container.decompress(path, predictor=inner), x)
+
+
+@pytest.mark.gpu
+def test_corrupt_files_raise(kom, tmp_path):
+    x = structured((2, 32, 32, 32, 1), np.uint16, 2.0)
+    path = tmp_path / 'c.kmp'
+    kom.container.compress(str(path), x, kom.MeanPredictor(0, 3))
+    raw = bytearray(path.read_bytes())
+    flipped = bytearray(raw)
+    flipped[-9] ^= 0x40                      # one payload bit: the CRC catches it
+    (tmp_path / 'flip.kmp').write_bytes(bytes(flipped))
+    (tmp_path / 'trunc.kmp').write_bytes(bytes(raw[:-100]))
+    (tmp_path / 'foreign.kmp').write_bytes(b'GIF89a' + bytes(64))
+    for name in ('flip.kmp', 'trunc.kmp', 'foreign.kmp'):
+        with pytest.raises(ValueError):
+            kom.container.decompress(str(tmp_path / name))

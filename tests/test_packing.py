@@ -1,11 +1,13 @@
-"""Bit-plane container: the numpy specification (oracle/packing.py) on the
-CPU, and the HIP kernels (kmp_pack.hip) byte-for-byte against it on the GPU.  The reference has
-no container stage, so these pin the build's own format ("parity unpinned" by the reference)."""
+"""Container payloads: the numpy specifications (oracle/packing.py: bit-planes,
+oracle/rice.py: block-adaptive Rice) on the CPU, and the HIP kernels (kmp_pack.hip, kmp_rice.hip)
+byte-for-byte against them on the GPU.  The reference has no container stage, so these pin the
+build's own formats ("parity unpinned" by the reference)."""
 
 import numpy as np
 import pytest
 
 from oracle import packing as OPK
+from oracle import rice as ORC
 
 
 def _residuals(n, dtype, rng, spread=4):
@@ -40,7 +42,102 @@ def test_spec_round_trip(dtype, n):
     assert np.array_equal(OPK.unpack(w, payload, n, dtype), x)
 
 
+def test_rice_spec_known_answer():
+    # residuals 0, -1, 1, -2 zigzag to 0, 1, 2, 3 (+ 60 zero-padded samples): S_0 = 6, S_1 = 2,
+    # words(0) = 0 + ceil(70 / 32) = 3, words(1) = 2 + ceil(66 / 32) = 5 -> k = 0, 3 unary words:
+    # sample 0 '1', sample 1 '01', sample 2 '001', sample 3 '0001', then 60 x '1'
+    x = np.array([0, 65535, 1, 65534], np.uint16)
+    params, bw, payload = ORC.pack(x)
+    assert params.tolist() == [1] and bw.tolist() == [3]
+    bits = '1' + '01' + '001' + '0001' + '1' * 60
+    want = [sum(1 << t for t in range(32) if 32 * i + t < len(bits) and bits[32 * i + t] == '1') for i in range(3)]
+    assert payload.tolist() == want
+    assert np.array_equal(ORC.unpack(params, bw, payload, 4, np.uint16), x)
+    params, bw, payload = ORC.pack(np.zeros(130, np.uint8))  # all-zero blocks take no payload
+    assert params.tolist() == [0, 0, 0] and bw.tolist() == [0, 0, 0] and payload.size == 0
+
+
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32])
+@pytest.mark.parametrize('n', [1, 63, 64, 65, 1000])
+def test_rice_spec_round_trip(dtype, n):
+    rng = np.random.default_rng(n + 7)
+    info = np.iinfo(dtype)
+    x = rng.integers(info.min, int(info.max) + 1, size=n, dtype=np.int64).astype(dtype)
+    x[: n // 2] = _residuals(n // 2, dtype, rng, spread=40)
+    params, bw, payload = ORC.pack(x)
+    W = np.dtype(dtype).itemsize * 8
+    assert len(params) == -(-n // 64) and payload.size == int(bw.astype(np.int64).sum())
+    assert params.max() <= W and bw.max() <= 2 * W + 2
+    assert np.array_equal(ORC.unpack(params, bw, payload, n, dtype), x)
+
+
+def test_rice_beats_planes_on_laplacian_residuals():
+    """The reason for the Rice format: on Laplacian residuals (what a good predictor leaves) it is
+    within ~0.7 bit/sample of the empirical entropy and clearly below the bit-plane format."""
+    rng = np.random.default_rng(0)
+    for scale in (1, 4, 16, 100):
+        r = np.round(rng.laplace(0, scale, size=1 << 16)).astype(np.int64)
+        x = (r % 65536).astype(np.uint16)
+        params, bw, payload = ORC.pack(x)
+        w, planes = OPK.pack(x)
+        rice_bits = (payload.size * 32 + 16 * len(params)) / x.size
+        plane_bits = (planes.size * 64 + 8 * len(w)) / x.size
+        _, c = np.unique(r, return_counts=True)
+        pr = c / c.sum()
+        H = float(-(pr * np.log2(pr)).sum())
+        assert rice_bits < H + 0.75 and rice_bits < plane_bits - 0.5, (scale, H, rice_bits, plane_bits)
+
+
 # --------------------------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32, np.float32])
+@pytest.mark.parametrize('shape', [(1,), (64,), (65,), (513,), (3, 17, 19), (2, 4096 * 64 + 5), (3 * 1024 * 64 + 8 * 64 + 17,)])
+@pytest.mark.parametrize('spread', [3, 40, 3000])
+def test_rice_matches_spec(kom, dtype, shape, spread):
+    rng = np.random.default_rng(sum(shape) + spread)
+    if dtype == np.float32:
+        x = rng.standard_normal(shape).astype(np.float32)
+        bits = x.view(np.uint32)
+    else:
+        info = np.iinfo(dtype)
+        x = rng.integers(info.min, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
+        flat = x.reshape(-1)
+        flat[: flat.size * 3 // 4] = _residuals(flat.size * 3 // 4, dtype, rng, spread=spread)
+        flat[: min(flat.size, 200)] = 0  # all-zero blocks too
+        bits = x
+    blob = kom.packing.pack(x)  # the default method is 'rice'
+    assert isinstance(blob, np.ndarray) and blob.dtype == np.uint8 and bytes(blob[:4]) == b'KMPR'
+    params, bw, payload = ORC.pack(bits)
+    head = 40 + 8 * x.ndim
+    nb = len(params)
+    p8 = (nb + 7) // 8 * 8
+    assert np.array_equal(blob[head:head + nb], params)
+    assert np.array_equal(blob[head + p8:head + p8 + nb], bw)
+    poff = head + 2 * p8
+    got = blob[poff:poff + 4 * payload.size].view(np.uint32)
+    assert np.array_equal(got, payload)
+    assert blob.size == poff + (4 * payload.size + 7) // 8 * 8
+    back = kom.packing.unpack(blob)
+    assert back.dtype == x.dtype and back.shape == x.shape
+    assert np.array_equal(back.view(np.uint8), x.view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_rice_torch_round_trip_large(kom):
+    """A full C3-sized coded map (512 x 32^3 uint16, device-resident): lossless through the Rice
+    kernels, and the numpy spec agrees on a slice of blocks."""
+    import torch
+    rng = np.random.default_rng(5)
+    r = np.round(rng.laplace(0, 6, size=(512, 32, 32, 32, 1))).astype(np.int64)
+    x = torch.from_numpy((r % 65536).astype(np.uint16)).cuda()
+    blob = kom.packing.pack(x)
+    assert blob.is_cuda
+    back = kom.packing.unpack(blob)
+    assert torch.equal(back, x)
+    assert blob.numel() < 0.45 * x.numel() * 2
+
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.int32, np.uint32, np.float32])
@@ -56,7 +153,7 @@ def test_pack_matches_spec(kom, dtype, shape):
         flat = x.reshape(-1)
         flat[: flat.size // 2] = _residuals(flat.size // 2, dtype, rng, spread=9)
         bits = x
-    blob = kom.packing.pack(x)
+    blob = kom.packing.pack(x, 'planes')
     assert isinstance(blob, np.ndarray) and blob.dtype == np.uint8
     w, payload = OPK.pack(bits)
     head = 40 + 8 * x.ndim
@@ -91,19 +188,21 @@ def test_pack_encoded_round_trip_and_ratio(kom):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('method', ['rice', 'planes'])
 @pytest.mark.parametrize('shape', [(0,), (3, 0, 5)])
-def test_pack_empty(kom, shape):
+def test_pack_empty(kom, shape, method):
     x = np.zeros(shape, np.uint16)
-    blob = kom.packing.pack(x)
+    blob = kom.packing.pack(x, method)
     assert blob.size == 40 + 8 * x.ndim  # header + shape, no widths, no payload
     back = kom.packing.unpack(blob)
     assert back.shape == x.shape and back.dtype == x.dtype
 
 
 @pytest.mark.gpu
-def test_unpack_rejects_bad_blobs(kom):
+@pytest.mark.parametrize('method', ['rice', 'planes'])
+def test_unpack_rejects_bad_blobs(kom, method):
     x = np.arange(1000, dtype=np.uint16)
-    blob = kom.packing.pack(x)
+    blob = kom.packing.pack(x, method)
     with pytest.raises(ValueError):
         kom.packing.unpack(blob[:-8])          # truncated payload
     bad = blob.copy()
@@ -122,12 +221,13 @@ def _poke(blob, off, fmt, value):
 
 
 @pytest.mark.gpu
-def test_unpack_rejects_inconsistent_headers(kom):
+@pytest.mark.parametrize('method', ['rice', 'planes'])
+def test_unpack_rejects_inconsistent_headers(kom, method):
     """every header field is checked against the others before a kernel runs --
     a sample count that disagrees with the shape, a wrong block count, an unknown dtype, a block
     width past the sample size, a payload word count that the widths do not add up to."""
     x = (np.arange(1000) % 7).astype(np.uint16)
-    blob = kom.packing.pack(x)
+    blob = kom.packing.pack(x, method)
     head = 40 + 8 * x.ndim
     cases = [
         _poke(blob, 16, '<q', 1 << 20),   # n past prod(shape): the kernel would write past `out`
@@ -135,9 +235,12 @@ def test_unpack_rejects_inconsistent_headers(kom):
         _poke(blob, 24, '<q', 3),         # nblocks too small for n
         _poke(blob, 6, '<H', 99),         # unknown dtype code (ValueError, not KeyError)
         _poke(blob, 32, '<q', 1),         # words smaller than the widths add up to
-        _poke(blob, head, '<B', 200),     # a block width past 16 bits
-        _poke(blob, head, '<B', 16),      # a legal width whose sum no longer matches words
-    ]
+        _poke(blob, head, '<B', 200),     # a block width / Rice k past 16 bits
+        _poke(blob, head, '<B', 16),      # planes: a legal width whose sum no longer matches words;
+    ]                                     # rice: k = 15 with too few payload words for its planes
+    if method == 'rice':
+        cases.append(_poke(blob, head + 16, '<B', 0))     # a coded block claiming no payload
+        cases.append(_poke(blob, head + 16, '<B', 90))    # more words than a 16-bit block can take
     for bad in cases:
         with pytest.raises(ValueError):
             kom.packing.unpack(bad)
