@@ -3,11 +3,13 @@
 The reference has no file format -- ``encode`` returns ``(lowres, (maps, dims))`` in memory
 (volume/encode_decode.py:56) -- so this is the build's own container: one file holds the
 entropy-coded ``encode`` result (``packing.pack_encoded``: block-adaptive Rice by default) plus
-everything needed to decode it without outside knowledge -- the spatial rank, the predictor
+everything needed to decode it without outside knowledge -- the pyramid levels (``compress``
+applies the reference's single-level ``encode`` recursively to the lowres, so only the coarsest
+lowres is stored raw), the spatial rank, the predictor
 (kind, padding, and a LinearPredictor's weights), the coder, the even-size ``dims``, the original
 sample dtype (float32 volumes travel bit-cast to uint32) and a CRC-32 of the payload.
 
-    info = compress(path, highres, predictor)     # encode on the GPU + Rice + one file write
+    info = compress(path, highres, predictor)     # pyramid encode on the GPU + Rice + one write
     highres = decompress(path)                    # read + unpack + decode on the GPU
     save(path, lowres, encoded, predictor=...)    # an encode() result you already have
     lowres, encoded, meta = load(path)
@@ -112,13 +114,23 @@ def load(path, device=True):
     return lowres, (maps, dims), meta
 
 
-def compress(path, highres, predictor, padding=None, method='rice'):
+def _auto_levels(shape, ndim, max_levels=4):
+    """Pyramid levels while every spatial extent stays >= 3 (its lowres >= 2, volume/utils.py:295-303)."""
+    sp, levels = list(shape[1:1 + ndim]), 0
+    while levels < max_levels and all(s >= 3 for s in sp):
+        sp = [(s + (s + 1) % 2 + 1) // 2 - (s + 1) % 2 for s in sp]  # the trimmed lowres extent
+        levels += 1
+    return max(levels, 1)
+
+
+def compress(path, highres, predictor, levels='auto', method='rice'):
     """Encode ``highres`` with a built-in ``predictor`` (:class:`MeanPredictor` /
     :class:`LinearPredictor`) and the lossless coder of its dtype (uint8 / uint16 modular, int32
-    raw, float32 bit-cast to uint32 modulo 2^32), entropy-code and write ``path``.  Returns
-    ``{'bytes', 'raw_bytes', 'ratio', 'bits_per_sample'}``."""
-    ndim = predictor.ndim
-    padding = predictor.padding if padding is None else padding
+    raw, float32 bit-cast to uint32 modulo 2^32) as a ``levels``-deep pyramid -- each level is the
+    reference's single-level ``encode`` (volume/encode_decode.py:30-56) applied to the previous
+    level's lowres, so only the coarsest lowres is stored raw -- entropy-code every array and write
+    ``path``.  Returns ``{'bytes', 'raw_bytes', 'ratio', 'bits_per_sample', 'levels'}``."""
+    ndim, padding = predictor.ndim, predictor.padding
     h, _ = dev.to_device(highres)
     sample = _NP_NAME[h.dtype]
     if h.dtype == torch.float32:
@@ -126,35 +138,58 @@ def compress(path, highres, predictor, padding=None, method='rice'):
     coder = _nd.NATURAL_CODER.get(h.dtype)
     if coder is None:
         raise TypeError(f'no lossless coder for {h.dtype}')
-    lowres, maps, dims = _nd._alloc_encoded(h, coder, ndim)
-    _nd.validate_padding(padding)
-    if padding != predictor.padding:
-        raise AssertionError('padding must match the predictor')
-    _nd.fused_encode_into(h, predictor, coder, lowres, maps, ndim)
-    nbytes = save(path, lowres, (maps, dims), predictor, padding, ndim, method, sample_dtype=sample)
+    levels = _auto_levels(h.shape, ndim) if levels == 'auto' else int(levels)
+    _nd._require(levels >= 1, 'levels must be >= 1')
+    x, arrays, meta_levels = h, [], []
+    for _ in range(levels):
+        sp = _nd._sp(x.shape, ndim)
+        _nd.validate_highres_shape((x.shape[0], *[s + (s + 1) % 2 for s in sp], *x.shape[1 + ndim:]), ndim)
+        lowres, maps, dims = _nd._alloc_encoded(x, coder, ndim)
+        _nd.fused_encode_into(x, predictor, coder, lowres, maps, ndim)
+        arrays.extend(maps)
+        meta_levels.append({'highres_shape': list(x.shape), 'dims': [int(d) for d in dims]})
+        x = lowres
+    meta = {'format': 'kompressor_amd', 'ndim': ndim, 'padding': padding, 'method': method,
+            'sample_dtype': sample, 'levels': meta_levels, 'lowres_shape': list(x.shape),
+            'predictor': _predictor_meta(predictor, padding, ndim)}
+    # one bundle: the coarsest lowres, then every level's maps finest first (no bundle dims: the
+    # per-level dims live in the metadata)
+    nbytes = _write(path, meta, packing.pack_encoded(x, (arrays, ()), method))
     raw = h.numel() * h.element_size()
-    return {'bytes': nbytes, 'raw_bytes': raw, 'ratio': raw / nbytes, 'bits_per_sample': 8.0 * nbytes / h.numel()}
+    return {'bytes': nbytes, 'raw_bytes': raw, 'ratio': raw / nbytes, 'bits_per_sample': 8.0 * nbytes / h.numel(),
+            'levels': levels}
 
 
 def decompress(path, predictor=None, as_numpy=True):
-    """Decode a file written by :func:`compress` (or :func:`save` with a built-in predictor) back
-    to the original array, bit for bit.  An ``external`` predictor must be passed in."""
-    lowres, (maps, dims), meta = load(path)
+    """Decode a file written by :func:`compress` (or :func:`save`) back to the original array, bit
+    for bit, coarsest level first.  A file coded with an external predictions_fn needs it passed."""
+    meta, body = _read(path)
+    lowres, (arrays, bundle_dims) = packing.unpack_encoded(torch.from_numpy(body).cuda())
     pred = predictor or predictor_from_meta(meta)
     if pred is None:
         raise AssertionError(f'{path} was coded with an external predictions_fn '
                              f'({meta["predictor"]["name"] if meta["predictor"] else "unknown"}): pass it')
     ndim, padding = meta['ndim'], meta['padding']
+    nmaps = _nd.NMAPS[ndim]
+    levels = meta.get('levels') or [{'dims': list(bundle_dims)}]  # save(): one level, dims in the bundle
+    if len(arrays) != nmaps * len(levels):
+        raise ValueError(f'{path}: {len(arrays)} coded maps for {len(levels)} levels of {nmaps}')
     coder = _nd.NATURAL_CODER[lowres.dtype]
-    if _nd.fused_plan(pred, _coder_fn(coder, ndim), padding, lowres.dtype, ndim, 1) is not None:
-        out = torch.empty((lowres.shape[0], *[2 * e - 1 + d for e, d in zip(_nd._sp(lowres.shape, ndim), dims)],
-                           *lowres.shape[1 + ndim:]), dtype=lowres.dtype, device='cuda')
-        _nd.fused_decode_into(lowres, list(maps), dims, pred, coder, out, ndim)
-    else:
-        out = _nd.decode(pred, _coder_fn(coder, ndim), lowres, (maps, dims), padding, ndim)
+    dec_fn = _coder_fn(coder, ndim)
+    x = lowres
+    for lvl in reversed(range(len(levels))):
+        maps = list(arrays[nmaps * lvl:nmaps * (lvl + 1)])
+        dims = tuple(levels[lvl]['dims'])
+        if _nd.fused_plan(pred, dec_fn, padding, x.dtype, ndim, 1) is not None:
+            out = torch.empty((x.shape[0], *[2 * e - 1 + d for e, d in zip(_nd._sp(x.shape, ndim), dims)],
+                               *x.shape[1 + ndim:]), dtype=x.dtype, device='cuda')
+            _nd.fused_decode_into(x, maps, dims, pred, coder, out, ndim)
+        else:
+            out = _nd.decode(pred, dec_fn, x, (maps, dims), padding, ndim)
+        x = out
     if meta.get('sample_dtype') == 'float32':
-        out = out.view(torch.float32)
-    return out.cpu().numpy() if as_numpy else out
+        x = x.view(torch.float32)
+    return x.cpu().numpy() if as_numpy else x
 
 
 def _coder_fn(coder, ndim):

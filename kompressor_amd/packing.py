@@ -36,6 +36,11 @@ import struct
 import torch
 
 from . import _device as dev
+import struct
+
+import torch
+
+from . import _device as dev
 from ._lib import check, lib
 
 ARRAY_MAGIC = b'KMPA'
@@ -44,23 +49,39 @@ BUNDLE_MAGIC = b'KMPB'
 VERSION = 1
 METHODS = ('rice', 'planes')
 _HEAD = struct.Struct('<4sHHIIqqq')  # magic, version, dtype, ndim, reserved, n, nblocks, words (40 bytes)
+_HEAD_MAX = _HEAD.size + 8 * 8       # header + the largest shape (ndim <= 8)
+_SAMPLE_BITS = {1: 8, 2: 16, 4: 32}
 
 
 def _pad8(n):
     return (n + 7) // 8 * 8
 
 
-def _device_bytes(b):
-    """A device uint8 tensor holding ``b`` (<= 128 bytes), written by a kernel, no host copy."""
-    out = dev.empty((len(b),), torch.uint8)
-    check(lib.kmp_pack_header(out.data_ptr(), b, len(b), 0, 0, None, 0, -1, dev.stream()), 'pack')
-    return out
+# ---------------------------------------------------------------------------------------------
+# pack: every kernel of an array is launched into a worst-case-sized blob (header and padding
+# written by kernels from arguments); the payload lengths of ALL arrays of a call are then read
+# with ONE host synchronisation (_finish)
+# ---------------------------------------------------------------------------------------------
+
+class _Pending:
+    """A launched pack: ``out`` holds the blob, whose payload length (``unit``-byte words at
+    header offset 32) is known once the stream reaches it."""
+
+    def __init__(self, out, poff, unit, ws):
+        self.out, self.poff, self.unit, self.ws = out, poff, unit, ws
+
+    def words_view(self):
+        return self.out[32:40].view(torch.int64)
+
+    def finish(self, words):
+        used = self.poff + self.unit * words
+        end = _pad8(used)
+        if end > used:
+            self.out[used:end].zero_()
+        return self.out[:end]
 
 
-def _pack_device(t):
-    """Plan (block widths + scan) and pack straight into a worst-case-sized blob, then ONE host
-    synchronisation to learn the payload length; the blob returned is a view of that buffer."""
-    t = t.contiguous()
+def _launch_planes(t):
     code = dev.dtype_code(t)
     n = t.numel()
     nb = int(lib.kmp_pack_blocks(n))
@@ -68,25 +89,16 @@ def _pack_device(t):
     head = _HEAD.pack(ARRAY_MAGIC, VERSION, code, t.dim(), 0, n, nb, 0) + struct.pack(f'<{t.dim()}q', *t.shape)
     woff = len(head)
     poff = woff + _pad8(nb)
-    cap = poff + nb * t.element_size() * 64  # every block at full width
-    out = dev.empty((cap,), torch.uint8)
-    wptr = out.data_ptr() + woff
-    check(lib.kmp_pack_plan(code, t.data_ptr(), n, wptr, ws.data_ptr(), dev.stream()), 'pack')
-    check(lib.kmp_pack(code, t.data_ptr(), n, wptr, ws.data_ptr(), out.data_ptr() + poff, dev.stream()), 'pack')
+    out = dev.empty((poff + nb * t.element_size() * 64,), torch.uint8)  # every block at full width
+    base = out.data_ptr()
+    check(lib.kmp_pack_plan(code, t.data_ptr(), n, base + woff, ws.data_ptr(), dev.stream()), 'pack')
+    check(lib.kmp_pack(code, t.data_ptr(), n, base + woff, ws.data_ptr(), base + poff, dev.stream()), 'pack')
     # header + widths padding + the scan's word count (offset 32), from kernel arguments
-    check(lib.kmp_pack_header(out.data_ptr(), head, len(head), woff + nb, poff, ws.data_ptr(), n, 32, dev.stream()),
-          'pack')
-    words = int(out[32:40].view(torch.int64).item())  # the one host synchronisation
-    return out[:poff + 8 * words]
+    check(lib.kmp_pack_header(base, head, len(head), woff + nb, poff, ws.data_ptr(), n, 32, dev.stream()), 'pack')
+    return _Pending(out, poff, 8, ws)
 
 
-_SAMPLE_BITS = {1: 8, 2: 16, 4: 32}
-
-
-def _pack_rice_device(t):
-    """Rice plan (params + bw + scan) and pack straight into a worst-case-sized blob; header and
-    padding written by kernels; ONE host synchronisation for the payload length."""
-    t = t.contiguous()
+def _launch_rice(t):
     code = dev.dtype_code(t)
     n = t.numel()
     nb = int(lib.kmp_pack_blocks(n))
@@ -96,26 +108,42 @@ def _pack_rice_device(t):
     aoff = len(head)
     boff = aoff + _pad8(nb)
     poff = boff + _pad8(nb)
-    cap = poff + _pad8(4 * nb * (2 * bits + 2))  # every block at its largest
-    out = dev.empty((cap,), torch.uint8)
+    out = dev.empty((poff + _pad8(4 * nb * (2 * bits + 2)),), torch.uint8)  # every block at its largest
     base = out.data_ptr()
     check(lib.kmp_rice_plan(code, t.data_ptr(), n, base + aoff, base + boff, ws.data_ptr(), dev.stream()), 'rice')
     check(lib.kmp_rice_pack(code, t.data_ptr(), n, base + aoff, ws.data_ptr(), base + poff, dev.stream()), 'rice')
     check(lib.kmp_pack_header(base, b'', 0, aoff + nb, boff, None, 0, -1, dev.stream()), 'rice')
     check(lib.kmp_pack_header(base, head, len(head), boff + nb, poff, ws.data_ptr(), n, 32, dev.stream()), 'rice')
-    words = int(out[32:40].view(torch.int64).item())  # the one host synchronisation
-    end = poff + _pad8(4 * words)
-    if end > poff + 4 * words:  # zero the payload's tail padding
-        check(lib.kmp_pack_header(base, b'', 0, poff + 4 * words, end, None, 0, -1, dev.stream()), 'rice')
-    return out[:end]
+    return _Pending(out, poff, 4, ws)
 
 
-def _parse_array(b):
-    """(dtype code, shape, n, nb, widths offset, payload offset, total bytes, words) of an array
-    blob: one device-to-host read of the header.  Every header field is checked against the others
-    before anything is launched, so a corrupt or hostile blob raises ValueError instead of steering
-    a kernel outside its buffers."""
-    hb = bytes(b[:min(b.numel(), _HEAD.size + 8 * 8)].cpu().numpy())
+def _launch(t, method):
+    t = t.contiguous()
+    if method == 'rice':
+        return _launch_rice(t)
+    if method == 'planes':
+        return _launch_planes(t)
+    raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
+
+
+def _finish(pending):
+    """The blobs of launched packs: ONE host synchronisation for all their payload lengths."""
+    if not pending:
+        return []
+    words = torch.cat([p.words_view() for p in pending]).tolist()
+    return [p.finish(w) for p, w in zip(pending, words)]
+
+
+# ---------------------------------------------------------------------------------------------
+# unpack: the headers of all arrays of a call in one device-to-host copy; every header field
+# checked against the others on the host; the side information checked on the device and read
+# back with ONE synchronisation for all arrays; then the unpack kernels
+# ---------------------------------------------------------------------------------------------
+
+def _parse_head(hb, avail):
+    """Header fields of an array blob from its first bytes ``hb`` (``avail`` bytes in the blob).
+    Every field is checked against the others before anything is launched, so a corrupt or
+    hostile blob raises ValueError instead of steering a kernel outside its buffers."""
     if len(hb) < _HEAD.size:
         raise ValueError('truncated array blob')
     magic, version, code, ndim, _, n, nb, words = _HEAD.unpack(hb[:_HEAD.size])
@@ -136,110 +164,135 @@ def _parse_array(b):
         raise ValueError(f'array blob payload of {words} words exceeds {nb} blocks of {per_block} words')
     woff = _HEAD.size + 8 * ndim
     if magic == ARRAY_MAGIC:
-        poff = woff + _pad8(nb)
-        return magic, code, shape, n, nb, woff, poff, poff + 8 * words, words
-    poff = woff + 2 * _pad8(nb)
-    return magic, code, shape, n, nb, woff, poff, poff + 4 * words, words
+        poff, total = woff + _pad8(nb), woff + _pad8(nb) + 8 * words
+    else:
+        poff = woff + 2 * _pad8(nb)
+        total = poff + 4 * words
+    if avail < total:
+        raise ValueError(f'truncated array blob ({avail} < {total} bytes)')
+    return dict(magic=magic, code=code, shape=shape, n=n, nb=nb, woff=woff, poff=poff, words=words, bits=bits)
 
 
-def _unpack_device(b):
-    magic, code, shape, n, nb, woff, poff, total, words = _parse_array(b)
-    if b.numel() < total:
-        raise ValueError(f'truncated array blob ({b.numel()} < {total} bytes)')
-    out = dev.empty(shape, dev.CODE_TO_TORCH[code])
-    if n == 0:
-        return out
-    if magic == RICE_MAGIC:
-        return _unpack_rice(b, code, n, nb, woff, poff, words, out)
-    widths = b[woff:woff + nb]
-    bits = _SAMPLE_BITS[out.element_size()]
-    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
-    # the widths must fit the sample type and add up to the header's payload length (the unpack
-    # kernel derives every block's payload offset from them): one synchronisation for both
+def _prepare(b, h):
+    """Output buffer + the block-offset scan for one parsed blob; returns the device tensor of
+    [bad side-information blocks, scanned payload words] to check before unpacking."""
+    h['out'] = dev.empty(h['shape'], dev.CODE_TO_TORCH[h['code']])
+    if h['n'] == 0:
+        return None
+    n, nb, woff = h['n'], h['nb'], h['woff']
+    ws = h['ws'] = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
+    if h['magic'] == ARRAY_MAGIC:
+        widths = h['widths'] = b[woff:woff + nb]
+        check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
+        # the widths must fit the sample type (the unpack kernel derives every block's payload
+        # offset from them, and their sum must be the header's payload length)
+        bad = (widths.to(torch.int32) > h['bits']).sum()
+    else:
+        params = h['params'] = b[woff:woff + nb]
+        bw = h['bw'] = b[woff + _pad8(nb):woff + _pad8(nb) + nb]
+        check(lib.kmp_unpack_plan(bw.data_ptr(), n, ws.data_ptr(), dev.stream()), 'rice unpack')
+        # side information the encoder can produce: k < W; an all-zero block has no payload; a
+        # coded block holds its 2k plane words and >= 2 unary words, at most 2W + 2 in all
+        k = params.to(torch.int32) - 1
+        bwi = bw.to(torch.int32)
+        coded = params > 0
+        bad = ((k >= h['bits']) | (coded & ((bwi < 2 * k + 2) | (bwi > 2 * h['bits'] + 2)))
+               | (~coded & (bwi != 0))).sum()
     off = int(lib.kmp_pack_total_offset(n))
-    scanned = ws[off:off + 8].view(torch.int64)
-    wmax, total_words = torch.cat([widths.max().to(torch.int64).reshape(1), scanned]).tolist()
-    if wmax > bits or total_words != words:
-        raise ValueError(f'array blob block widths are inconsistent (max {wmax} of {bits} bits, '
-                         f'{total_words} payload words, header says {words})')
-    check(lib.kmp_unpack(code, b.data_ptr() + poff, n, widths.data_ptr(), ws.data_ptr(), out.data_ptr(),
-                         dev.stream()), 'unpack')
+    return torch.cat([bad.to(torch.int64).reshape(1), ws[off:off + 8].view(torch.int64)])
+
+
+def _run_unpack(b, h):
+    if h['n'] == 0:
+        return h['out']
+    n, code, ws, out = h['n'], h['code'], h['ws'], h['out']
+    if h['magic'] == ARRAY_MAGIC:
+        check(lib.kmp_unpack(code, b.data_ptr() + h['poff'], n, h['widths'].data_ptr(), ws.data_ptr(),
+                             out.data_ptr(), dev.stream()), 'unpack')
+    else:
+        check(lib.kmp_rice_unpack(code, b.data_ptr() + h['poff'], n, h['params'].data_ptr(), h['bw'].data_ptr(),
+                                  ws.data_ptr(), out.data_ptr(), dev.stream()), 'rice unpack')
     return out
 
 
-def _unpack_rice(b, code, n, nb, aoff, poff, words, out):
-    params, bw = b[aoff:aoff + nb], b[aoff + _pad8(nb):aoff + _pad8(nb) + nb]
-    bits = _SAMPLE_BITS[out.element_size()]
-    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    check(lib.kmp_unpack_plan(bw.data_ptr(), n, ws.data_ptr(), dev.stream()), 'rice unpack')
-    # every block's side information must be one the encoder can produce (k < W; an all-zero
-    # block has no payload; a coded block holds its 2k plane words and >= 2 unary words, at most
-    # 2W + 2 in all) and the sizes must add up to the header's payload length: one synchronisation
-    off = int(lib.kmp_pack_total_offset(n))
-    k = params.to(torch.int32) - 1
-    bwi = bw.to(torch.int32)
-    coded = params > 0
-    bad = (k >= bits) | (coded & ((bwi < 2 * k + 2) | (bwi > 2 * bits + 2))) | (~coded & (bwi != 0))
-    nbad, total_words = torch.cat([bad.sum().to(torch.int64).reshape(1), ws[off:off + 8].view(torch.int64)]).tolist()
-    if nbad or total_words != words:
-        raise ValueError(f'rice blob side information is inconsistent ({nbad} bad blocks, {total_words} payload '
-                         f'words, header says {words})')
-    check(lib.kmp_rice_unpack(code, b.data_ptr() + poff, n, params.data_ptr(), bw.data_ptr(), ws.data_ptr(),
-                              out.data_ptr(), dev.stream()), 'rice unpack')
-    return out
+def _unpack_many(b, spans):
+    """The arrays stored at byte ``spans`` [(offset, length)] of the device blob ``b``."""
+    if not spans:
+        return []
+    heads = torch.cat([b[o:o + min(ln, _HEAD_MAX)] for o, ln in spans]).cpu().numpy().tobytes()
+    parsed, pos = [], 0
+    for o, ln in spans:
+        k = min(ln, _HEAD_MAX)
+        parsed.append(_parse_head(heads[pos:pos + k], ln))
+        pos += k
+    views = [b[o:o + ln] for o, ln in spans]
+    checks = [(i, _prepare(v, h)) for i, (v, h) in enumerate(zip(views, parsed))]
+    live = [(i, c) for i, c in checks if c is not None]
+    if live:
+        vals = torch.stack([c for _, c in live]).tolist()  # the one synchronisation
+        for (i, _), (nbad, total) in zip(live, vals):
+            if nbad or total != parsed[i]['words']:
+                raise ValueError(f'array blob side information is inconsistent ({nbad} bad blocks, {total} '
+                                 f'payload words, header says {parsed[i]["words"]})')
+    return [_run_unpack(v, h) for v, h in zip(views, parsed)]
 
 
-def _pack_any(t, method):
-    if method == 'rice':
-        return _pack_rice_device(t)
-    if method == 'planes':
-        return _pack_device(t)
-    raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
-
+# ---------------------------------------------------------------------------------------------
+# public API
+# ---------------------------------------------------------------------------------------------
 
 def pack(x, method='rice'):
     """Pack one array (uint8 / uint16 / int32 / uint32 / float32 samples) into a blob."""
     t, kind = dev.to_device(x)
-    return dev.from_device(_pack_any(t, method), kind)
+    return dev.from_device(_finish([_launch(t, method)])[0], kind)
 
 
 def unpack(blob):
     """Inverse of :func:`pack`: the array, bit for bit."""
     b, kind = dev.to_device(blob)
-    return dev.from_device(_unpack_device(b), kind)
+    return dev.from_device(_unpack_many(b, [(0, b.numel())])[0], kind)
 
 
 def pack_encoded(lowres, encoded, method='rice'):
-    """One blob for an ``encode`` result ``(lowres, (maps, dims))``."""
+    """One blob for an ``encode`` result ``(lowres, (maps, dims))`` (any number of maps; ``dims``
+    may be empty): every array's kernels are launched first, then ONE synchronisation."""
     maps, dims = encoded
     kind = 'torch' if isinstance(lowres, torch.Tensor) else 'numpy'
-    blobs = [_pack_any(dev.to_device(a)[0], method) for a in (lowres, *maps)]
+    blobs = _finish([_launch(dev.to_device(a)[0], method) for a in (lowres, *maps)])
     nsp = len(dims)
     head = struct.pack('<4sHHI', BUNDLE_MAGIC, VERSION, len(blobs), nsp)
     head += struct.pack(f'<{nsp}i', *[int(d) for d in dims])
     head += b'\0' * (_pad8(len(head)) - len(head))
     head += struct.pack(f'<{len(blobs)}q', *[int(bl.numel()) for bl in blobs])
-    parts = [_device_bytes(head)]
-    for bl in blobs:
-        parts.append(bl)
-        if bl.numel() % 8:
-            parts.append(_device_bytes(bytes(8 - bl.numel() % 8)))
+    parts = [torch.frombuffer(bytearray(head), dtype=torch.uint8).to('cuda', non_blocking=False)]
+    parts += blobs  # every blob is already a multiple of 8 bytes
     return dev.from_device(torch.cat(parts), kind)
 
 
 def unpack_encoded(blob):
     """Inverse of :func:`pack_encoded`: ``(lowres, (maps, dims))``."""
     b, kind = dev.to_device(blob)
-    magic, version, count, nsp = struct.unpack('<4sHHI', bytes(b[:12].cpu().numpy()))
-    if magic != BUNDLE_MAGIC or version != VERSION:
+    hb = b[:min(b.numel(), 4096)].cpu().numpy().tobytes()
+    if len(hb) < 12:
+        raise ValueError('truncated bundle')
+    magic, version, count, nsp = struct.unpack('<4sHHI', hb[:12])
+    if magic != BUNDLE_MAGIC or version != VERSION or nsp > 8:
         raise ValueError(f'not a kompressor_amd bundle (magic {magic!r}, version {version})')
-    dims = struct.unpack(f'<{nsp}i', bytes(b[12:12 + 4 * nsp].cpu().numpy()))
     off = _pad8(12 + 4 * nsp)
-    lengths = struct.unpack(f'<{count}q', bytes(b[off:off + 8 * count].cpu().numpy()))
+    if len(hb) < off + 8 * count:
+        hb = b[:off + 8 * count].cpu().numpy().tobytes()
+        if len(hb) < off + 8 * count:
+            raise ValueError('truncated bundle')
+    dims = struct.unpack(f'<{nsp}i', hb[12:12 + 4 * nsp])
+    lengths = struct.unpack(f'<{count}q', hb[off:off + 8 * count])
     off += 8 * count
-    arrays = []
+    spans = []
     for ln in lengths:
-        arrays.append(dev.from_device(_unpack_device(b[off:off + ln]), kind))
+        if ln < 0 or off + ln > b.numel():
+            raise ValueError('truncated bundle')
+        spans.append((off, ln))
         off += _pad8(ln)
+    arrays = [dev.from_device(a, kind) for a in _unpack_many(b, spans)]
+    if not arrays:
+        raise ValueError('empty bundle')
     return arrays[0], (tuple(arrays[1:]), tuple(int(d) for d in dims))

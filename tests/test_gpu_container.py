@@ -63,18 +63,24 @@ def test_compress_decompress_lossless(kom, tmp_path, name, ndim, shape, dtype, n
     back = kom.container.decompress(path)
     assert back.dtype == x.dtype and back.shape == x.shape
     assert np.array_equal(back.view(np.uint8), x.view(np.uint8))
-    # the decoded maps equal the in-memory encode() result exactly (the predictor came from the file)
-    lo, (maps, dims), meta = kom.container.load(path)
+    assert info['levels'] >= 2
+    # every stored level equals the reference's single-level encode applied to the previous
+    # level's lowres (the predictor came from the file)
+    lo, (maps, _), meta = kom.container.load(path)
     assert meta['predictor']['kind'] == ('linear' if name.startswith('linear') else 'mean')
+    assert len(meta['levels']) == info['levels'] and len(maps) == info['levels'] * (7 if ndim == 3 else 3)
     h = torch.from_numpy(x).cuda()
     if dtype == np.float32:
         h = h.view(torch.uint32)
     ns = kom.volume if ndim == 3 else kom.image
     enc = {torch.uint16: ns.encode_values_uint16, torch.uint8: ns.encode_values_uint8,
            torch.uint32: kom.volume.encode_values_uint32}[h.dtype]
-    rlo, (rmaps, rdims) = ns.encode(pred, enc, h, padding=pred.padding)
-    assert tuple(dims) == tuple(rdims) and torch.equal(lo, rlo)
-    assert all(torch.equal(a, b) for a, b in zip(maps, rmaps))
+    nm = 7 if ndim == 3 else 3
+    for lvl, ml in enumerate(meta['levels']):
+        h, (rmaps, rdims) = ns.encode(pred, enc, h, padding=pred.padding)
+        assert tuple(ml['dims']) == tuple(rdims)
+        assert all(torch.equal(a, b) for a, b in zip(maps[nm * lvl:nm * (lvl + 1)], rmaps)), lvl
+    assert torch.equal(lo, h)
 
 
 @pytest.mark.gpu
@@ -88,6 +94,21 @@ def test_rice_smaller_than_planes_on_structured_volumes(kom, tmp_path):
         p = kom.container.compress(str(tmp_path / 'p.kmp'), x, pred, method='planes')
         assert r['bytes'] < 0.93 * p['bytes'], (noise, r, p)
         assert np.array_equal(kom.container.decompress(str(tmp_path / 'r.kmp')), x)
+
+
+@pytest.mark.gpu
+def test_pyramid_levels_shrink_the_file(kom, tmp_path):
+    """Only the coarsest lowres is stored unpredicted: each extra level replaces raw lowres samples
+    (1/8 of the voxels at level 1) by small residuals, so the file shrinks with the level count."""
+    x = structured((8, 64, 64, 64, 1), np.uint16, 2.0, seed=4)
+    pred = kom.MeanPredictor(0, 3)
+    sizes = []
+    for levels in (1, 2, 4):
+        info = kom.container.compress(str(tmp_path / f'l{levels}.kmp'), x, pred, levels=levels)
+        assert np.array_equal(kom.container.decompress(str(tmp_path / f'l{levels}.kmp')), x)
+        sizes.append(info['bytes'])
+    assert sizes[0] > sizes[1] > sizes[2], sizes
+    assert sizes[2] < 0.8 * sizes[0], sizes
 
 
 @pytest.mark.gpu

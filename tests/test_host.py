@@ -196,3 +196,20 @@ def test_pyramid_validates_levels():
     with pytest.raises(AssertionError):
         kom.volume.encode_pyramid([kom.MeanPredictor(0, 3)], kom.volume.encode_values_uint16,
                                   np.zeros((1, 9, 9, 9, 1), np.uint16), 2)
+
+
+def test_container_rejects_foreign_and_truncated_files(tmp_path):
+    """kompressor_amd.container reads and checks the file header and the payload CRC on the host
+    before anything touches the GPU."""
+    import kompressor_amd as kom
+    (tmp_path / 'foreign.kmp').write_bytes(b'GIF89a' + bytes(64))
+    (tmp_path / 'short.kmp').write_bytes(b'KMP')
+    import json
+    import struct
+    meta = json.dumps({'bundle_bytes': 64, 'crc32': 0}).encode()
+    meta += b' ' * (-len(meta) % 8)
+    (tmp_path / 'trunc.kmp').write_bytes(struct.pack('<4sHHQ', b'KMPF', 1, 0, len(meta)) + meta + bytes(10))
+    (tmp_path / 'crc.kmp').write_bytes(struct.pack('<4sHHQ', b'KMPF', 1, 0, len(meta)) + meta + bytes(range(64)))
+    for name in ('foreign.kmp', 'short.kmp', 'trunc.kmp', 'crc.kmp'):
+        with pytest.raises(ValueError):
+            kom.container.decompress(str(tmp_path / name))

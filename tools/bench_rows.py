@@ -232,6 +232,73 @@ def main():
              gpu_time(unpack_dev, args.reps))
         del tiles, lo, maps
 
+    # Rice entropy coder (kmp_rice.hip) vs the bit-plane format on structured C3-shaped volumes:
+    # a smooth 512^3 field + Gaussian noise of std 1 / 4 / 16, tiled 64^3, MeanPredictor(0) maps
+    if not want or 'rice' in want:
+        from kompressor_amd import _device as kdev
+        from kompressor_amd._lib import lib as klib
+        zz, yy, xx = torch.meshgrid(*[torch.arange(512, device='cuda', dtype=torch.float32)] * 3, indexing='ij')
+        field = (torch.sin(xx / 41.0) * torch.cos(yy / 29.0) + torch.sin(zz / 53.0 + xx / 97.0)
+                 + 1.5 * torch.exp(-((xx - 200) ** 2 + (yy - 300) ** 2 + (zz - 250) ** 2) / (2 * 90.0 ** 2)))
+        field = 4000 + 9000 * (field - field.min()) / (field.max() - field.min())
+        del zz, yy, xx
+        pred = kom.MeanPredictor(0, 3)
+        gen = torch.Generator(device='cuda').manual_seed(0)
+        for noise in (1.0, 4.0, 16.0):
+            vol = (field + noise * torch.randn(field.shape, device='cuda', generator=gen)).round().clamp(0, 65535)
+            tiles = vol.to(torch.int32).to(torch.uint16).view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5) \
+                .reshape(512, 64, 64, 64, 1).contiguous()
+            del vol
+            lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, tiles)
+            raw = tiles.numel() * 2
+            b_r = kom.packing.pack_encoded(lo, (maps, dims), 'rice')
+            b_p = kom.packing.pack_encoded(lo, (maps, dims), 'planes')
+            lo2, (maps2, _) = kom.packing.unpack_encoded(b_r)
+            assert torch.equal(lo2, lo) and all(torch.equal(a, b) for a, b in zip(maps2, maps))
+            t_enc = gpu_time(lambda: kom.packing.pack_encoded(lo, (maps, dims), 'rice'), args.reps)
+            t_dec = gpu_time(lambda: kom.packing.unpack_encoded(b_r), args.reps)
+            m = maps[3]
+            n, code = m.numel(), kdev.dtype_code(m)
+            nb = int(klib.kmp_pack_blocks(n))
+            ws = torch.empty(int(klib.kmp_pack_workspace_bytes(n)), dtype=torch.uint8, device='cuda')
+            prm = torch.empty(nb, dtype=torch.uint8, device='cuda')
+            bwv = torch.empty(nb, dtype=torch.uint8, device='cuda')
+            pay = torch.empty(nb * 34 * 4, dtype=torch.uint8, device='cuda')
+            out = torch.empty_like(m)
+
+            def rice_pack_dev():
+                klib.kmp_rice_plan(code, m.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(), kdev.stream())
+                klib.kmp_rice_pack(code, m.data_ptr(), n, prm.data_ptr(), ws.data_ptr(), pay.data_ptr(), kdev.stream())
+
+            def rice_unpack_dev():
+                klib.kmp_unpack_plan(bwv.data_ptr(), n, ws.data_ptr(), kdev.stream())
+                klib.kmp_rice_unpack(code, pay.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(),
+                                     out.data_ptr(), kdev.stream())
+
+            rice_pack_dev()
+            rice_unpack_dev()
+            torch.cuda.synchronize()
+            assert torch.equal(out, m)
+            words = int(ws[int(klib.kmp_pack_total_offset(n)):int(klib.kmp_pack_total_offset(n)) + 8]
+                        .view(torch.int64).item())
+            cmap = 4 * words + 2 * nb
+            tag = f'noise{int(noise)}'
+            line = {'row': f'rice:{tag}', 'what': f'structured 512^3 u16 (smooth field + N(0, {noise}^2)), 512 x 64^3, '
+                                                 f'MeanPredictor(0)',
+                    'ratio_rice': round(raw / b_r.numel(), 3), 'ratio_planes': round(raw / b_p.numel(), 3),
+                    'bits_per_voxel_rice': round(8 * b_r.numel() / tiles.numel(), 3),
+                    'bits_per_voxel_planes': round(8 * b_p.numel() / tiles.numel(), 3),
+                    'pack_encoded_ms': round(t_enc * 1e3, 3), 'unpack_encoded_ms': round(t_dec * 1e3, 3),
+                    'pack_encoded_GBps_raw': round(raw / t_enc / 1e9, 1),
+                    'unpack_encoded_GBps_raw': round(raw / t_dec / 1e9, 1)}
+            print(json.dumps(line), flush=True)
+            emit(f'rice:{tag}:pack_device', 'rice plan + scan + pack kernels of the 32 MiB C map (no header / sync)',
+                 m.numel() * 2 * 2 + cmap, gpu_time(rice_pack_dev, args.reps))
+            emit(f'rice:{tag}:unpack_device', 'scan + rice unpack kernels of the same map', m.numel() * 2 + cmap,
+                 gpu_time(rice_unpack_dev, args.reps))
+            del tiles, lo, maps, maps2, lo2, b_r, b_p
+        del field
+
     # geometry primitives (volume/utils.py) on the C3 tile batch
     if not want or 'primitives' in want:
         hp, _ = _nd.d_pad_highres(vol, 3)                       # [512, 65^3]
