@@ -266,6 +266,11 @@ int kmp_rice_plan(int32_t dtype, const void* x, int64_t n, uint8_t* params, uint
 /* the payload (4-byte aligned) of x, after kmp_rice_plan on the same workspace */
 int kmp_rice_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* params, const void* workspace,
                   uint32_t* payload, kmp_stream_t stream);
+/* count the blocks whose stored side information no encoder produces -- format 0 (planes):   */
+/* side_a = widths; 1 (rice): side_a = params, side_b = bw -- into the uint64 at workspace +    */
+/* kmp_pack_total_offset(n) + 8, beside the payload length of the last scan (one read for both) */
+int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const uint8_t* side_b, int64_t n,
+                     void* workspace, kmp_stream_t stream);
 /* the samples, after kmp_unpack_plan(bw, n, workspace) (the block offsets from the stored bw) */
 int kmp_rice_unpack(int32_t dtype, const uint32_t* payload, int64_t n, const uint8_t* params, const uint8_t* bw,
                     const void* workspace, void* out, kmp_stream_t stream);

@@ -98,6 +98,7 @@ _PROTOS = {
     'kmp_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     'kmp_rice_plan': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     'kmp_rice_pack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
+    'kmp_unpack_check': (ctypes.c_int, [_i32, _i32, _vp, _vp, _i64, _vp, _vp]),
     'kmp_rice_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
                                                    _vp, _vp]),

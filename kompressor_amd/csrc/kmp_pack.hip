@@ -254,7 +254,7 @@ int64_t kmp_pack_blocks(int64_t n) { return n > 0 ? ceil_div(n, pk::kBlock) : 0;
 
 int64_t kmp_pack_workspace_bytes(int64_t n) {
   const int64_t nb = kmp_pack_blocks(n), nchunk = ceil_div(nb, pk::kChunk);
-  return ceil_div(nb * 4, 8) * 8 + nchunk * 16 + 8;
+  return ceil_div(nb * 4, 8) * 8 + nchunk * 16 + 16;  // + the scan's total and kmp_unpack_check's count
 }
 
 int64_t kmp_pack_total_offset(int64_t n) {

@@ -254,7 +254,52 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
     uint32_t q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = 0u;
-    if (param > 0 && uw > 0) {
+    bool done = false;
+    if (param > 0 && uw > 0 && uw <= 8) {
+      // fast path (the common case): the block's unary stream fits 8 words, held in registers by
+      // every lane of the group (same addresses: one request per cache line); the lane's codes
+      // span [S, E) -- after terminator 8j - 1 up to terminator 8j + 7 -- and, when that is at
+      // most 64 bits, are read off one 64-bit window with 8 ctz steps
+      uint32_t U[8], C[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) U[i] = i < uw ? us[i] : 0u;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        C[i] = acc;  // terminators before word i
+        acc += __builtin_popcount(U[i]);
+      }
+      auto term = [&](uint32_t r) __attribute__((always_inline)) {  // stream position of terminator r
+        uint32_t wsel = 0, word = U[0], before = 0;
+#pragma unroll
+        for (int i = 1; i < 8; ++i)
+          if (C[i] <= r) { wsel = i; word = U[i]; before = C[i]; }
+        return 32u * wsel + (uint32_t)select32(word, r - before);
+      };
+      auto pick = [&](uint32_t i) __attribute__((always_inline)) {  // U[i], 0 past the stream
+        uint32_t v = 0u;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v = i == (uint32_t)t ? U[t] : v;
+        return v;
+      };
+      if (acc >= 64u) {
+        const uint32_t S = j > 0 ? term(8u * j - 1u) + 1u : 0u;
+        const uint32_t E = term(8u * j + 7u) + 1u;
+        if (E - S <= 64u) {
+          const uint32_t w0 = S >> 5, sh = S & 31u;
+          const uint32_t a = pick(w0), b = pick(w0 + 1), c = pick(w0 + 2);
+          uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t t = (uint32_t)__builtin_ctzll(win | (1ull << 63));
+            q[e] = t;
+            win = t >= 63u ? 0ull : win >> (t + 1u);
+          }
+          done = true;
+        }
+      }
+    }
+    if (param > 0 && uw > 0 && !done) {  // general path: the stream words from memory
       uint32_t pos = 0;  // stream position where sample 8j's code starts
       if (j > 0) {
         const uint32_t r = 8u * j - 1u;  // 0-based rank of the terminator ending sample 8j - 1
@@ -299,6 +344,33 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
   }
 }
 
+// side information a blob may hold (one workgroup; written next to the scan's total): planes --
+// widths <= W; rice -- k < W, an all-zero block has no payload, a coded block holds its 2k plane
+// words and >= 2 unary words, at most 2W + 2 in all.  The count of violating blocks is read back
+// with the payload length before any unpack kernel runs.
+__global__ void __launch_bounds__(1024) side_check_kernel(int format, int W, const uint8_t* __restrict__ a,
+                                                        const uint8_t* __restrict__ b, int64_t nb,
+                                                        uint64_t* __restrict__ bad_out) {
+  __shared__ uint32_t part[16];
+  uint32_t bad = 0;
+  for (int64_t i = threadIdx.x; i < nb; i += 1024) {
+    if (format == 0) {
+      bad += a[i] > W;
+    } else {
+      const int k = (int)a[i] - 1, words = b[i];
+      bad += a[i] == 0 ? (words != 0) : (k >= W || words < 2 * k + 2 || words > 2 * W + 2);
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) bad += __shfl_xor(bad, d, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int i = 0; i < 16; ++i) t += part[i];
+    *bad_out = t;
+  }
+}
+
 }  // namespace rc
 }  // namespace kmp
 
@@ -335,6 +407,18 @@ int kmp_rice_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* params
   else if (W == 16) rc::rice_pack_kernel<16><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, w.local, w.cbase, nb, payload);
   else rc::rice_pack_kernel<32><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, w.local, w.cbase, nb, payload);
   return check_launch("rice_pack");
+}
+
+int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const uint8_t* side_b, int64_t n,
+                     void* workspace, kmp_stream_t stream) {
+  const int W = pk::sample_bits(dtype);
+  KMP_REQUIRE(W > 0, "unpack_check: unsupported dtype");
+  KMP_REQUIRE(format == 0 || format == 1, "unpack_check: format must be 0 (planes) or 1 (rice)");
+  KMP_REQUIRE(n >= 0 && workspace && (n == 0 || (side_a && (format == 0 || side_b))), "unpack_check: bad argument");
+  const int64_t nb = kmp_pack_blocks(n);
+  uint64_t* bad = (uint64_t*)((char*)workspace + kmp_pack_total_offset(n) + 8);
+  rc::side_check_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(format, W, side_a, side_b, nb, bad);
+  return check_launch("unpack_check");
 }
 
 int kmp_rice_unpack(int32_t dtype, const uint32_t* payload, int64_t n, const uint8_t* params, const uint8_t* bw,

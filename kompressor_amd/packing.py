@@ -175,7 +175,7 @@ def _parse_head(hb, avail):
 
 def _prepare(b, h):
     """Output buffer + the block-offset scan for one parsed blob; returns the device tensor of
-    [bad side-information blocks, scanned payload words] to check before unpacking."""
+    [scanned payload words, bad side-information blocks] to check before unpacking."""
     h['out'] = dev.empty(h['shape'], dev.CODE_TO_TORCH[h['code']])
     if h['n'] == 0:
         return None
@@ -184,22 +184,18 @@ def _prepare(b, h):
     if h['magic'] == ARRAY_MAGIC:
         widths = h['widths'] = b[woff:woff + nb]
         check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
-        # the widths must fit the sample type (the unpack kernel derives every block's payload
-        # offset from them, and their sum must be the header's payload length)
-        bad = (widths.to(torch.int32) > h['bits']).sum()
+        check(lib.kmp_unpack_check(0, h['code'], widths.data_ptr(), None, n, ws.data_ptr(), dev.stream()), 'unpack')
     else:
         params = h['params'] = b[woff:woff + nb]
         bw = h['bw'] = b[woff + _pad8(nb):woff + _pad8(nb) + nb]
         check(lib.kmp_unpack_plan(bw.data_ptr(), n, ws.data_ptr(), dev.stream()), 'rice unpack')
-        # side information the encoder can produce: k < W; an all-zero block has no payload; a
-        # coded block holds its 2k plane words and >= 2 unary words, at most 2W + 2 in all
-        k = params.to(torch.int32) - 1
-        bwi = bw.to(torch.int32)
-        coded = params > 0
-        bad = ((k >= h['bits']) | (coded & ((bwi < 2 * k + 2) | (bwi > 2 * h['bits'] + 2)))
-               | (~coded & (bwi != 0))).sum()
+        check(lib.kmp_unpack_check(1, h['code'], params.data_ptr(), bw.data_ptr(), n, ws.data_ptr(), dev.stream()),
+              'rice unpack')
+    # [payload words the stored block sizes add up to, blocks with impossible side information]
+    # (kmp_unpack_check: widths past W; Rice k >= W, a zero block with payload, a coded block
+    # smaller than its planes + 2 unary words or larger than 2W + 2 words)
     off = int(lib.kmp_pack_total_offset(n))
-    return torch.cat([bad.to(torch.int64).reshape(1), ws[off:off + 8].view(torch.int64)])
+    return ws[off:off + 16].view(torch.int64)
 
 
 def _run_unpack(b, h):
@@ -230,7 +226,7 @@ def _unpack_many(b, spans):
     live = [(i, c) for i, c in checks if c is not None]
     if live:
         vals = torch.stack([c for _, c in live]).tolist()  # the one synchronisation
-        for (i, _), (nbad, total) in zip(live, vals):
+        for (i, _), (total, nbad) in zip(live, vals):
             if nbad or total != parsed[i]['words']:
                 raise ValueError(f'array blob side information is inconsistent ({nbad} bad blocks, {total} '
                                  f'payload words, header says {parsed[i]["words"]})')
