@@ -121,7 +121,63 @@ __device__ __forceinline__ void sweep(const float* st, const L3P& a, int Yc, int
   }
 }
 
-template <typename T, bool DEC, int P>
+// The plane-c sweep on the matrix cores: the 14 channels KC of every cell of the wave's rows as
+// v_mfma_f32_16x16x4_f32 tiles -- M = 16 cells of one row, N = 16 channel columns (KC, then two
+// zero-weight pads), K = the 4 node columns dx of one node row (dz, dy): 16 steps for the 64
+// features.  Lane l feeds A[cell = l & 15][dx = l >> 4] = the staged node (dz, dy, cell + dx) and
+// B[dx][ch = l & 15] = W[n][KC[ch]] (16 weight VGPRs, loaded once), and receives channel l & 15
+// of cells 4 (l >> 4) .. +3 -- four consecutive cells, one 8-byte LDS store after the cast.  An
+// f32 MFMA is bit-for-bit the k-ordered fmaf chain from its C input (cdna_hip_programming.md §3),
+// so seeded with the bias and stepped in n order every value equals the VALU sweep's and the
+// oracle's chain.  The per-wave LDS tile [14][rows][Ex + pad] (u16) takes the results back to the
+// lane-owns-4-cells layout of the epilogue.
+template <typename T, int P>
+__device__ __forceinline__ void sweep_mfma(const float* st, const L3P& a, int Y0, int X, int r, const float (&wb)[16],
+                                           float bias, uint16_t* tile, int tstride, uint32_t (&out)[14][5]) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15, q = lane >> 4;
+  const int gpr = a.Ex / 16;  // 16-cell groups per row
+#pragma unroll 1
+  for (int g = 0; g < 16; g += 2) {  // two independent accumulators in flight
+    int base[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gg = g + u, ry = gg / gpr;
+      const int yc = min(Y0 + ry, a.Ey - 1);  // rows past the plane compute a clamped row (never read)
+      base[u] = (a.nr + yc) * a.pitch + (gg % gpr) * 16 + j + q;  // staged plane 1, row yc, node cell + dx
+    }
+    f32x4 acc[2] = {(f32x4){bias, bias, bias, bias}, (f32x4){bias, bias, bias, bias}};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int off = (s >> 2) * a.nr * a.pitch + (s & 3) * a.pitch;  // node plane dz, row dy
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(st[base[u] + off], wb[s], acc[u], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gg = g + u, ry = gg / gpr, cx = (gg % gpr) * 16 + 4 * q;
+      if (j < 14) {
+        const uint32_t c0 = cvt_sat<T>(acc[u][0]), c1 = cvt_sat<T>(acc[u][1]);
+        const uint32_t c2 = cvt_sat<T>(acc[u][2]), c3 = cvt_sat<T>(acc[u][3]);
+        *(uint2*)(tile + j * tstride + ry * a.Ex + cx) = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the wave reads back its own tile
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+  for (int kk = 0; kk < 14; ++kk) {
+    const uint2 v = *(const uint2*)(tile + kk * tstride + r * a.Ex + X);
+    out[kk][1] = v.x & 0xffffu;
+    out[kk][2] = v.x >> 16;
+    out[kk][3] = v.y & 0xffffu;
+    out[kk][4] = v.y >> 16;
+  }
+}
+
+template <typename T, bool DEC, int P, bool MF>
 __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   constexpr int VX = 4;  // u16: 4 outputs per lane
   static_assert(sizeof(T) == 2, "u16");
@@ -133,6 +189,10 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   float* st = (float*)smem;
   const int plane_words = a.nr * a.pitch;
   uint32_t* xrow = smem + NPL * plane_words;
+  // MF: per-wave transpose tiles [14][rows * Ex + 8] u16 after the exchange rows (the pad staggers
+  // the channels' rows over the LDS banks)
+  const int tstride = a.rows * a.Ex + 8;
+  uint16_t* tile = (uint16_t*)(xrow + a.nwv * kXch * a.Ex) + (size_t)(threadIdx.x >> 6) * 14 * tstride;
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
@@ -156,6 +216,17 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   const bool vy1 = Y < a.Lcy;
   const bool vy0 = Y >= 1;
   const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+
+  // MF: the lane's B operands (W[4s + dx][KC[ch]], dx = lane >> 4, ch = lane & 15; pad channels
+  // 14, 15 weigh 0) and the bias seed of its accumulator column (channel lane & 15)
+  float wb[16], bias_ch = 0.0f;
+  if constexpr (MF) {
+    constexpr int KCm[16] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16, -1, -1};
+    const int ch = KCm[lane & 15], dx = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wb[s] = ch >= 0 ? a.W[(4 * s + dx) * 19 + ch] : 0.0f;
+    bias_ch = ch >= 0 ? a.b[ch] : 0.0f;
+  }
 
   const int hplane = a.H * a.W_;
   const int lplane = a.Ey * a.Ex;
@@ -253,7 +324,8 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   constexpr int KQ[kNQ] = {5, 13, 14, 17, 18};                               // plane c-1
   uint32_t PC[14][5], PQ[5][5];
   sweep<T, P, 0, 5>(st, a, Yc, X, KQ, 0, PQ);
-  sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), PC);
+  if constexpr (MF) sweep_mfma<T, P>(st, a, Y0, X, r, wb, bias_ch, tile, tstride, PC);
+  else sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), PC);
   auto& P0 = PC[0]; auto& P1 = PC[1]; auto& P2 = PC[2]; auto& P3 = PC[3]; auto& P4 = PC[4];
   auto& P6 = PC[5]; auto& P7 = PC[6]; auto& P8 = PC[7]; auto& P9 = PC[8]; auto& P10 = PC[9];
   auto& P11 = PC[10]; auto& P12 = PC[11]; auto& P15 = PC[12]; auto& P16 = PC[13];
@@ -410,7 +482,8 @@ static int l3p_env(const char* name, int dflt) {
 
 template <typename T>
 static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
-                               const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds) {
+                               const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds,
+                               bool& mfma) {
   constexpr int VX = 4;
   if (!std::is_same<T, uint16_t>::value) return false;
   if (l3p_env("KMP_DISABLE_FAST", 0) || l3p_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
@@ -445,6 +518,13 @@ static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   const int npl = 2 * P + 3;
   lds = (size_t)(npl * a.nr * a.pitch + waves * l3p::kXch * g.E[2]) * sizeof(uint32_t);
   if (lds > 64 * 1024) return false;
+  // the MFMA plane-c sweep (16-cell row groups, P = 1): its per-wave transpose tiles
+  mfma = l3p_env("KMP_L3P_MFMA", 1) && P == 1 && g.E[2] % 16 == 0;
+  if (mfma) {
+    const size_t tiles = (size_t)waves * 14 * (rows * g.E[2] + 8) * sizeof(uint16_t);
+    if (lds + tiles > 64 * 1024) mfma = false;
+    else lds += tiles;
+  }
   const int64_t nblk = B * (ze - zb);
   a.xcd_per = (l3p_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
   grid = dim3((unsigned)nblk);
@@ -460,7 +540,8 @@ int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
-    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    bool mfma = false;
+    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds, mfma)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -472,7 +553,8 @@ int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    l3p::linear3dp_kernel<T, false, 1><<<grid, block, lds, stream>>>(a);
+    if (mfma) l3p::linear3dp_kernel<T, false, 1, true><<<grid, block, lds, stream>>>(a);
+    else l3p::linear3dp_kernel<T, false, 1, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3dp_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -486,7 +568,8 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
-    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
+    bool mfma = false;
+    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds, mfma)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -499,7 +582,8 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    l3p::linear3dp_kernel<T, true, 1><<<grid, block, lds, stream>>>(a);
+    if (mfma) l3p::linear3dp_kernel<T, true, 1, true><<<grid, block, lds, stream>>>(a);
+    else l3p::linear3dp_kernel<T, true, 1, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3dp_decode");
   }
   return KMP_ERR_UNSUPPORTED;

@@ -254,52 +254,7 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
     uint32_t q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = 0u;
-    bool done = false;
-    if (param > 0 && uw > 0 && uw <= 8) {
-      // fast path (the common case): the block's unary stream fits 8 words, held in registers by
-      // every lane of the group (same addresses: one request per cache line); the lane's codes
-      // span [S, E) -- after terminator 8j - 1 up to terminator 8j + 7 -- and, when that is at
-      // most 64 bits, are read off one 64-bit window with 8 ctz steps
-      uint32_t U[8], C[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) U[i] = i < uw ? us[i] : 0u;
-      uint32_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        C[i] = acc;  // terminators before word i
-        acc += __builtin_popcount(U[i]);
-      }
-      auto term = [&](uint32_t r) __attribute__((always_inline)) {  // stream position of terminator r
-        uint32_t wsel = 0, word = U[0], before = 0;
-#pragma unroll
-        for (int i = 1; i < 8; ++i)
-          if (C[i] <= r) { wsel = i; word = U[i]; before = C[i]; }
-        return 32u * wsel + (uint32_t)select32(word, r - before);
-      };
-      auto pick = [&](uint32_t i) __attribute__((always_inline)) {  // U[i], 0 past the stream
-        uint32_t v = 0u;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v = i == (uint32_t)t ? U[t] : v;
-        return v;
-      };
-      if (acc >= 64u) {
-        const uint32_t S = j > 0 ? term(8u * j - 1u) + 1u : 0u;
-        const uint32_t E = term(8u * j + 7u) + 1u;
-        if (E - S <= 64u) {
-          const uint32_t w0 = S >> 5, sh = S & 31u;
-          const uint32_t a = pick(w0), b = pick(w0 + 1), c = pick(w0 + 2);
-          uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint32_t t = (uint32_t)__builtin_ctzll(win | (1ull << 63));
-            q[e] = t;
-            win = t >= 63u ? 0ull : win >> (t + 1u);
-          }
-          done = true;
-        }
-      }
-    }
-    if (param > 0 && uw > 0 && !done) {  // general path: the stream words from memory
+    if (param > 0 && uw > 0) {
       uint32_t pos = 0;  // stream position where sample 8j's code starts
       if (j > 0) {
         const uint32_t r = 8u * j - 1u;  // 0-based rank of the terminator ending sample 8j - 1
