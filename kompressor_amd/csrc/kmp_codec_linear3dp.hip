@@ -132,36 +132,72 @@ __device__ __forceinline__ void sweep(const float* st, const L3P& a, int Yc, int
 // oracle's chain.  The per-wave LDS tile [14][rows][Ex + pad] (u16) takes the results back to the
 // lane-owns-4-cells layout of the epilogue.
 template <typename T, int P>
-__device__ __forceinline__ void sweep_mfma(const float* st, const L3P& a, int Y0, int X, int r, const float (&wb)[16],
-                                           float bias, uint16_t* tile, int tstride, uint32_t (&out)[14][5]) {
+__device__ __forceinline__ void sweep_mfma(const float* st, const L3P& a, int Yc, int Y0, int X, int r,
+                                           const float (&wb)[16], float bias, uint16_t* tile, int tstride,
+                                           uint32_t (&PQ)[kNQ][5], uint32_t (&out)[14][5]) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NB = 2 * P + 2;
   const int lane = threadIdx.x & 63;
   const int j = lane & 15, q = lane >> 4;
   const int gpr = a.Ex / 16;  // 16-cell groups per row
-#pragma unroll 1
-  for (int g = 0; g < 16; g += 2) {  // two independent accumulators in flight
-    int base[2];
+  // plane c: 16 groups of 16 cells in flight on the matrix pipe; plane c-1: the VALU chain of
+  // the 5 channels KQ of the lane's 4 cells (sweep<>'s arithmetic), one node row per step, so
+  // the scheduler interleaves the packed FMAs with the MFMAs of the same step
+  f32x4 acc[16];
+  int base[16];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int gg = g + u, ry = gg / gpr;
-      const int yc = min(Y0 + ry, a.Ey - 1);  // rows past the plane compute a clamped row (never read)
-      base[u] = (a.nr + yc) * a.pitch + (gg % gpr) * 16 + j + q;  // staged plane 1, row yc, node cell + dx
-    }
-    f32x4 acc[2] = {(f32x4){bias, bias, bias, bias}, (f32x4){bias, bias, bias, bias}};
+  for (int u = 0; u < 16; ++u) {
+    const int ry = u / gpr;
+    const int yc = min(Y0 + ry, a.Ey - 1);  // rows past the plane compute a clamped row (never read)
+    base[u] = (a.nr + yc) * a.pitch + (u % gpr) * 16 + j + q;  // staged plane 1, row yc, node cell + dx
+    acc[u] = (f32x4){bias, bias, bias, bias};
+  }
+  const __attribute__((address_space(4))) float* Wc = (const __attribute__((address_space(4))) float*)a.Wr;
+  f32x2 aq[kNQ][2];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int off = (s >> 2) * a.nr * a.pitch + (s & 3) * a.pitch;  // node plane dz, row dy
+  for (int kk = 0; kk < kNQ; ++kk) {
+    const float bk = a.b[kKQ[kk]];
+    aq[kk][0] = (f32x2){bk, bk};
+    aq[kk][1] = (f32x2){bk, bk};
+  }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(st[base[u] + off], wb[s], acc[u], 0, 0, 0);
-    }
+  for (int s = 0; s < NB * NB; ++s) {
+    const int dz = s / NB, dy = s % NB;
+    const int off = dz * a.nr * a.pitch + dy * a.pitch;  // node plane dz, row dy
+    float bv[16];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int gg = g + u, ry = gg / gpr, cx = (gg % gpr) * 16 + 4 * q;
-      if (j < 14) {
-        const uint32_t c0 = cvt_sat<T>(acc[u][0]), c1 = cvt_sat<T>(acc[u][1]);
-        const uint32_t c2 = cvt_sat<T>(acc[u][2]), c3 = cvt_sat<T>(acc[u][3]);
-        *(uint2*)(tile + j * tstride + ry * a.Ex + cx) = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
+    for (int u = 0; u < 16; ++u) bv[u] = st[base[u] + off];
+    // VALU: plane c-1 (staged planes 0..), the lane's 7 nodes of this row
+    const float* rowp = (const float*)__builtin_assume_aligned(st + (dz * a.nr + (Yc + dy)) * a.pitch + X, 16);
+    const float4 f0 = *(const float4*)rowp, f1 = *(const float4*)(rowp + 4);
+    const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[u], wb[s], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int dx = 0; dx < NB; ++dx) {
+#pragma unroll
+      for (int kk = 0; kk < kNQ; ++kk) {
+        const float w = Wc[(s * kNQ + kk) * NB + dx];
+        const f32x2 w2 = {w, w};
+        aq[kk][0] = __builtin_elementwise_fma((f32x2){f[dx], f[dx + 1]}, w2, aq[kk][0]);
+        aq[kk][1] = __builtin_elementwise_fma((f32x2){f[dx + 2], f[dx + 3]}, w2, aq[kk][1]);
       }
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < kNQ; ++kk) {
+    PQ[kk][1] = cvt_sat<T>(aq[kk][0].x);
+    PQ[kk][2] = cvt_sat<T>(aq[kk][0].y);
+    PQ[kk][3] = cvt_sat<T>(aq[kk][1].x);
+    PQ[kk][4] = cvt_sat<T>(aq[kk][1].y);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int ry = u / gpr, cx = (u % gpr) * 16 + 4 * q;
+    if (j < 14) {
+      const uint32_t c0 = cvt_sat<T>(acc[u][0]), c1 = cvt_sat<T>(acc[u][1]);
+      const uint32_t c2 = cvt_sat<T>(acc[u][2]), c3 = cvt_sat<T>(acc[u][3]);
+      *(uint2*)(tile + j * tstride + ry * a.Ex + cx) = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the wave reads back its own tile
@@ -323,9 +359,12 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   constexpr int KC[kNC] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16};  // plane c
   constexpr int KQ[kNQ] = {5, 13, 14, 17, 18};                               // plane c-1
   uint32_t PC[14][5], PQ[5][5];
-  sweep<T, P, 0, 5>(st, a, Yc, X, KQ, 0, PQ);
-  if constexpr (MF) sweep_mfma<T, P>(st, a, Y0, X, r, wb, bias_ch, tile, tstride, PC);
-  else sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), PC);
+  if constexpr (MF) {
+    sweep_mfma<T, P>(st, a, Yc, Y0, X, r, wb, bias_ch, tile, tstride, PQ, PC);
+  } else {
+    sweep<T, P, 0, 5>(st, a, Yc, X, KQ, 0, PQ);
+    sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), PC);
+  }
   auto& P0 = PC[0]; auto& P1 = PC[1]; auto& P2 = PC[2]; auto& P3 = PC[3]; auto& P4 = PC[4];
   auto& P6 = PC[5]; auto& P7 = PC[6]; auto& P8 = PC[7]; auto& P9 = PC[8]; auto& P10 = PC[9];
   auto& P11 = PC[10]; auto& P12 = PC[11]; auto& P15 = PC[12]; auto& P16 = PC[13];
@@ -519,7 +558,7 @@ static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   lds = (size_t)(npl * a.nr * a.pitch + waves * l3p::kXch * g.E[2]) * sizeof(uint32_t);
   if (lds > 64 * 1024) return false;
   // the MFMA plane-c sweep (16-cell row groups, P = 1): its per-wave transpose tiles
-  mfma = l3p_env("KMP_L3P_MFMA", 1) && P == 1 && g.E[2] % 16 == 0;
+  mfma = l3p_env("KMP_L3P_MFMA", 0) && P == 1 && g.E[2] % 16 == 0;
   if (mfma) {
     const size_t tiles = (size_t)waves * 14 * (rows * g.E[2] + 8) * sizeof(uint16_t);
     if (lds + tiles > 64 * 1024) mfma = false;

@@ -83,9 +83,13 @@ def test_linear_chunks(kom):
 
 @pytest.mark.parametrize('shape', [(8, 64, 64, 64, 1), (2, 17, 30, 16, 1), (1, 9, 14, 128, 1), (2, 12, 33, 32, 1),
                                    (1, 6, 8, 8, 1)])
-def test_linear_fused_p1(kom, shape):
+@pytest.mark.parametrize('mfma', ['0', '1'])
+def test_linear_fused_p1(kom, shape, mfma, monkeypatch):
     """The fused LinearPredictor p = 1 volume kernel (kmp_codec_linear3dp.hip): residuals and lowres
-    bit-exact to the oracle's fma chain + aggregation, lossless, z-region (chunked) launches."""
+    bit-exact to the oracle's fma chain + aggregation, lossless, z-region (chunked) launches -- with
+    the plane-c channels on the packed-FMA VALU sweep (default) and on the f32 MFMA sweep
+    (KMP_L3P_MFMA=1, v_mfma_f32_16x16x4_f32: the same k-ordered chain, so the same bits)."""
+    monkeypatch.setenv('KMP_L3P_MFMA', mfma)
     hi = _data(shape, np.uint16, 7)
     w, b = _weights(3, 1, 8, np.uint16)
     pred = kom.LinearPredictor(w, b, 1, 3)
