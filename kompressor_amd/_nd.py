@@ -710,7 +710,23 @@ def _chunk_regions(boxes, E):
         else:
             regions.extend(boxes[k:j])
         k = j
-    return regions, _covers(regions, E)
+    return _merge_slabs(regions, E), _covers(regions, E)
+
+
+def _merge_slabs(regions, E):
+    """Adjacent full-cross-section slabs merged into one region: the fused kernels give any region
+    the whole-array call's values (chunk invariance, tests/volume/test_encode_decode.py:509-539), so
+    slabs that tile [a, b) along the leading axis are ONE launch -- at chunk = 32 on 64^3 tiles the
+    windows' two slabs become the single whole-frame launch."""
+    full = [r for r in regions if all(tuple(r[a]) == (0, e) for a, e in enumerate(E) if a > 0)]
+    rest = [r for r in regions if not all(tuple(r[a]) == (0, e) for a, e in enumerate(E) if a > 0)]
+    merged = []
+    for r in sorted(full, key=lambda r: r[0][0]):
+        if merged and merged[-1][0][1] == r[0][0]:
+            merged[-1] = [(merged[-1][0][0], r[0][1])] + list(merged[-1][1:])
+        else:
+            merged.append(list(r))
+    return merged + rest
 
 
 def d_process_chunks(predictions_fn, code_fn, lowres, reference_maps, chunk_list, padding, nsp):

@@ -170,9 +170,8 @@ def test_fused_chunk_regions_merge_and_cover():
     chunks = list(product(*[yield_chunks(l, 32) for l in L]))
     regions, covered = fused_chunk_regions(chunks, E, 3)
     assert covered
-    # one launch per distinct slab, overlapping planes launched once
-    assert [r[0] for r in regions] == [(0, 30), (30, 32)]
-    assert all(r[1:] == [(0, 32), (0, 32)] for r in regions)
+    # the two slabs (overlapping planes launched once) tile the frame: merged into ONE launch
+    assert regions == [[(0, 32), (0, 32), (0, 32)]]
     # odd extents, small chunks, 2D
     for E2, L2, c in [((8, 9), (9, 9), 6), ((17, 16), (17, 17), 11), ((5, 5), (5, 5), 4)]:
         ch = list(product(*[yield_chunks(l, c) for l in L2]))
