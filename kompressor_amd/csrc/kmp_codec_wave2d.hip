@@ -13,6 +13,7 @@
 // the 5-way aggregation onto LR / UD / C (image/utils.py:58-86: sums of 1/2 means
 // >> log2(count) == its f32 x0.5 + truncation), and the mod-2^k coder (utils.py:38-55).
 // Image-per-XCD block order keeps the workgroup-edge halo rows in one L2.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kmp_wave.h"
@@ -33,6 +34,7 @@ struct W2 {
   int32_t txn, rows, nwv, ngrp;  // lanes per row, rows per wave, waves per workgroup, workgroups per image
   int32_t xcd_per;               // > 0: image-per-XCD block order (workgroups per image)
   int32_t ybeg, yend;            // output rows written (a chunked-driver region; all rows otherwise)
+  int32_t nvblk;                 // virtual blocks (B * ngrp), grid-strided over the workgroups
   const float* wt;               // LIN: LinearPredictor weights [4, 5] row-major and bias [5]
   const float* bias;
 };
@@ -47,7 +49,7 @@ __device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: 
 // per-cell channels): pred[cell, k] = fma chain over the 4 nodes (n = dy*2 + dx) from b[k], cast
 // to T; LR = ch0 (x) + ch1 (x-1), UD = ch2 (y) + ch3 (y-1), C = ch4, with the same counts / shifts.
 template <typename T, bool DEC, bool ONE, bool LIN>
-__global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
+__device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   using V = typename std::conditional<DEC, uint2, uint4>::type;
@@ -57,7 +59,7 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   const int tx = lane % a.txn;
   const int r = lane / a.txn;
   const int X = tx * VX;
-  int blk = (int)blockIdx.x;
+  int blk = vblk;
   if (a.xcd_per > 0) {
     const int x = blk % 8, k = blk / 8;
     blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
@@ -241,6 +243,14 @@ __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   }
 }
 
+// A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; a multiple of 8
+// workgroups keeps every virtual block on the XCD of the image-per-XCD order): fewer, longer-lived
+// workgroups than one per 16 output rows (KMP_W2_ITERS virtual blocks per workgroup)
+template <typename T, bool DEC, bool ONE, bool LIN>
+__global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_body<T, DEC, ONE, LIN>(a, v);
+}
+
 // uint8 form of the mean kernel (BASELINE config C2), SWAR: the lane's 8 cells travel as 4 words
 // of two 16-bit lanes each, so every node / mean / prediction / residual step is one 32-bit op
 // for two cells (node pair sums <= 510, means <= 255: no carry between the halves; residuals add
@@ -257,7 +267,7 @@ __device__ __forceinline__ uint32_t shift_pairs(uint32_t hi, uint32_t lo) {  // 
 }
 
 template <bool DEC>
-__global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
+__device__ __forceinline__ void wave2d_u8_body(const W2& a, int vblk) {
   constexpr int VX = 8;
   constexpr uint32_t B8 = 0x00ff00ffu;
   using V = typename std::conditional<DEC, uint2, uint4>::type;
@@ -267,7 +277,7 @@ __global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
   const int tx = lane % a.txn;
   const int r = lane / a.txn;
   const int X = tx * VX;
-  int blk = (int)blockIdx.x;
+  int blk = vblk;
   if (a.xcd_per > 0) {
     const int x = blk % 8, k = blk / 8;
     blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
@@ -398,6 +408,11 @@ __global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
   }
 }
 
+template <bool DEC>
+__global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_u8_body<DEC>(a, v);
+}
+
 }  // namespace w2
 
 static int w2_env(const char* name, int dflt) {
@@ -439,7 +454,11 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.ybeg = (int)yb;
   a.yend = (int)ye;
   const int64_t nblk = B * ngrp;
-  grid = dim3((unsigned)nblk);
+  const int64_t iters = std::max(1, w2_env("KMP_W2_ITERS", 2));  // 2: +5 % encode, +1.5 % decode at C2 (ab_wave2d_iters.log)
+  int64_t nwg = ceil_div(nblk, iters);
+  if (a.xcd_per > 0) nwg = ceil_div(nwg, (int64_t)8) * 8;  // keep v % 8 == blockIdx % 8
+  a.nvblk = (int)nblk;
+  grid = dim3((unsigned)std::min(nwg, nblk));
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);
 }
