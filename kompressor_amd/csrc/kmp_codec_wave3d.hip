@@ -22,6 +22,7 @@
 // >> log2(count) == its f32 x0.5 / x0.25 + truncation for these ranges) and the mod-2^k coder
 // (utils.py:38-55), then writes lowres + 7 maps (8 B per lane each) or the 2x2x2 highres block
 // rows (16 B per lane each).
+#include <algorithm>
 #include <cstdlib>
 
 #include "kmp_wave.h"
@@ -44,6 +45,7 @@ struct W3 {
   int32_t xcd_per;  // > 0: XCD-contiguous block order (blocks per XCD), 0: identity
   int32_t nt_nodes; // plane kernel: 1 = non-temporal node-row loads, 0 = default policy (L2-shared halo)
   int64_t nB;       // tiles in the batch (debug-build bounds checks only)
+  int32_t nvblk;    // virtual blocks, grid-strided over the workgroups
 };
 
 // rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row;
@@ -62,8 +64,8 @@ struct OutRows {
 };
 
 // WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
-template <typename T, bool DEC, int PL, int WPE, bool ONE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
+template <typename T, bool DEC, int PL, bool ONE>
+__device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   using NR = NodeRows<DEC>;
@@ -76,7 +78,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   const int X = tx * VX;
   // a.xcd_per > 0: tile-per-XCD order -- XCD x = blockIdx % 8 codes whole tiles, its k-th block
   // is block (k % per_tile) of tile (k / per_tile) * 8 + x, so the z-halo neighbours share an L2
-  int blk = (int)blockIdx.x;
+  int blk = vblk;
   if (a.xcd_per > 0) {
     const int x = blk % 8, k = blk / 8;
     blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
@@ -355,6 +357,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 }
 
+// A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; gridDim a multiple
+// of 8 keeps each virtual block on the XCD the tile-per-XCD order gives it)
+template <typename T, bool DEC, int PL, int WPE, bool ONE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave3d_plane_body<T, DEC, PL, ONE>(a, v);
+}
+
 }  // namespace w3
 
 // ------------------------------------------------------------------------------------------
@@ -403,7 +412,11 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
   a.nt_nodes = w3_env("KMP_W3_NT_NODES", 0);
   a.nB = B;
-  grid = dim3((unsigned)nblk);
+  const int64_t iters = std::max(1, w3_env("KMP_W3_ITERS", 1));
+  int64_t nwg = ceil_div(nblk, iters);
+  if (a.xcd_per > 0) nwg = ceil_div(nwg, (int64_t)8) * 8;  // keep v % 8 == blockIdx % 8
+  a.nvblk = (int)nblk;
+  grid = dim3((unsigned)std::min(nwg, nblk));
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);
 }
