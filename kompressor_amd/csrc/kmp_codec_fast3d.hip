@@ -495,6 +495,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
     if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3r_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1, MFMA
+    if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
@@ -528,6 +530,8 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3r_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
