@@ -569,6 +569,188 @@ __global__ void __launch_bounds__(kThreads) mean_predict_lds_kernel(
   }
 }
 
+// Words of padding before and after the two LDS cell planes of the mean predictor kernels.
+__host__ __device__ __forceinline__ int32_t mp_pad_words(int64_t Lcx) { return (int32_t)(4 * ((Lcx + 4) / 4)); }
+
+// Row mapping of a plane's positions onto the workgroup: a wave covers R = 64 / W rows of W
+// consecutive x positions (lane = r * W + x), the 4 waves interleave row groups.  Every lane's
+// (row, x) is fixed per call, so the per-position work has no index division, and the
+// conditions that depend on the row (first / last row) change only between row groups.
+struct RowMap {
+  int32_t lr, lx, R;  // this lane's row within the group, its x, rows per wave
+  bool lane_ok;
+};
+__device__ __forceinline__ RowMap row_map(int32_t W) {
+  RowMap m;
+  const int32_t lane = threadIdx.x & 63;
+  m.R = 64 / W;
+  m.lr = (int32_t)((float)lane * (1.0f / (float)W));  // lane < 64: exact after the fix-up
+  if (m.lr * W > lane) --m.lr;
+  else if ((m.lr + 1) * W <= lane) ++m.lr;
+  m.lx = lane - m.lr * W;
+  m.lane_ok = m.lr < m.R;
+  return m;
+}
+
+// The 7 maps at the output positions of plane oz from two LDS cell planes (cell plane oz in slot
+// s_cur, oz - 1 in s_prev; ``cells`` must have Lcx + 1 readable words before slot 0 and after
+// slot 1).  Positions
+// ox < Lcx go through the row mapping in x chunks of <= 64; the last column (ox == Lcx, where
+// only the three maps with an even x parity exist and only the cells at ox - 1 contribute) is a
+// separate pass with one lane per row.
+template <typename T>
+__device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t oz, int64_t b, int32_t Lcz,
+                                                int32_t Lcy, int32_t Lcx, const MapPtrs& outs, int s_cur, int s_prev) {
+  const int32_t nplanes = Lcz + 1, oyn = Lcy + 1, oxn = Lcx + 1, cplane = Lcy * Lcx;
+  const bool z0 = oz < Lcz, z1 = oz >= 1;  // cell planes oz and oz - 1 exist
+  T* const o0 = (T*)outs.p[0] + ((b * Lcz + oz) * Lcy) * oxn;       // LR (1,1,0)
+  T* const o1 = (T*)outs.p[1] + ((b * Lcz + oz) * oyn) * Lcx;       // UD (1,0,1)
+  T* const o2 = (T*)outs.p[2] + ((b * nplanes + oz) * Lcy) * Lcx;   // FB (0,1,1)
+  T* const o3 = (T*)outs.p[3] + ((b * Lcz + oz) * Lcy) * Lcx;       // C  (1,1,1)
+  T* const o4 = (T*)outs.p[4] + ((b * Lcz + oz) * oyn) * oxn;       // Z  (1,0,0)
+  T* const o5 = (T*)outs.p[5] + ((b * nplanes + oz) * Lcy) * oxn;   // Y  (0,1,0)
+  T* const o6 = (T*)outs.p[6] + ((b * nplanes + oz) * oyn) * Lcx;   // X  (0,0,1)
+  const uint32_t* cur = cells + s_cur * cplane;
+  const uint32_t* prev = cells + s_prev * cplane;
+  const uint32_t nz = (uint32_t)z0 + z1;
+  const int32_t wv = threadIdx.x >> 6;
+  for (int32_t xc = 0; xc < Lcx; xc += 64) {
+    const RowMap m = row_map(Lcx - xc < 64 ? Lcx - xc : 64);
+    const int32_t ox = xc + m.lx;
+    const bool x1 = ox >= 1;
+    for (int32_t oy0 = wv * m.R; oy0 <= Lcy; oy0 += 4 * m.R) {
+      const int32_t oy = oy0 + m.lr;
+      if (!m.lane_ok || oy > Lcy) continue;
+      const bool y0 = oy < Lcy, y1 = oy >= 1;
+      const int32_t q = oy * Lcx + ox;  // cell (oy, ox)
+      // c<z><y><x>: cell (oz - z, oy - y, ox - x); 0 where it does not exist.  The reads are
+      // unconditional (the cell slots carry Lcx + 1 words of padding on both sides, so every
+      // index here stays inside the workgroup's LDS) and masked afterwards: no exec-mask
+      // branch per read.
+      const uint32_t mz0 = z0 ? ~0u : 0u, mz1 = z1 ? ~0u : 0u;
+      const uint32_t my0 = y0 ? ~0u : 0u, my1 = y1 ? ~0u : 0u, mx1 = x1 ? ~0u : 0u;
+      const uint32_t c000 = cur[q] & (mz0 & my0), c001 = cur[q - 1] & (mz0 & my0 & mx1);
+      const uint32_t c010 = cur[q - Lcx] & (mz0 & my1), c011 = cur[q - Lcx - 1] & (mz0 & my1 & mx1);
+      const uint32_t c100 = prev[q] & (mz1 & my0), c101 = prev[q - 1] & (mz1 & my0 & mx1);
+      const uint32_t c110 = prev[q - Lcx] & (mz1 & my1);
+      const uint32_t nx = 1u + x1, ny = (uint32_t)y0 + y1;
+      const int32_t px = oy * oxn + ox, pc = oy * Lcx + ox;
+      o6[pc] = (T)((c000 + c010 + c110 + c100) >> ((nz * ny) >> 1));
+      if (z0) {
+        o1[pc] = (T)((c000 + c010) >> (ny >> 1));
+        o4[px] = (T)((c000 + c001 + c011 + c010) >> ((ny * nx) >> 1));
+      }
+      if (y0) {
+        o2[pc] = (T)((c000 + c100) >> (nz >> 1));
+        o5[px] = (T)((c000 + c001 + c101 + c100) >> ((nz * nx) >> 1));
+        if (z0) {
+          o0[px] = (T)((c000 + c001) >> (nx >> 1));
+          o3[pc] = (T)c000;
+        }
+      }
+    }
+  }
+  // the last column, ox = Lcx: LR, Z, Y from the cells at x = Lcx - 1
+  for (int32_t oy = threadIdx.x; oy <= Lcy; oy += kThreads) {
+    const bool y0 = oy < Lcy, y1 = oy >= 1;
+    const int32_t q = oy * Lcx + Lcx - 1;
+    const uint32_t c001 = cur[q] & (z0 && y0 ? ~0u : 0u), c011 = cur[q - Lcx] & (z0 && y1 ? ~0u : 0u);
+    const uint32_t c101 = prev[q] & (z1 && y0 ? ~0u : 0u);
+    const uint32_t ny = (uint32_t)y0 + y1;
+    const int32_t px = oy * oxn + Lcx;
+    if (z0) o4[px] = (T)((c001 + c011) >> (ny >> 1));
+    if (y0) {
+      o5[px] = (T)((c001 + c101) >> (nz >> 1));
+      if (z0) o0[px] = (T)c001;
+    }
+  }
+}
+
+// Fused mean predictor, one workgroup per output plane (3D, u8 / u16, C == 1, p <= 2).  The
+// 2p+3 window planes that output plane oz reads are copied into LDS as one contiguous byte range
+// with 16-byte loads; the two cell planes it aggregates (oz - 1 and oz) are summed there --
+// directly for p = 0 (8 nodes), separably for p >= 1 (x sums of 2p+2 nodes first, then the
+// (2p+2)^2 box of x sums) -- and each thread then owns output positions (oy, ox) and writes all 7
+// maps at that position from the 8 cells around it.  The rolling kernel above fetches every
+// node of every cell with its own 2-byte global load; that was its cost (131 -> 93 us for the
+// 512 C3 windows).  A z-rolling variant of this kernel (3-slot node ring, next plane prefetched
+// in registers, each cell plane summed once) measured slower, 100-108 us: the plane-parallel grid
+// hides the load latency as well and has 8x the workgroups.
+template <typename T, int P>
+__global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
+    const T* __restrict__ win, E3<int32_t> S, int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs, int32_t xcd_per,
+    int32_t nodes_bytes, int32_t xs_bytes) {
+  constexpr int KK = 2 * P + 2;
+  constexpr float NN = (float)(KK * KK * KK);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int32_t nplanes = Lcz + 1;
+  int32_t blk = (int32_t)blockIdx.x;
+  if (xcd_per > 0) {  // consecutive planes of one window on one XCD: shared node planes hit its L2
+    const int32_t x = blk % 8, k = blk / 8;
+    blk = ((k / xcd_per) * 8 + x) * xcd_per + (k % xcd_per);
+  }
+  const int32_t oz = blk % nplanes;
+  const int64_t b = blk / nplanes;
+  const int32_t S1 = S.e[1], S2 = S.e[2], plane = S1 * S2;
+  const int32_t zlo = oz >= 1 ? oz - 1 : 0;
+  const int32_t zhi = oz + KK < S.e[0] ? oz + KK : S.e[0];  // node planes [zlo, zhi)
+
+  // ---- node planes -> LDS: the aligned 16-byte blocks covering the byte range (every block
+  // holds at least one byte of the window, so it lies in a mapped page) ----
+  const unsigned char* g0 = (const unsigned char*)(win + (b * S.e[0] + zlo) * (int64_t)plane);
+  const int32_t shift = (int32_t)((uintptr_t)g0 & 15);
+  const uint4* src = (const uint4*)(g0 - shift);
+  const int32_t nchunk = ((zhi - zlo) * plane * (int32_t)sizeof(T) + shift + 15) >> 4;
+  for (int32_t i = threadIdx.x; i < nchunk; i += kThreads) *(uint4*)(smem + 16 * i) = src[i];
+  const T* nodes = (const T*)(smem + shift);  // [z - zlo][y][x]
+  uint32_t* xs = (uint32_t*)(smem + nodes_bytes);  // p >= 1: [z - zlo][y][cx] sums over x
+  // [slot: z = oz - 1 + slot][cy][cx], after a pad of >= Lcx + 1 words
+  uint32_t* cells = (uint32_t*)(smem + nodes_bytes + xs_bytes) + mp_pad_words(Lcx);
+  __syncthreads();
+
+  const int32_t cplane = Lcy * Lcx;
+  const float rcx = 1.0f / (float)Lcx;
+  if constexpr (P > 0) {
+    const int32_t nxs = (zhi - zlo) * S1 * Lcx;
+    for (int32_t i = threadIdx.x; i < nxs; i += kThreads) {
+      int32_t zy, cx;
+      divmod_small(i, Lcx, rcx, zy, cx);
+      const T* row = nodes + zy * S2 + cx;  // (z - zlo) * plane + y * S2 == zy * S2
+      uint32_t s = 0;
+#pragma unroll
+      for (int dx = 0; dx < KK; ++dx) s += row[dx];
+      xs[i] = s;
+    }
+    __syncthreads();
+  }
+  // cell planes oz - 1 (slot 0) and oz (slot 1), rows of both planes through the row mapping
+  const int32_t wv = threadIdx.x >> 6;
+  for (int32_t xc = 0; xc < Lcx; xc += 64) {
+    const RowMap m = row_map(Lcx - xc < 64 ? Lcx - xc : 64);
+    const int32_t cx = xc + m.lx;
+    for (int32_t r0 = wv * m.R; r0 < 2 * Lcy; r0 += 4 * m.R) {
+      const int32_t r = r0 + m.lr;
+      const int32_t slot = r >= Lcy, cy = r - slot * Lcy;
+      const int32_t z = oz - 1 + slot;
+      if (!m.lane_ok || r >= 2 * Lcy || z < 0 || z >= Lcz) continue;  // (a missing plane is never read)
+      uint32_t s = 0;
+      if constexpr (P == 0) {
+        const T* q = nodes + (z - zlo) * plane + cy * S2 + cx;
+        s = (uint32_t)q[0] + q[1] + q[S2] + q[S2 + 1] + q[plane] + q[plane + 1] + q[plane + S2] + q[plane + S2 + 1];
+      } else {
+#pragma unroll
+        for (int dz = 0; dz < KK; ++dz)
+#pragma unroll
+          for (int dy = 0; dy < KK; ++dy) s += xs[((z - zlo + dz) * S1 + cy + dy) * Lcx + cx];
+      }
+      cells[slot * cplane + cy * Lcx + cx] = (uint32_t)cast_f32<T>((float)s / NN);  // exact sum (< 2^24)
+    }
+  }
+  __syncthreads();
+
+  mean_maps_plane<T>(cells, oz, b, Lcz, Lcy, Lcx, outs, 1, 0);
+}
+
 // ------------------------------------------------------------------------------------------
 // Mean predictor on a padded lowres window (tests/volume/test_encode_decode.py:46-53):
 // cell mean = astype(T)(f32 sum of the (2p+2)^d neighbourhood / N), then the map aggregation.
@@ -1207,6 +1389,25 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     T* cm = (T*)outs.p[center_map(nsp)];
     const bool small = fits32({vol(B, S, C), total});
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
+      // one workgroup per output plane when the plane's window planes fit LDS
+      const int64_t plane = S.e[1] * S.e[2];
+      const int64_t nodes_bytes = 16 * (ceil_div((2 * padding + 3) * plane * (int64_t)sizeof(T), 16) + 1);
+      const int64_t xs_bytes = padding > 0 ? 4 * (2 * padding + 3) * S.e[1] * cells.e[2] : 0;
+      const int64_t lds_plane = nodes_bytes + xs_bytes + 8 * cells.e[1] * cells.e[2] + 8 * mp_pad_words(cells.e[2]);
+      const int64_t nblk_plane = B * (cells.e[0] + 1);
+      if (nsp == 3 && C == 1 && padding <= 2 && lds_plane <= 64 * 1024 && nblk_plane < ((int64_t)1 << 31) &&
+          (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31) &&
+          !std::getenv("KMP_MP_LDS")) {
+        auto launch = [&](auto kern) {
+          kern<<<(unsigned)nblk_plane, kThreads, (size_t)lds_plane, (hipStream_t)stream>>>(
+              (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2], outs,
+              B % 8 == 0 ? (int32_t)(cells.e[0] + 1) : 0, (int32_t)nodes_bytes, (int32_t)xs_bytes);
+          return check_launch("mean_predict_plane");
+        };
+        if (padding == 0) return launch(mean_predict_plane_kernel<T, 0>);
+        if (padding == 1) return launch(mean_predict_plane_kernel<T, 1>);
+        return launch(mean_predict_plane_kernel<T, 2>);
+      }
       if (rows_ok(C, {vol(B, S, C), total}) && padding <= 1) {
         const int32_t XO = (int32_t)std::min<int64_t>(cells.e[2] + 1, 64);
         const int32_t YB = std::max(1, std::min(8, kThreads / XO));

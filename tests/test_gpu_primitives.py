@@ -120,6 +120,33 @@ def test_coders_keep_torch(kom):
     assert int(out.to(torch.int32).sum()) == 0
 
 
+@pytest.mark.parametrize('shape,dtype', [((2, 64, 64, 64, 1), np.uint16), ((3, 17, 9, 22, 1), np.uint8),
+                                         ((1, 5, 41, 7, 1), np.uint16)])
+@pytest.mark.parametrize('padding', [0, 1, 2])
+def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
+    """The LDS-staged mean predictor (one workgroup per output plane; 3D, C == 1) on C3 tiles and
+    ragged windows, against the oracle and the element-gather kernel it replaced (KMP_MP_LDS=1)."""
+    import os
+    hi = _rand(shape, dtype, 11)
+    lo = oracle.volume.lowres_from_highres(oracle.volume.pad_highres(hi)[0])
+    window = oracle.volume.pad_neighborhood(lo, padding)
+    want = oracle.predictors.mean_predictions_fn(padding, 3)(window)
+    runs = {}
+    for env, val, name in ((None, None, 'mean_predict_plane'), ('KMP_MP_LDS', '1', 'mean_predict_maps')):
+        if env:
+            os.environ[env] = val
+        try:
+            runs[(env, val)] = kom.MeanPredictor(padding, 3)(torch.from_numpy(window).cuda())
+            assert kom._lib.lib.kmp_last_launch().decode() == name, env
+        finally:
+            if env:
+                del os.environ[env]
+    for a, b in zip(runs[(None, None)], want):
+        _eq(a, b)
+    for key, got in runs.items():
+        assert all(torch.equal(a, b) for a, b in zip(runs[(None, None)], got)), key
+
+
 @pytest.mark.parametrize('ndim', [3, 2])
 @pytest.mark.parametrize('padding', [0, 1, 2])
 def test_mean_predictor_callable(kom, ndim, padding):

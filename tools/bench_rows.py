@@ -157,12 +157,17 @@ def main():
     if not want or 'volume_callback' in want:
         pred = kom.MeanPredictor(0, 3)
         cb = lambda lowres: pred(lowres)  # noqa: E731  (not recognised as fused: the reference's step sequence)
-        sub = vol[:128]
-        lo, (maps, dims) = V.encode(cb, V.encode_values_uint16, sub)
-        te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), 3)
-        td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), 3)
-        emit('volume_callback:encode', 'callback encode (window, opaque predictions_fn, fused coder + trims)', sub.numel() * 4, te)
-        emit('volume_callback:decode', 'callback decode (window, opaque predictions_fn, fused coder + interleave)', sub.numel() * 4, td)
+        for nt in (512, 128):  # the whole C3 batch (GPU-bound), and 128 tiles (host-bound, ~0.1 ms per call)
+            sub = vol[:nt]
+            lo, (maps, dims) = V.encode(cb, V.encode_values_uint16, sub)
+            te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), 5)
+            td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), 5)
+            tag = 'volume_callback' if nt == 512 else f'volume_callback_{nt}'
+            emit(tag + ':encode', f'callback encode, {nt} tiles (window, opaque predictions_fn, fused coder)',
+                 sub.numel() * 4, te)
+            emit(tag + ':decode', f'callback decode, {nt} tiles (window, opaque predictions_fn, fused coder)',
+                 sub.numel() * 4, td)
+            del lo, maps
 
     # categorical rank coder (utils.py:58-111): 1M elements x 256 float32 logits
     if not want or 'categorical' in want:
@@ -245,10 +250,10 @@ def main():
         pred = kom.MeanPredictor(0, 3)
         gen = torch.Generator(device='cuda').manual_seed(0)
         for noise in (1.0, 4.0, 16.0):
-            vol = (field + noise * torch.randn(field.shape, device='cuda', generator=gen)).round().clamp(0, 65535)
-            tiles = vol.to(torch.int32).to(torch.uint16).view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5) \
+            nvol = (field + noise * torch.randn(field.shape, device='cuda', generator=gen)).round().clamp(0, 65535)
+            tiles = nvol.to(torch.int32).to(torch.uint16).view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5) \
                 .reshape(512, 64, 64, 64, 1).contiguous()
-            del vol
+            del nvol
             lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, tiles)
             raw = tiles.numel() * 2
             b_r = kom.packing.pack_encoded(lo, (maps, dims), 'rice')

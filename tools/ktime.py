@@ -19,6 +19,19 @@ if len(sys.argv) > 4 and sys.argv[4] == 'linear':
     pred = kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim)
 else:
     pred = kom.MeanPredictor(p, ndim)
+if len(sys.argv) > 4 and sys.argv[4] == 'callback':  # the callback path: opaque predictions_fn
+    ns = kom.volume if ndim == 3 else kom.image
+    enc_fn, dec_fn = ((ns.encode_values_uint16, ns.decode_values_uint16) if ndim == 3
+                      else (ns.encode_values_uint8, ns.decode_values_uint8))
+    cb = lambda lowres: pred(lowres)  # noqa: E731
+    lo, enc = ns.encode(cb, enc_fn, hi, padding=p)
+    for _ in range(reps):
+        lo, enc = ns.encode(cb, enc_fn, hi, padding=p)
+        rec = ns.decode(cb, dec_fn, lo, enc, padding=p)
+    torch.cuda.synchronize()
+    assert torch.equal(rec, hi)
+    print('ok', os.environ.get('KMP_TAG', ''))
+    sys.exit(0)
 coder = _nd.NATURAL_CODER[hi.dtype]
 lo, maps, dims = _nd._alloc_encoded(hi, coder, ndim)
 rec = torch.empty_like(hi)
