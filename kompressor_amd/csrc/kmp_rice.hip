@@ -303,27 +303,40 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
 // widths <= W; rice -- k < W, an all-zero block has no payload, a coded block holds its 2k plane
 // words and >= 2 unary words, at most 2W + 2 in all.  The count of violating blocks is read back
 // with the payload length before any unpack kernel runs.
-__global__ void __launch_bounds__(1024) side_check_kernel(int format, int W, const uint8_t* __restrict__ a,
-                                                        const uint8_t* __restrict__ b, int64_t nb,
-                                                        uint64_t* __restrict__ bad_out) {
-  __shared__ uint32_t part[16];
+// Side-information check over all blocks: a thread tests 8 consecutive blocks (one 8-byte load
+// per side array when both are 8-byte aligned), a wave sums its count and adds it to *bad_out
+// (zeroed by the launcher) with one vector atomic when it is non-zero.  Was one 1024-thread
+// workgroup reading a byte per block: 103 us for the 524288 blocks of a 32 MiB u16 map.
+template <bool ALIGNED>
+__global__ void __launch_bounds__(256) side_check_kernel(int format, int W, const uint8_t* __restrict__ a,
+                                                       const uint8_t* __restrict__ b, int64_t nb,
+                                                       unsigned long long* __restrict__ bad_out) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   uint32_t bad = 0;
-  for (int64_t i = threadIdx.x; i < nb; i += 1024) {
-    if (format == 0) {
-      bad += a[i] > W;
+  if (i0 < nb) {
+    uint8_t av[8], bv[8];
+    if (ALIGNED && i0 + 8 <= nb) {
+      *(uint2*)av = *(const uint2*)(a + i0);
+      *(uint2*)bv = format ? *(const uint2*)(b + i0) : make_uint2(0, 0);
     } else {
-      const int k = (int)a[i] - 1, words = b[i];
-      bad += a[i] == 0 ? (words != 0) : (k >= W || words < 2 * k + 2 || words > 2 * W + 2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // past the end: a zero block with no payload, which is valid
+        av[j] = i0 + j < nb ? a[i0 + j] : 0;
+        bv[j] = format && i0 + j < nb ? b[i0 + j] : 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (format == 0) {
+        bad += av[j] > W;
+      } else {
+        const int k = (int)av[j] - 1, words = bv[j];
+        bad += av[j] == 0 ? (words != 0) : (k >= W || words < 2 * k + 2 || words > 2 * W + 2);
+      }
     }
   }
   for (int d = 32; d >= 1; d >>= 1) bad += __shfl_xor(bad, d, 64);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = bad;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int i = 0; i < 16; ++i) t += part[i];
-    *bad_out = t;
-  }
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, (unsigned long long)bad);
 }
 
 }  // namespace rc
@@ -371,8 +384,15 @@ int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const
   KMP_REQUIRE(format == 0 || format == 1, "unpack_check: format must be 0 (planes) or 1 (rice)");
   KMP_REQUIRE(n >= 0 && workspace && (n == 0 || (side_a && (format == 0 || side_b))), "unpack_check: bad argument");
   const int64_t nb = kmp_pack_blocks(n);
-  uint64_t* bad = (uint64_t*)((char*)workspace + kmp_pack_total_offset(n) + 8);
-  rc::side_check_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(format, W, side_a, side_b, nb, bad);
+  unsigned long long* bad = (unsigned long long*)((char*)workspace + kmp_pack_total_offset(n) + 8);
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(bad, 0, sizeof(*bad), s) != hipSuccess) return fail(KMP_ERR_LAUNCH, "unpack_check: memset");
+  if (nb == 0) return KMP_OK;
+  const unsigned grid = (unsigned)ceil_div(nb, (int64_t)8 * 256);
+  if ((((uintptr_t)side_a | (uintptr_t)side_b) & 7) == 0)
+    rc::side_check_kernel<true><<<grid, 256, 0, s>>>(format, W, side_a, side_b, nb, bad);
+  else
+    rc::side_check_kernel<false><<<grid, 256, 0, s>>>(format, W, side_a, side_b, nb, bad);
   return check_launch("unpack_check");
 }
 

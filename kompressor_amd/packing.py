@@ -36,11 +36,6 @@ import struct
 import torch
 
 from . import _device as dev
-import struct
-
-import torch
-
-from . import _device as dev
 from ._lib import check, lib
 
 ARRAY_MAGIC = b'KMPA'
@@ -58,80 +53,71 @@ def _pad8(n):
 
 
 # ---------------------------------------------------------------------------------------------
-# pack: every kernel of an array is launched into a worst-case-sized blob (header and padding
-# written by kernels from arguments); the payload lengths of ALL arrays of a call are then read
-# with ONE host synchronisation (_finish)
+# pack, in two phases so the payloads land in their final place: (1) per array the plan kernels
+# (block widths / Rice parameters + the offset scan) write the side information into a small
+# buffer and the payload length into the workspace; ONE host synchronisation reads every length;
+# (2) the output is allocated at its exact size and every array's header, side information and
+# payload are written straight into it (no concatenation copy of the payloads)
 # ---------------------------------------------------------------------------------------------
 
-class _Pending:
-    """A launched pack: ``out`` holds the blob, whose payload length (``unit``-byte words at
-    header offset 32) is known once the stream reaches it."""
+class _Plan:
+    """Phase 1 of packing one array; ``write`` is phase 2 once the payload length is known."""
 
-    def __init__(self, out, poff, unit, ws):
-        self.out, self.poff, self.unit, self.ws = out, poff, unit, ws
+    def __init__(self, t, method):
+        if method not in METHODS:
+            raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
+        self.t, self.method = t, method
+        self.code, self.n = dev.dtype_code(t), t.numel()
+        self.nb = nb = int(lib.kmp_pack_blocks(self.n))
+        self.ws = dev.empty((int(lib.kmp_pack_workspace_bytes(self.n)),), torch.uint8)
+        self.hlen = _HEAD.size + 8 * t.dim()
+        if method == 'rice':  # params | bw, each padded to 8 bytes
+            self.side = torch.zeros((2 * _pad8(nb),), dtype=torch.uint8, device='cuda')
+            check(lib.kmp_rice_plan(self.code, t.data_ptr(), self.n, self.side.data_ptr(),
+                                    self.side.data_ptr() + _pad8(nb), self.ws.data_ptr(), dev.stream()), 'rice')
+            self.magic, self.unit = RICE_MAGIC, 4
+        else:  # widths, padded to 8 bytes
+            self.side = torch.zeros((_pad8(nb),), dtype=torch.uint8, device='cuda')
+            check(lib.kmp_pack_plan(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
+                                    dev.stream()), 'pack')
+            self.magic, self.unit = ARRAY_MAGIC, 8
+        self.poff = self.hlen + self.side.numel()
 
     def words_view(self):
-        return self.out[32:40].view(torch.int64)
+        off = int(lib.kmp_pack_total_offset(self.n))
+        return self.ws[off:off + 8].view(torch.int64)
 
-    def finish(self, words):
-        used = self.poff + self.unit * words
-        end = _pad8(used)
-        if end > used:
-            self.out[used:end].zero_()
-        return self.out[:end]
+    def size(self, words):
+        return _pad8(self.poff + self.unit * words)
 
-
-def _launch_planes(t):
-    code = dev.dtype_code(t)
-    n = t.numel()
-    nb = int(lib.kmp_pack_blocks(n))
-    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    head = _HEAD.pack(ARRAY_MAGIC, VERSION, code, t.dim(), 0, n, nb, 0) + struct.pack(f'<{t.dim()}q', *t.shape)
-    woff = len(head)
-    poff = woff + _pad8(nb)
-    out = dev.empty((poff + nb * t.element_size() * 64,), torch.uint8)  # every block at full width
-    base = out.data_ptr()
-    check(lib.kmp_pack_plan(code, t.data_ptr(), n, base + woff, ws.data_ptr(), dev.stream()), 'pack')
-    check(lib.kmp_pack(code, t.data_ptr(), n, base + woff, ws.data_ptr(), base + poff, dev.stream()), 'pack')
-    # header + widths padding + the scan's word count (offset 32), from kernel arguments
-    check(lib.kmp_pack_header(base, head, len(head), woff + nb, poff, ws.data_ptr(), n, 32, dev.stream()), 'pack')
-    return _Pending(out, poff, 8, ws)
+    def write(self, dst, words):
+        """Header, side information and payload into the device byte view ``dst`` (``size`` bytes)."""
+        t, used = self.t, self.poff + self.unit * words
+        head = _HEAD.pack(self.magic, VERSION, self.code, t.dim(), 0, self.n, self.nb, words)
+        head += struct.pack(f'<{t.dim()}q', *t.shape)
+        base = dst.data_ptr()
+        check(lib.kmp_pack_header(base, head, len(head), used, dst.numel(), None, 0, -1, dev.stream()), 'pack')
+        dst[self.hlen:self.poff].copy_(self.side)
+        if self.method == 'rice':
+            check(lib.kmp_rice_pack(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
+                                    base + self.poff, dev.stream()), 'rice')
+        else:
+            check(lib.kmp_pack(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
+                               base + self.poff, dev.stream()), 'pack')
 
 
-def _launch_rice(t):
-    code = dev.dtype_code(t)
-    n = t.numel()
-    nb = int(lib.kmp_pack_blocks(n))
-    bits = _SAMPLE_BITS[t.element_size()]
-    ws = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    head = _HEAD.pack(RICE_MAGIC, VERSION, code, t.dim(), 0, n, nb, 0) + struct.pack(f'<{t.dim()}q', *t.shape)
-    aoff = len(head)
-    boff = aoff + _pad8(nb)
-    poff = boff + _pad8(nb)
-    out = dev.empty((poff + _pad8(4 * nb * (2 * bits + 2)),), torch.uint8)  # every block at its largest
-    base = out.data_ptr()
-    check(lib.kmp_rice_plan(code, t.data_ptr(), n, base + aoff, base + boff, ws.data_ptr(), dev.stream()), 'rice')
-    check(lib.kmp_rice_pack(code, t.data_ptr(), n, base + aoff, ws.data_ptr(), base + poff, dev.stream()), 'rice')
-    check(lib.kmp_pack_header(base, b'', 0, aoff + nb, boff, None, 0, -1, dev.stream()), 'rice')
-    check(lib.kmp_pack_header(base, head, len(head), boff + nb, poff, ws.data_ptr(), n, 32, dev.stream()), 'rice')
-    return _Pending(out, poff, 4, ws)
+def _plan_all(arrays, method):
+    """Phase 1 for every array, then the ONE synchronisation: (plans, payload words)."""
+    plans = [_Plan(dev.to_device(a)[0].contiguous(), method) for a in arrays]
+    words = torch.cat([p.words_view() for p in plans]).tolist() if plans else []
+    return plans, words
 
 
-def _launch(t, method):
-    t = t.contiguous()
-    if method == 'rice':
-        return _launch_rice(t)
-    if method == 'planes':
-        return _launch_planes(t)
-    raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
-
-
-def _finish(pending):
-    """The blobs of launched packs: ONE host synchronisation for all their payload lengths."""
-    if not pending:
-        return []
-    words = torch.cat([p.words_view() for p in pending]).tolist()
-    return [p.finish(w) for p, w in zip(pending, words)]
+def _write_bytes(dst, data):
+    """Host bytes into the device byte view ``dst`` through the header kernel (no host copy sync)."""
+    for i in range(0, len(data), 128):
+        chunk = data[i:i + 128]
+        check(lib.kmp_pack_header(dst.data_ptr() + i, chunk, len(chunk), 0, 0, None, 0, -1, dev.stream()), 'pack')
 
 
 # ---------------------------------------------------------------------------------------------
@@ -240,7 +226,10 @@ def _unpack_many(b, spans):
 def pack(x, method='rice'):
     """Pack one array (uint8 / uint16 / int32 / uint32 / float32 samples) into a blob."""
     t, kind = dev.to_device(x)
-    return dev.from_device(_finish([_launch(t, method)])[0], kind)
+    (plan,), (words,) = _plan_all([t], method)
+    out = dev.empty((plan.size(words),), torch.uint8)
+    plan.write(out, words)
+    return dev.from_device(out, kind)
 
 
 def unpack(blob):
@@ -251,18 +240,24 @@ def unpack(blob):
 
 def pack_encoded(lowres, encoded, method='rice'):
     """One blob for an ``encode`` result ``(lowres, (maps, dims))`` (any number of maps; ``dims``
-    may be empty): every array's kernels are launched first, then ONE synchronisation."""
+    may be empty): every array's plan kernels, ONE synchronisation, then every array written in
+    place."""
     maps, dims = encoded
     kind = 'torch' if isinstance(lowres, torch.Tensor) else 'numpy'
-    blobs = _finish([_launch(dev.to_device(a)[0], method) for a in (lowres, *maps)])
+    plans, words = _plan_all((lowres, *maps), method)
+    sizes = [p.size(w) for p, w in zip(plans, words)]
     nsp = len(dims)
-    head = struct.pack('<4sHHI', BUNDLE_MAGIC, VERSION, len(blobs), nsp)
+    head = struct.pack('<4sHHI', BUNDLE_MAGIC, VERSION, len(plans), nsp)
     head += struct.pack(f'<{nsp}i', *[int(d) for d in dims])
     head += b'\0' * (_pad8(len(head)) - len(head))
-    head += struct.pack(f'<{len(blobs)}q', *[int(bl.numel()) for bl in blobs])
-    parts = [torch.frombuffer(bytearray(head), dtype=torch.uint8).to('cuda', non_blocking=False)]
-    parts += blobs  # every blob is already a multiple of 8 bytes
-    return dev.from_device(torch.cat(parts), kind)
+    head += struct.pack(f'<{len(plans)}q', *sizes)  # every blob is a multiple of 8 bytes
+    out = dev.empty((len(head) + sum(sizes),), torch.uint8)
+    _write_bytes(out, head)
+    off = len(head)
+    for p, w, sz in zip(plans, words, sizes):
+        p.write(out[off:off + sz], w)
+        off += sz
+    return dev.from_device(out, kind)
 
 
 def unpack_encoded(blob):
