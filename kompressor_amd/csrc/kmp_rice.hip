@@ -219,7 +219,10 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
                                                         const uint64_t* __restrict__ cbase, int64_t nb,
                                                         void* __restrict__ out) {
   constexpr int NP = Sw<W>::NP;
+  constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave step's 8 blocks, at most
+  __shared__ uint32_t span_lds[4][SPAN];
   const int lane = threadIdx.x & 63, j = lane & 7;
+  uint32_t* const wspan = span_lds[(threadIdx.x >> 6) & 3];
   const int64_t nstep = (nb + 7) / 8;
   for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
        st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
@@ -228,9 +231,24 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
     uint64_t off = 0;
     if (blk < nb) {
       param = params[blk];
-      words = bw[blk];
+      words = min((int)bw[blk], 2 * W + 2);  // a corrupt bw never steers a read past the span
       off = cbase[blk / kChunk] + local[blk];
     }
+    // the step's 8 blocks are consecutive in the payload: stage their words [start, end) in LDS
+    // with coalesced loads, so the low planes and the unary walk below read LDS, not memory
+    const uint64_t start = __shfl(off, 0, 64);
+    uint64_t end = blk < nb ? off + (uint64_t)words : start;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint64_t o = __shfl_xor(end, d, 64);
+      end = o > end ? o : end;
+    }
+    const int cnt = (int)min<uint64_t>(end - start, (uint64_t)SPAN);
+    for (int i = lane; i < cnt; i += 64) wspan[i] = payload[start + i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t* const bp = wspan + (off - start);  // this lane's block in LDS
     const int k = param > 0 ? min(param - 1, W - 1) : 0;
     const int uw = param > 0 ? max(words - 2 * k, 0) : 0;  // a corrupt bw never steers a read past the block
     // low bits: planes 8p + j < k, transposed back to the lane's 8 samples
@@ -239,8 +257,8 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
     for (int p = 0; p < NP; ++p) {
       const int b = 8 * p + j;
       const bool have = param > 0 && b < k && 2 * b + 1 < words;
-      Z[p][0] = have ? payload[off + 2 * b] : 0u;
-      Z[p][1] = have ? payload[off + 2 * b + 1] : 0u;
+      Z[p][0] = have ? bp[2 * b] : 0u;
+      Z[p][1] = have ? bp[2 * b + 1] : 0u;
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -250,7 +268,7 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
     uint32_t lowv[Sw<W>::NW];
     scatter_bytes<W>(Z, lowv);
     // unary part: start after terminator 8j - 1, then 8 quotients by ctz
-    const uint32_t* us = payload + off + 2 * k;
+    const uint32_t* us = bp + 2 * k;
     uint32_t q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = 0u;
@@ -296,6 +314,9 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
       set_sample<W>(wout, e, unzigzag<W>(z));
     }
     store8s<W>(out, n, st * 512 + (int64_t)lane * 8, wout);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();  // the next step's staging must not overtake these reads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
 }
 
