@@ -38,6 +38,7 @@ struct W3P {
   int32_t nslab, zbegin, zend;
   int32_t txn, rows, nwv, nyg;
   int32_t xcd_per;  // > 0: tile-per-XCD block order (blocks per tile), 0: identity
+  int32_t zrun;     // wave3dr_kernel: output planes per workgroup (even)
 };
 
 template <bool DEC>
@@ -314,6 +315,295 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 }
 
+// ---- z-rolling variant: a workgroup owns a run of ZR consecutive output planes of one tile and
+// keeps the z box sums of its rows in registers.  Going from cell plane m-1 to m adds node plane
+// m+P+1 and subtracts node plane m-1-P (integer sums: exact), so each output plane loads 2 node
+// rows per lane (plus the halo rows) instead of 2P+3, and the loads of output plane c+1 are issued
+// before plane c is computed.  The x / y sums, the means, the 19-way aggregation and the coder
+// are the plane-block kernel's above.
+template <bool DEC>
+struct RollStep {
+  typename NodeRow<DEC>::V add_own, add_halo, sub_own, sub_halo, cur;  // cur: node plane c's own row
+  OutRows o;
+};
+
+template <typename T, bool DEC, int P>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 3 : 1)))
+wave3dr_kernel(W3P a) {
+  constexpr int PD = 1;  // prefetch distance in output planes (2 measured no faster: r2ar)
+  constexpr int VX = 8 / (int)sizeof(T);
+  constexpr int NB = 2 * P + 2;
+  constexpr uint32_t NN = NB * NB * NB;
+  constexpr int NE = VX + 2 * P + 1;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  using V = typename NodeRow<DEC>::V;
+
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int tx = lane % a.txn;
+  const int r = lane / a.txn;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int yg = blk % a.nyg;
+  blk /= a.nyg;
+  const int pb = blk % a.nslab;
+  const int64_t b = blk / a.nslab;
+  const int Y0 = (yg * a.nwv + wv) * a.rows;
+  if (Y0 >= a.Ey) return;
+  const int Y = Y0 + r;
+  const bool live = Y < a.Ey;
+  const int c0 = a.zbegin + pb * a.zrun;
+  const int Z1 = a.zend;
+  const int c1 = c0 + a.zrun < Z1 ? c0 + a.zrun : Z1;
+  const int rows = a.rows;
+
+  const int ysrc = live ? Y : lsrc(Y, a.Ly, a.Ey);
+  const bool hup = r <= P, hdn = r >= rows - P - 1;
+  const int hrow = hup ? Y0 - P - 1 + r : Y0 + rows + (r - (rows - P - 1));
+  const int hsrc = lsrc(hrow, a.Ly, a.Ey);
+  const bool has_halo = hup || hdn;
+  const bool vy1 = Y < a.Lcy;
+  const bool vy0 = Y >= 1;
+  const bool xfirst = tx == 0, xlast = tx == a.txn - 1;
+  const bool xdims = a.Lx != a.Ex;
+
+  const int hplane = a.H * a.W;
+  const int lplane = a.Ey * a.Ex;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
+  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
+  const int hx = 2 * X;
+  const int ho_own = 2 * ysrc * a.W + hx, ho_halo = 2 * hsrc * a.W + hx;
+  const int lo_own = ysrc * a.Ex + X, lo_halo = hsrc * a.Ex + X;
+
+  const T* mbase[7];
+  int mplane[7];
+  bool mok_y[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    int par[3];
+    map_parity(3, k, par);
+    const int ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
+    mplane[k] = ey * a.Ex;
+    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + (live ? Y : 0) * a.Ex + X;
+    mok_y[k] = live && (!par[1] || vy1);
+  }
+
+  auto load_node = [&](int t, V& own, V& halo) __attribute__((always_inline)) {
+    const int sz = lsrc(t, a.Lz, a.Ez);
+    if constexpr (DEC) {
+      const T* p = lin + sz * lplane;
+      own = ld8c(p + lo_own);
+      halo = has_halo ? ld8c(p + lo_halo) : V{};
+    } else {
+      const T* p = hin + 2 * sz * hplane;
+      own = ld16c(p + ho_own);
+      halo = has_halo ? ld16c(p + ho_halo) : V{};
+    }
+  };
+  auto load_out = [&](int q, OutRows& O) __attribute__((always_inline)) {
+    O = OutRows{};
+    const bool vz1 = q < a.Lcz;
+    if constexpr (DEC) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        int par[3];
+        map_parity(3, k, par);
+        if (mok_y[k] && (!par[0] || vz1)) O.mv[k] = ld8(mbase[k] + q * mplane[k]);
+      }
+    } else {
+      const T* p = hin + 2 * q * hplane;
+      if (live && vy1) O.e1 = ld16(p + ho_own + a.W);
+      if (live && vz1) O.o0 = ld16(p + hplane + ho_own);
+      if (live && vz1 && vy1) O.o1 = ld16(p + hplane + ho_own + a.W);
+    }
+  };
+  // step for output plane c: add node plane c+P+1, subtract c-1-P (the z sums move from cell
+  // plane c-1 to c), node plane c's own row (the lowres / X map samples), the stream rows
+  auto load_step = [&](int c, RollStep<DEC>& S) __attribute__((always_inline)) {
+    load_node(c + P + 1, S.add_own, S.add_halo);
+    load_node(c - 1 - P, S.sub_own, S.sub_halo);
+    if constexpr (DEC) S.cur = ld8c(lin + c * lplane + lo_own);
+    else S.cur = ld16c(hin + 2 * c * hplane + ho_own);
+    load_out(c, S.o);
+  };
+
+  // z sums of cell plane c0-1 (node planes c0-1-P .. c0+P): the prologue's 2P+2 planes
+  uint32_t zo[VX], zh[VX];
+#pragma unroll
+  for (int i = 0; i < VX; ++i) zo[i] = zh[i] = 0;
+  RollStep<DEC> S[PD + 1];
+  {
+    V own[NB], halo[NB];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) load_node(c0 - 1 - P + t, own[t], halo[t]);
+#pragma unroll
+    for (int k = 0; k < PD; ++k)
+      if (c0 + k < c1) load_step(c0 + k, S[k]);
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        zo[i] += node_el<T, DEC>(own[t], i);
+        zh[i] += node_el<T, DEC>(halo[t], i);
+      }
+  }
+
+  auto xbox = [&](const uint32_t (&z)[VX], uint32_t (&out)[VX]) __attribute__((always_inline)) {
+    uint32_t e[NE];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const uint32_t s = shup(z[VX - P + k], 1);
+      e[k] = xfirst ? z[P - 1 - k] : s;
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) e[P + i] = z[i];
+#pragma unroll
+    for (int k = 0; k <= P; ++k) {
+      const uint32_t s = shdn(z[k], 1);
+      e[P + VX + k] = xlast ? (xdims ? z[VX - 1] : z[VX - 1 - k]) : s;
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += e[i + k];
+      out[i] = acc;
+    }
+  };
+  // cell means of the cell plane whose z sums are zo / zh, rows Y (Mo) and Y-1 (Ma)
+  auto cell_means = [&](uint32_t (&Mo)[VX + 1], uint32_t (&Ma)[VX + 1]) __attribute__((always_inline)) {
+    uint32_t xo[VX], xh[VX];
+    xbox(zo, xo);
+    xbox(zh, xh);
+    uint32_t so[VX], su[VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) so[i] = su[i] = 0;
+#pragma unroll
+    for (int d = -P - 1; d <= P + 1; ++d) {
+      const int j = r + d;
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        uint32_t v = d == 0 ? xo[i] : (d < 0 ? shup(xo[i], -d * a.txn) : shdn(xo[i], d * a.txn));
+        if (d < 0) {
+          const uint32_t h = d == -P - 1 ? xh[i] : shdn(xh[i], (d + P + 1) * a.txn);
+          v = j < 0 ? h : v;
+        } else if (d > 0) {
+          const uint32_t h = d == P + 1 ? xh[i] : shup(xh[i], (P + 1 - d) * a.txn);
+          v = j >= rows ? h : v;
+        }
+        if (d >= -P) so[i] += v;
+        if (d <= P) su[i] += v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      Mo[i + 1] = so[i] / NN;
+      Ma[i + 1] = su[i] / NN;
+    }
+    Mo[0] = shup(Mo[VX], 1);
+    Ma[0] = shup(Ma[VX], 1);
+  };
+  uint32_t Mo[2][VX + 1], Ma[2][VX + 1];  // [0]: cell plane c-1, [1]: cell plane c
+  cell_means(Mo[0], Ma[0]);
+
+  bool vx[VX + 1];
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+
+  // one output plane: Sc holds its loads; plane c+PD's loads go into Sn first
+  auto step = [&](int c, RollStep<DEC>& Sc, RollStep<DEC>& Sn) __attribute__((always_inline)) {
+    if (c + PD < c1) load_step(c + PD, Sn);  // in flight during planes c .. c+PD-1
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      zo[i] += node_el<T, DEC>(Sc.add_own, i) - node_el<T, DEC>(Sc.sub_own, i);
+      zh[i] += node_el<T, DEC>(Sc.add_halo, i) - node_el<T, DEC>(Sc.sub_halo, i);
+    }
+    cell_means(Mo[1], Ma[1]);  // all lanes (shuffles)
+    if (live) {
+      const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+      uint32_t M[2][2][VX + 1];
+#pragma unroll
+      for (int q = 0; q <= VX; ++q) {
+        M[0][0][q] = (vz0 && vy0 && vx[q]) ? Ma[0][q] : 0u;
+        M[0][1][q] = (vz0 && vy1 && vx[q]) ? Mo[0][q] : 0u;
+        M[1][0][q] = (vz1 && vy0 && vx[q]) ? Ma[1][q] : 0u;
+        M[1][1][q] = (vz1 && vy1 && vx[q]) ? Mo[1][q] : 0u;
+      }
+      const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+      uint32_t pred[7][VX];  // LR, UD, FB, C, Z, Y, X
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pred[0][i] = (M[1][1][i] + M[1][1][i + 1]) >> (nx >> 1);
+        pred[1][i] = (M[1][0][i + 1] + M[1][1][i + 1]) >> (ny >> 1);
+        pred[2][i] = (M[0][1][i + 1] + M[1][1][i + 1]) >> (nz >> 1);
+        pred[3][i] = M[1][1][i + 1];
+        pred[4][i] = (M[1][0][i] + M[1][0][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((ny * nx) >> 1);
+        pred[5][i] = (M[0][1][i] + M[0][1][i + 1] + M[1][1][i] + M[1][1][i + 1]) >> ((nz * nx) >> 1);
+        pred[6][i] = (M[0][0][i + 1] + M[0][1][i + 1] + M[1][0][i + 1] + M[1][1][i + 1]) >> ((nz * ny) >> 1);
+      }
+      const OutRows& Oc = Sc.o;
+      if constexpr (!DEC) {
+        const uint4 own = Sc.cur;
+        uint32_t res[7][VX], lov[VX];
+#pragma unroll
+        for (int i = 0; i < VX; ++i) {
+          lov[i] = el16<T>(own, 2 * i);
+          res[0][i] = (el16<T>(Oc.o1, 2 * i) - pred[0][i]) & MASK;      // LR (1,1,0)
+          res[1][i] = (el16<T>(Oc.o0, 2 * i + 1) - pred[1][i]) & MASK;  // UD (1,0,1)
+          res[2][i] = (el16<T>(Oc.e1, 2 * i + 1) - pred[2][i]) & MASK;  // FB (0,1,1)
+          res[3][i] = (el16<T>(Oc.o1, 2 * i + 1) - pred[3][i]) & MASK;  // C  (1,1,1)
+          res[4][i] = (el16<T>(Oc.o0, 2 * i) - pred[4][i]) & MASK;      // Z  (1,0,0)
+          res[5][i] = (el16<T>(Oc.e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
+          res[6][i] = (el16<T>(own, 2 * i + 1) - pred[6][i]) & MASK;    // X  (0,0,1)
+        }
+        st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          int par[3];
+          map_parity(3, k, par);
+          if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+        }
+      } else {
+        const uint2 own = Sc.cur;
+        uint32_t lov[VX], dv[7][VX];
+#pragma unroll
+        for (int i = 0; i < VX; ++i) lov[i] = el8<T>(own, i);
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+#pragma unroll
+          for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(Oc.mv[k], i)) & MASK;
+        T* h0 = hout + 2 * c * hplane + ho_own;
+        st16(h0, pack16<T, VX>(lov, dv[6]));
+        if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[5], dv[2]));
+        if (vz1) {
+          T* h1 = h0 + hplane;
+          st16(h1, pack16<T, VX>(dv[4], dv[1]));
+          if (vy1) st16(h1 + a.W, pack16<T, VX>(dv[0], dv[3]));
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q <= VX; ++q) {
+      Mo[0][q] = Mo[1][q];
+      Ma[0][q] = Ma[1][q];
+    }
+  };
+  // PD+1 planes per iteration so the step buffers are addressed statically (no register indexing)
+#pragma unroll 1
+  for (int c = c0; c < c1; c += PD + 1) {
+#pragma unroll
+    for (int k = 0; k <= PD; ++k)
+      if (c + k < c1) step(c + k, S[k], S[(k + PD) % (PD + 1)]);
+  }
+}
+
 }  // namespace w3p
 
 // ------------------------------------------------------------------------------------------
@@ -374,6 +664,21 @@ static bool wave3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   return nblk < ((int64_t)1 << 31);
 }
 
+// z-rolling kernel (wave3dr_kernel): the z run per workgroup in output planes, 0 = the plane-block
+// kernel.  Default: runs of 8 for p = 2 with 16-bit samples (C3: 151 / 127 -> 124 / 108 us per
+// direction, profiles/round2/ab_wave3dr.log); the plane-block kernel stays faster for p = 1 (91 /
+// 91 vs 112 / 106) and for 8-bit samples the rolling form is untuned.  KMP_W3P_ROLL overrides.
+static int w3p_roll(int P, int bytes) {
+  const int zr = w3p_env("KMP_W3P_ROLL", P == 2 && bytes == 2 ? 8 : 0);
+  return zr >= 2 ? (zr + 1) / 2 * 2 : 0;
+}
+
+template <typename T, bool DEC>
+static void launch_wave3dr(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
+  if (P == 1) w3p::wave3dr_kernel<T, DEC, 1><<<grid, block, 0, stream>>>(a);
+  else w3p::wave3dr_kernel<T, DEC, 2><<<grid, block, 0, stream>>>(a);
+}
+
 template <typename T, bool DEC>
 static void launch_wave3dp(int P, int pl, int wpe, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
   if (P == 1) {
@@ -403,13 +708,19 @@ int try_wave3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
     dim3 grid, block;
     int pl, wpe;
     w3p_cfg(pred->padding, false, pl, wpe);
-    if (!wave3dp_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    const int zr = w3p_roll(pred->padding, (int)sizeof(T));
+    if (!wave3dp_geometry<T>(g, B, C, pred, region, zr ? zr : pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
+    if (zr) {
+      a.zrun = zr;
+      launch_wave3dr<T, false>(pred->padding, grid, block, stream, a);
+      return check_launch("wave3dr_encode");
+    }
     launch_wave3dp<T, false>(pred->padding, pl, wpe, grid, block, stream, a);
     return check_launch("wave3dp_encode");
   }
@@ -424,7 +735,8 @@ int try_wave3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
     dim3 grid, block;
     int pl, wpe;
     w3p_cfg(pred->padding, true, pl, wpe);
-    if (!wave3dp_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    const int zr = w3p_roll(pred->padding, (int)sizeof(T));
+    if (!wave3dp_geometry<T>(g, B, C, pred, region, zr ? zr : pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -432,6 +744,11 @@ int try_wave3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
     }
     a.hi_out = hi;
     a.lo_in = lowres;
+    if (zr) {
+      a.zrun = zr;
+      launch_wave3dr<T, true>(pred->padding, grid, block, stream, a);
+      return check_launch("wave3dr_decode");
+    }
     launch_wave3dp<T, true>(pred->padding, pl, wpe, grid, block, stream, a);
     return check_launch("wave3dp_decode");
   }

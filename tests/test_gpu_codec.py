@@ -318,13 +318,20 @@ def _last_launch(kom):
     ((2, 7, 5, 32, 1), np.uint16, 2),      # odd height, rows beyond the volume
     ((1, 64, 64, 64, 1), np.uint16, 2),
 ])
-@pytest.mark.parametrize('pl', [None, '1', '2'])
+@pytest.mark.parametrize('pl', [None, '1', '2', 'roll8', 'roll16'])
 def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
-    """The p = 1, 2 wave kernel (kmp_codec_wave3dp.hip) against the oracle, encode and decode, and
-    chunked (z-region) launches, at the default and both forced planes-per-workgroup; asserts the
-    kernel served the call."""
-    if pl is not None:
+    """The p = 1, 2 wave kernels (kmp_codec_wave3dp.hip) against the oracle, encode and decode, and
+    chunked (z-region) launches: the plane-block kernel at the default and both forced
+    planes-per-workgroup, and the z-rolling kernel with runs of 8 and 16 planes (KMP_W3P_ROLL);
+    asserts the kernel served the call."""
+    kernel = 'wave3dr' if p == 2 and dtype == np.uint16 else 'wave3dp'  # the default per (p, dtype)
+    if pl is not None and pl.startswith('roll'):
+        monkeypatch.setenv('KMP_W3P_ROLL', pl[4:])
+        kernel = 'wave3dr'
+    elif pl is not None:
         monkeypatch.setenv('KMP_W3P_PL', pl)
+        monkeypatch.setenv('KMP_W3P_ROLL', '0')
+        kernel = 'wave3dp'
     import oracle
     from oracle import predictors as OP
     ns, ons = kom.volume, oracle.volume
@@ -334,13 +341,13 @@ def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
     want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, 3), oenc, x, padding=p)
     pred = kom.MeanPredictor(p, 3)
     lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
-    assert _last_launch(kom) == 'wave3dp_encode'
+    assert _last_launch(kom) == kernel + '_encode'
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, b) in enumerate(zip(maps, want_maps)):
         bad = np.argwhere(a != b)
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
     assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
-    assert _last_launch(kom) == 'wave3dp_decode'
+    assert _last_launch(kom) == kernel + '_decode'
     lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(5, 7, 9), padding=p), x)
