@@ -33,6 +33,7 @@ struct W2P {
   int32_t xcd_per;
   int32_t ybeg, yend;
   int32_t wbase;  // first wave (of rows rows) the launch covers
+  int32_t rrun;   // wave2dr_kernel: output rows per wave (a multiple of rows)
 };
 
 template <typename T, bool DEC, int P>
@@ -223,6 +224,218 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
   }
 }
 
+// ---- y-rolling variant: a wave owns a run of a.rrun consecutive output rows (steps of ``rows``
+// rows, full width) instead of one row group.  The x box sums of a step's node rows are computed
+// once and serve three steps: as the current rows, as the previous step's rows (the p+1 rows
+// above come from them by one shuffle instead of a halo load) and as the next step's rows (the
+// p+1 rows below).  So a step loads one node row and its output rows per lane, against the
+// plane-group kernel's node row + up to two halo rows; the node rows of step s+2 and the output
+// rows of step s+1 are in flight while step s computes.
+template <typename T, bool DEC, int P>
+__global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  constexpr int NB = 2 * P + 2;
+  constexpr uint32_t NN = NB * NB;
+  constexpr int NE = VX + 2 * P + 1;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+  constexpr bool SWAR = sizeof(T) == 1;
+  constexpr int VW = SWAR ? VX / 2 : VX;
+
+  const int lane = threadIdx.x & 63;
+  const int wv_ = threadIdx.x >> 6;
+  const int tx = lane % a.txn;
+  const int r = lane / a.txn;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int grp = blk % a.ngrp;
+  const int64_t b = blk / a.ngrp;
+  const int rows = a.rows;
+  const int Ys = a.ybeg + (grp * a.nwv + wv_) * a.rrun;  // first row of this wave's run
+  if (Ys >= a.yend) return;  // whole idle wave
+  const int Ye = Ys + a.rrun < a.yend ? Ys + a.rrun : a.yend;
+  const bool xfirst = tx == 0, xlast = tx == a.txn - 1;
+  const bool xdims = a.Lx != a.Ex;
+  const int64_t himg = (int64_t)a.H * a.W;
+  const int hx = 2 * X;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * himg;
+  T* hout = DEC ? (T*)a.hi_out + b * himg : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
+
+  auto load_node = [&](int y0) __attribute__((always_inline)) {  // node row y0 + r (mirrored past the ends)
+    const int y = lsrc(y0 + r, a.Ly, a.Ey);
+    if constexpr (DEC) return (V)ld8c(lin + y * a.Ex + X);
+    else return (V)ld16c(hin + 2 * y * a.W + hx);
+  };
+  struct Out {
+    uint4 o0;
+    uint2 mv[3];
+  };
+  auto load_out = [&](int y0, Out& O) __attribute__((always_inline)) {
+    const int Y = y0 + r;
+    const bool live = Y < a.Ey && Y < Ye, vy1 = Y < a.Lcy;
+    const int Yc = live ? Y : 0;
+    O.o0 = make_uint4(0, 0, 0, 0);
+    O.mv[0] = O.mv[1] = O.mv[2] = make_uint2(0, 0);
+    if constexpr (DEC) {
+      const int64_t m_lr = (b * a.Lcy + Yc) * a.Ex + X, m_ud = (b * a.Ey + Yc) * a.Ex + X;
+      if (live && vy1) O.mv[0] = ld8((const T*)a.maps.p[0] + m_lr);
+      if (live) O.mv[1] = ld8((const T*)a.maps.p[1] + m_ud);
+      if (live && vy1) O.mv[2] = ld8((const T*)a.maps.p[2] + m_lr);
+    } else {
+      if (live && vy1) O.o0 = ld16(hin + (2 * Y + 1) * a.W + hx);
+    }
+  };
+  auto nodes = [&](const V& v, uint32_t (&n)[VX]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      if constexpr (DEC) n[i] = el8<T>(v, i);
+      else n[i] = el16<T>(v, 2 * i);
+    }
+  };
+  // x box sums of a node row, SWAR-packed for 8-bit samples (sums < 2^16)
+  auto xpack = [&](const V& v, uint32_t (&pk)[VW]) __attribute__((always_inline)) {
+    uint32_t z[VX], out[VX];
+    nodes(v, z);
+    uint32_t e[NE];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const uint32_t s = shup(z[VX - P + k], 1);
+      e[k] = xfirst ? z[P - 1 - k] : s;
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) e[P + i] = z[i];
+#pragma unroll
+    for (int k = 0; k <= P; ++k) {
+      const uint32_t s = shdn(z[k], 1);
+      e[P + VX + k] = xlast ? (xdims ? z[VX - 1] : z[VX - 1 - k]) : s;
+    }
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += e[i + k];
+      out[i] = acc;
+    }
+#pragma unroll
+    for (int w = 0; w < VW; ++w) pk[w] = SWAR ? (out[2 * w] | out[2 * w + 1] << 16) : out[w];
+  };
+
+  // pipeline: x sums of the previous and current steps, node rows of the next step, output rows
+  uint32_t pprev[VW], pcur[VW];
+  V own = load_node(Ys), vnext = load_node(Ys + rows);
+  Out Ocur, Onext;
+  load_out(Ys, Ocur);
+  xpack(load_node(Ys - rows), pprev);
+  xpack(own, pcur);
+
+#pragma unroll 1
+  for (int Y0 = Ys; Y0 < Ye; Y0 += rows) {
+    const bool more = Y0 + rows < Ye;
+    const V vnn = more ? load_node(Y0 + 2 * rows) : V{};  // step s+2's node rows
+    if (more) load_out(Y0 + rows, Onext);
+    uint32_t pnext[VW];
+    xpack(vnext, pnext);
+    // the p+1 rows above / below the step: previous step's last rows, next step's first rows
+    uint32_t pu[VW], pd[VW];
+#pragma unroll
+    for (int w = 0; w < VW; ++w) {
+      pu[w] = shdn(pprev[w], (rows - P - 1) * a.txn);
+      pd[w] = shup(pnext[w], (rows - P - 1) * a.txn);
+    }
+    uint32_t so[VW], su[VW];
+#pragma unroll
+    for (int w = 0; w < VW; ++w) so[w] = su[w] = 0;
+#pragma unroll
+    for (int d = -P - 1; d <= P + 1; ++d) {
+      const int j = r + d;
+#pragma unroll
+      for (int w = 0; w < VW; ++w) {
+        uint32_t v = d == 0 ? pcur[w] : (d < 0 ? shup(pcur[w], -d * a.txn) : shdn(pcur[w], d * a.txn));
+        if (d < 0) {
+          const uint32_t h = d == -P - 1 ? pu[w] : shdn(pu[w], (d + P + 1) * a.txn);
+          v = j < 0 ? h : v;
+        } else if (d > 0) {
+          const uint32_t h = d == P + 1 ? pd[w] : shup(pd[w], (P + 1 - d) * a.txn);
+          v = j >= rows ? h : v;
+        }
+        if (d >= -P) so[w] += v;
+        if (d <= P) su[w] += v;
+      }
+    }
+    uint32_t M1[VX + 1], M0[VX + 1];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t o = SWAR ? (so[i / 2] >> (16 * (i & 1))) & 0xffffu : so[i];
+      const uint32_t u = SWAR ? (su[i / 2] >> (16 * (i & 1))) & 0xffffu : su[i];
+      M1[i + 1] = o / NN;
+      M0[i + 1] = u / NN;
+    }
+    M1[0] = shup(M1[VX], 1);
+    M0[0] = shup(M0[VX], 1);
+
+    const int Y = Y0 + r;
+    if (Y < a.Ey && Y < Ye) {
+      const bool vy1 = Y < a.Lcy, vy0 = Y >= 1;
+      bool vx[VX + 1];
+#pragma unroll
+      for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+      const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
+#pragma unroll
+      for (int q = 0; q <= VX; ++q) {
+        M1[q] = (vy1 && vx[q]) ? M1[q] : 0u;
+        M0[q] = (vy0 && vx[q]) ? M0[q] : 0u;
+      }
+      uint32_t pred[3][VX];  // LR, UD, C
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pred[0][i] = (M1[i] + M1[i + 1]) >> (nx >> 1);
+        pred[1][i] = (M0[i + 1] + M1[i + 1]) >> (ny >> 1);
+        pred[2][i] = M1[i + 1];
+      }
+      uint32_t n[VX];
+      nodes(own, n);
+      const int64_t m_lr = (b * a.Lcy + Y) * a.Ex + X, m_ud = (b * a.Ey + Y) * a.Ex + X;
+      if constexpr (!DEC) {
+        uint32_t res[3][VX];
+#pragma unroll
+        for (int i = 0; i < VX; ++i) {
+          res[0][i] = (el16<T>(Ocur.o0, 2 * i) - pred[0][i]) & MASK;      // LR (1,0)
+          res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;      // UD (0,1)
+          res[2][i] = (el16<T>(Ocur.o0, 2 * i + 1) - pred[2][i]) & MASK;  // C  (1,1)
+        }
+        st8((T*)a.lo_out + m_ud, pack8<T, VX>(n));
+        if (vy1) st8((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
+        st8((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
+        if (vy1) st8((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+      } else {
+        uint32_t dv[3][VX];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(Ocur.mv[k], i)) & MASK;
+        T* h0 = hout + 2 * Y * a.W + hx;
+        st16(h0, pack16<T, VX>(n, dv[1]));
+        if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[0], dv[2]));
+      }
+    }
+    // slide the pipeline by one step
+#pragma unroll
+    for (int w = 0; w < VW; ++w) {
+      pprev[w] = pcur[w];
+      pcur[w] = pnext[w];
+    }
+    own = vnext;
+    vnext = vnn;
+    Ocur = Onext;
+  }
+}
+
 }  // namespace w2p
 
 static int w2p_env(const char* name, int dflt) {
@@ -230,9 +443,18 @@ static int w2p_env(const char* name, int dflt) {
   return v ? std::atoi(v) : dflt;
 }
 
+// y-rolling kernel (wave2dr_kernel): output rows per wave, 0 = the row-group kernel; rounded up to
+// a multiple of the wave's rows.  Default 32 (C2 p = 1: 33.5 / 31.4 -> 28.4 / 28.1 us per
+// direction, profiles/round2/ab_wave2dr.log).  KMP_W2R_RUN overrides.
+static int w2p_run(int P, int bytes) {
+  (void)P;
+  (void)bytes;
+  return w2p_env("KMP_W2R_RUN", 32);
+}
+
 template <typename T>
 static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
-                             const kmp_region* region, w2p::W2P& a, dim3& grid, dim3& block) {
+                             const kmp_region* region, int run, w2p::W2P& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
   if (w2p_env("KMP_DISABLE_WAVE", 0) || w2p_env("KMP_DISABLE_FAST", 0)) return false;
@@ -252,7 +474,12 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   const int64_t rows = 64 / txn;
   if (rows < P + 1) return false;  // an "above" and a "below" halo row per lane at most
   // only the waves covering the region's rows are launched
-  const int64_t w0 = yb / rows, w1 = ceil_div(ye, rows);
+  int64_t w0 = yb / rows, w1 = ceil_div(ye, rows);
+  if (run > 0) {  // rolling: runs of ``run`` rows from the region's first row
+    run = (int)(ceil_div(run, rows) * rows);
+    w0 = 0;
+    w1 = ceil_div(ye - yb, (int64_t)run);
+  }
   const int64_t waves = w1 - w0;
   const int64_t nwv = waves < 4 ? waves : 4;
   const int64_t ngrp = ceil_div(waves, nwv);
@@ -265,6 +492,7 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   a.ybeg = (int)yb;
   a.yend = (int)ye;
   a.wbase = (int)w0;
+  a.rrun = run;
   const int64_t nblk = B * ngrp;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));
@@ -273,6 +501,11 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
 
 template <typename T, bool DEC>
 static void launch_wave2dp(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
+  if (a.rrun > 0) {
+    if (P == 1) w2p::wave2dr_kernel<T, DEC, 1><<<grid, block, 0, s>>>(a);
+    else w2p::wave2dr_kernel<T, DEC, 2><<<grid, block, 0, s>>>(a);
+    return;
+  }
   if (P == 1) w2p::wave2dp_kernel<T, DEC, 1><<<grid, block, 0, s>>>(a);
   else w2p::wave2dp_kernel<T, DEC, 2><<<grid, block, 0, s>>>(a);
 }
@@ -283,7 +516,8 @@ int try_wave2dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w2p::W2P a{};
     dim3 grid, block;
-    if (!wave2dp_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (!wave2dp_geometry<T>(g, B, C, pred, region, w2p_run(pred->padding, (int)sizeof(T)), a, grid, block))
+      return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 3; ++k)
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -291,7 +525,7 @@ int try_wave2dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
     a.lo_out = lowres;
     a.maps = maps;
     launch_wave2dp<T, false>(pred->padding, grid, block, stream, a);
-    return check_launch("wave2dp_encode");
+    return check_launch(a.rrun > 0 ? "wave2dr_encode" : "wave2dp_encode");
   }
   return KMP_ERR_UNSUPPORTED;
 }
@@ -302,7 +536,8 @@ int try_wave2dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w2p::W2P a{};
     dim3 grid, block;
-    if (!wave2dp_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (!wave2dp_geometry<T>(g, B, C, pred, region, w2p_run(pred->padding, (int)sizeof(T)), a, grid, block))
+      return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 3; ++k) {
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -311,7 +546,7 @@ int try_wave2dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
     a.hi_out = hi;
     a.lo_in = lowres;
     launch_wave2dp<T, true>(pred->padding, grid, block, stream, a);
-    return check_launch("wave2dp_decode");
+    return check_launch(a.rrun > 0 ? "wave2dr_decode" : "wave2dp_decode");
   }
   return KMP_ERR_UNSUPPORTED;
 }

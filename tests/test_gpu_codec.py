@@ -353,6 +353,11 @@ def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(5, 7, 9), padding=p), x)
 
 
+def _W2P_DEFAULT(p, dtype):
+    """The image p = 1, 2 kernel the dispatcher picks without overrides."""
+    return 'wave2dr'
+
+
 @pytest.mark.parametrize('shape,dtype,p', [
     ((8, 256, 256, 1), np.uint8, 1),     # C2 geometry: 16 lanes per row, 4 rows per wave
     ((8, 256, 256, 1), np.uint8, 2),     # rows (4) < 2p+2: a lane holds both halo rows
@@ -362,9 +367,14 @@ def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
     ((1, 20, 256, 1), np.uint16, 1),     # 2 rows per wave
     ((2, 9, 16, 1), np.uint8, 2),        # one lane per row, Ey = 5 < rows
 ])
-def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
-    """The p = 1, 2 image wave kernel (kmp_codec_wave2dp.hip) against the oracle, whole-image and
-    row-region (chunked) launches; asserts which kernel served the call."""
+@pytest.mark.parametrize('run', [None, '0', '8', '12', '64'])
+def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
+    """The p = 1, 2 image wave kernels (kmp_codec_wave2dp.hip) against the oracle, whole-image and
+    row-region (chunked) launches: the row-group kernel and the y-rolling kernel with runs of 8, 12
+    and 64 rows per wave (KMP_W2R_RUN, rounded up to the wave's rows); asserts which kernel served
+    the call."""
+    if run is not None:
+        monkeypatch.setenv('KMP_W2R_RUN', run)
     import oracle
     from oracle import predictors as OP
     ns, ons = kom.image, oracle.image
@@ -375,13 +385,14 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
     pred = kom.MeanPredictor(p, 2)
     lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
     wave = (shape[2] // 2 // (8 // np.dtype(dtype).itemsize)) in (1, 2, 4, 8, 16, 32, 64)
-    assert _last_launch(kom) == ('wave2dp_encode' if wave else 'fast2d_encode')
+    kern = _W2P_DEFAULT(p, dtype) if run is None else ('wave2dp' if run == '0' else 'wave2dr')
+    assert _last_launch(kom) == (kern + '_encode' if wave else 'fast2d_encode')
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, b) in enumerate(zip(maps, want_maps)):
         bad = np.argwhere(a != b)
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
     assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
-    assert _last_launch(kom) == ('wave2dp_decode' if wave else 'fast2d_decode')
+    assert _last_launch(kom) == (kern + '_decode' if wave else 'fast2d_decode')
     lo2, (maps2, _) = ns.encode_chunks(pred, enc, x, chunk=5, padding=p)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, b) for a, b in zip(maps2, want_maps))
     assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=(7, 9), padding=p), x)

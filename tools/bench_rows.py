@@ -115,7 +115,7 @@ def main():
         codec_rows(f'volume_mean_p{p}', V, OV, vol, vol_h, kom.MeanPredictor(p, 3), OP.mean_predictions_fn(p, 3),
                    V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16, OV.decode_values_uint16,
                    p, raw_v, 3)
-    for p in (0, 1):
+    for p in (0, 1, 2):
         codec_rows(f'image_mean_p{p}', I, OI, img, img_h, kom.MeanPredictor(p, 2), OP.mean_predictions_fn(p, 2),
                    I.encode_values_uint8, I.decode_values_uint8, OI.encode_values_uint8, OI.decode_values_uint8,
                    p, raw_i, 2)
