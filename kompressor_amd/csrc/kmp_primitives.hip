@@ -695,13 +695,22 @@ __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
   const int32_t zlo = oz >= 1 ? oz - 1 : 0;
   const int32_t zhi = oz + KK < S.e[0] ? oz + KK : S.e[0];  // node planes [zlo, zhi)
 
-  // ---- node planes -> LDS: the aligned 16-byte blocks covering the byte range (every block
-  // holds at least one byte of the window, so it lies in a mapped page) ----
+  // ---- node planes -> LDS: the aligned 16-byte blocks covering the byte range; the partial
+  // blocks at either end copy only the window's own bytes ----
   const unsigned char* g0 = (const unsigned char*)(win + (b * S.e[0] + zlo) * (int64_t)plane);
   const int32_t shift = (int32_t)((uintptr_t)g0 & 15);
+  const int32_t nbytes = (zhi - zlo) * plane * (int32_t)sizeof(T);
   const uint4* src = (const uint4*)(g0 - shift);
-  const int32_t nchunk = ((zhi - zlo) * plane * (int32_t)sizeof(T) + shift + 15) >> 4;
-  for (int32_t i = threadIdx.x; i < nchunk; i += kThreads) *(uint4*)(smem + 16 * i) = src[i];
+  const int32_t nchunk = (nbytes + shift + 15) >> 4;
+  for (int32_t i = threadIdx.x; i < nchunk; i += kThreads) {
+    const int32_t lo = 16 * i - shift;  // byte range [lo, lo + 16) of the window planes
+    if (lo >= 0 && lo + 16 <= nbytes) {
+      *(uint4*)(smem + 16 * i) = src[i];
+    } else {  // the partial first / last block: only its bytes inside the window, element by element
+      for (int32_t k = lo < 0 ? 0 : lo; k < lo + 16 && k < nbytes; k += (int32_t)sizeof(T))
+        *(T*)(smem + shift + k) = *(const T*)(g0 + k);
+    }
+  }
   const T* nodes = (const T*)(smem + shift);  // [z - zlo][y][x]
   uint32_t* xs = (uint32_t*)(smem + nodes_bytes);  // p >= 1: [z - zlo][y][cx] sums over x
   // [slot: z = oz - 1 + slot][cy][cx], after a pad of >= Lcx + 1 words
