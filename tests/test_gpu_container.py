@@ -39,11 +39,13 @@ CASES = [
     ('mean0_u8_img', 2, (16, 256, 256, 1), np.uint8, 1.0),
     ('mean0_f32', 3, (2, 64, 64, 64, 1), np.float32, 0.5),
     ('linear0_u16', 3, (2, 32, 32, 32, 1), np.uint16, 2.0),
+    ('mean2_u16', 3, (2, 40, 36, 64, 1), np.uint16, 2.0),      # the z-rolling p = 2 kernel
+    ('mean2_u8_img', 2, (4, 100, 256, 1), np.uint8, 1.0),      # the y-rolling image kernel
 ]
 
 
 def _predictor(kom, name, ndim):
-    p = 1 if 'mean1' in name else 0
+    p = int(name[4]) if name.startswith('mean') else 0
     if name.startswith('linear'):
         n, k = 8, 19
         w = (np.full((n, k), 1.0 / n) + np.random.default_rng(3).standard_normal((n, k)) * 0.01).astype(np.float32)
