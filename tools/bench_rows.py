@@ -147,8 +147,8 @@ def main():
     if not want or 'volume_chunks' in want:
         pred = kom.MeanPredictor(0, 3)
         lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, vol)
-        te = gpu_time(lambda: V.encode_chunks(pred, V.encode_values_uint16, vol, chunk=32), 3)
-        td = gpu_time(lambda: V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=32), 3)
+        te = gpu_time(lambda: V.encode_chunks(pred, V.encode_values_uint16, vol, chunk=32), args.reps)
+        td = gpu_time(lambda: V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=32), args.reps)
         emit('volume_chunks:encode', 'encode_chunks chunk=32, fused region launches', 2 * raw_v, te)
         emit('volume_chunks:decode', 'decode_chunks chunk=32, fused region launches', 2 * raw_v, td)
 
@@ -160,8 +160,8 @@ def main():
         for nt in (512, 128):  # the whole C3 batch (GPU-bound), and 128 tiles (host-bound, ~0.1 ms per call)
             sub = vol[:nt]
             lo, (maps, dims) = V.encode(cb, V.encode_values_uint16, sub)
-            te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), 5)
-            td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), 5)
+            te = gpu_time(lambda: V.encode(cb, V.encode_values_uint16, sub), args.reps)
+            td = gpu_time(lambda: V.decode(cb, V.decode_values_uint16, lo, (maps, dims)), args.reps)
             tag = 'volume_callback' if nt == 512 else f'volume_callback_{nt}'
             emit(tag + ':encode', f'callback encode, {nt} tiles (window, opaque predictions_fn, fused coder)',
                  sub.numel() * 4, te)

@@ -29,6 +29,7 @@ plan.highres.copy_(vol)
 for name, fn in (('encode', lambda: V.encode(cb, V.encode_values_uint16, vol)),
                  ('decode', lambda: V.decode(cb, V.decode_values_uint16, lo, enc)),
                  ('fused_encode', lambda: V.encode(pred, V.encode_values_uint16, vol)),
+                 ('chunks_encode', lambda: V.encode_chunks(pred, V.encode_values_uint16, vol, chunk=32)),
                  ('graph_encode', lambda: plan.encode()),
                  ('graph_decode', lambda: plan.decode())):
     for _ in range(10):
