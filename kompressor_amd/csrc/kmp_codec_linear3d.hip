@@ -57,21 +57,32 @@ __device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: 
 // register pair (pairing cells 0/1 and 2/3 instead needs node pairs (x+1, x+2) assembled by
 // moves in every channel: 214 v_mov per wave, 18 % of a VALU stream the SQ counters show busy
 // 75 % of the cycles).  The chain is unchanged: fma over n = dz*4 + dy*2 + dx from the bias.
-// ``Wt`` is the LDS copy of the weights, channel-major [19][8] with every weight stored twice
-// (the packed operand {w, w}), then the bias [19] (uniform ds_reads: the constants never compete
-// for scalar registers).
-template <typename T, int K, int G>
+// The weights: SG (default) reads W [8][19] and b with uniform loads into scalar registers, the
+// packed operand {w, w} built by the FMA's operand selection -- no LDS copy, no barrier before the
+// first channel, and 106 / 100 VGPRs instead of 146 (4-5 waves per SIMD instead of 3): C3 168 / 222
+// -> 143 / 191 us per direction (profiles/round2/ab_linear3d_sgpr.log).  KMP_L3_SGPR=0: ``Wt``, the
+// LDS copy, channel-major [19][8] with every weight stored twice, then the bias [19].
+typedef const __attribute__((address_space(4))) float* CFloat;  // uniform loads (scalar registers)
+
+template <typename T, int K, int G, bool SG>
 __device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 (&NP1)[3][G][3], int pl, int g,
-                                        const float* Wt, uint32_t (&out)[4]) {
-  // weights stored pre-splat ({w, w} per n): each 16-byte read is two ready operand pairs
+                                        const float* Wt, CFloat Wc, CFloat Bc, uint32_t (&out)[4]) {
   f32x2 w2[8];
+  float bk;
+  if constexpr (SG) {  // W [8][19] and b read with uniform (scalar) loads
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = *(const float4*)(Wt + K * 16 + 4 * q);
-    w2[2 * q] = (f32x2){v.x, v.y};
-    w2[2 * q + 1] = (f32x2){v.z, v.w};
+    for (int n = 0; n < 8; ++n) w2[n] = (f32x2){Wc[n * 19 + K], Wc[n * 19 + K]};
+    bk = Bc[K];
+  } else {
+    // weights stored pre-splat ({w, w} per n): each 16-byte read is two ready operand pairs
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *(const float4*)(Wt + K * 16 + 4 * q);
+      w2[2 * q] = (f32x2){v.x, v.y};
+      w2[2 * q + 1] = (f32x2){v.z, v.w};
+    }
+    bk = Wt[19 * 16 + K];
   }
-  const float bk = Wt[19 * 16 + K];
   f32x2 a02 = {bk, bk}, a13 = {bk, bk};
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
@@ -90,7 +101,7 @@ __device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 
 constexpr int kXch = 5;  // channels exchanged downwards: 3, 9, 10, 16 (plane c), 17 (plane c-1)
 constexpr int kWtWords = 324;  // 19 * 8 weights stored twice + 19 biases, rounded up to 16 B
 
-template <typename T, bool DEC>
+template <typename T, bool DEC, bool SG>
 __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   constexpr int VX = 8 / (int)sizeof(T);
   static_assert(VX == 4 || VX == 8, "u16 / u8");
@@ -100,15 +111,18 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   float* Wt = (float*)smem;
   uint32_t* xrow = smem + kWtWords;
-  for (int t = threadIdx.x; t < 19 * 9; t += blockDim.x) {
-    if (t < 152) {  // W[n][k] -> Wt[k][n] twice
-      Wt[(t % 19) * 16 + 2 * (t / 19)] = a.W[t];
-      Wt[(t % 19) * 16 + 2 * (t / 19) + 1] = a.W[t];
-    } else {
-      Wt[304 + (t - 152)] = a.b[t - 152];
+  const CFloat Wc = (CFloat)a.W, Bc = (CFloat)a.b;
+  if constexpr (!SG) {
+    for (int t = threadIdx.x; t < 19 * 9; t += blockDim.x) {
+      if (t < 152) {  // W[n][k] -> Wt[k][n] twice
+        Wt[(t % 19) * 16 + 2 * (t / 19)] = a.W[t];
+        Wt[(t % 19) * 16 + 2 * (t / 19) + 1] = a.W[t];
+      } else {
+        Wt[304 + (t - 152)] = a.b[t - 152];
+      }
     }
+    __syncthreads();
   }
-  __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
@@ -247,7 +261,7 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
 #define KMP_CH(OUT, PLANE, K)                                             \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                         \
     uint32_t o[4];                                                        \
-    channel<T, K, G>(NP, NP1, PLANE, g, Wt, o);                           \
+    channel<T, K, G, SG>(NP, NP1, PLANE, g, Wt, Wc, Bc, o);               \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j]; \
   }
 
@@ -465,7 +479,8 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
     a.maps = maps;
     a.W = pred->weights;
     a.b = pred->bias;
-    l3::linear3d_kernel<T, false><<<grid, block, lds, stream>>>(a);
+    if (l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, false, true><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, false, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -488,7 +503,8 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
     a.lo_in = lowres;
     a.W = pred->weights;
     a.b = pred->bias;
-    l3::linear3d_kernel<T, true><<<grid, block, lds, stream>>>(a);
+    if (l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, true, true><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, true, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_decode");
   }
   return KMP_ERR_UNSUPPORTED;
