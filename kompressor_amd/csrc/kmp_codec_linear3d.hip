@@ -43,6 +43,7 @@ struct L3 {
   int32_t zbegin, zend;
   int32_t txn, rows, nwv;
   int32_t xcd_per;
+  int32_t uld;
 };
 
 template <typename T>
@@ -177,12 +178,30 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   // ---- all loads up front: node planes c-1, c, c+1 (own row + the last row's halo row).  The
   // encode loads unconditionally from clamped, in-bounds addresses (rows / planes past the edges
   // read a valid neighbour whose values the masks discard): no zero-initialised registers and no
-  // exec-mask branches, 208 -> 190 us at C3 (same box, ab_linear3d_loads.log).  The decode keeps
-  // its guarded loads, which measured 1-3 % faster for it. ----
+  // exec-mask branches, 208 -> 190 us at C3 (same box, ab_linear3d_loads.log).  The decode does
+  // the same (map planes clamped to the last one that exists): with the weights in scalar registers
+  // 190-205 -> 178-187 us (profiles/round2/ab_linear3d_uld.log); KMP_L3_ULD=0 keeps the guarded
+  // loads, which measured 1-3 % faster with the LDS weight copy. ----
   V own[3], dn[3];
   uint4 e1, o0, o1;
   uint2 mv[7];
   if constexpr (DEC) {
+   if (a.uld) {  // decode with unconditional clamped loads (masks discard the edge values)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int q = c - 1 + t;
+      const T* p = lin + lsrc(q < 0 ? 0 : q, a.Lz, a.Ez) * lplane;
+      own[t] = ld8c(p + lo_own);
+      dn[t] = ld8c(p + lo_dn);
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int par[3];
+      map_parity(3, k, par);
+      const int cz = par[0] ? (c < a.Lcz ? c : (a.Lcz > 0 ? a.Lcz - 1 : 0)) : c;
+      mv[k] = ld8(mbase[k] + cz * mplane[k]);
+    }
+   } else {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       own[t] = dn[t] = V{};
@@ -199,6 +218,7 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
       mv[k] = make_uint2(0, 0);
       if (mok_y[k] && (!par[0] || vz1)) mv[k] = ld8(mbase[k] + c * mplane[k]);
     }
+   }
   } else {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -503,6 +523,7 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
     a.lo_in = lowres;
     a.W = pred->weights;
     a.b = pred->bias;
+    a.uld = l3_env("KMP_L3_ULD", 1) && a.Lcz > 0 && a.Lcy > 0;  // clamped map planes / rows exist
     if (l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, true, true><<<grid, block, lds, stream>>>(a);
     else l3::linear3d_kernel<T, true, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_decode");
