@@ -10,6 +10,8 @@
 // One wavefront per element: the 64 lanes stage the element's logits in LDS and each counts a
 // 1/64 share of the comparisons, reduced with cross-lane adds.  NaN sorts after every number
 // (numpy / XLA argsort order).
+#include <cstdlib>
+
 #include "kmp_common.h"
 
 namespace kmp {
@@ -182,6 +184,283 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_select_kern
   }
 }
 
+
+// ---- 16-byte vector form (L % 4 == 0, L <= 256 * E4, rows 16-B aligned) -----------------------
+// Lane l holds classes s * 256 + 4 l + q (q = 0..3) of slot s as one float4: one 16-B load per lane
+// and slot instead of four 4-B loads; classes past L are loaded as NaN.  Each wave walks its
+// elements (wave-uniform indices: loop control and addressing on the scalar unit) with a ring of
+// kCatPF rows in registers, refilling a slot as soon as it is ranked.  The VALU work per element
+// is what bounds this kernel, so:
+//   encode: #{j : l_j < l_i, or l_j == l_i and j < i} from two float compares per class (NaN rows
+//   of the reference order handled by a uniform branch; padding NaNs never count), the j < i part
+//   as a scalar lane mask.
+//   decode: order_key integers; rank 0 by one wave max; otherwise a 256-bin histogram (LDS
+//   atomics) of the 8 highest bits in which the keys differ (DPP OR-reduce), a DPP prefix scan
+//   over the bins to pick the one that holds rank k, and a bitwise radix select inside that bin,
+//   stopping as soon as the key range [t, hi) that holds rank k contains one key.  Then the m-th
+//   highest class index with a key in [t, hi).
+constexpr int kCatPF = 4;  // 8 measured no faster (the loads are not what bounds it)
+typedef float cat_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int E4>
+struct CatRow {
+  cat_f32x4 v[E4];
+  int64_t x;
+};
+
+template <typename T, int E4>
+__device__ __forceinline__ void cat_load(const float* __restrict__ logits, int64_t L, const T* __restrict__ x,
+                                         int64_t el, int lane, CatRow<E4>& r) {
+  const cat_f32x4* row = (const cat_f32x4*)(logits + el * L);
+  const float qnan = __builtin_nanf("");
+#pragma unroll
+  for (int s = 0; s < E4; ++s) {
+    const int c4 = s * 64 + lane;
+    r.v[s] = 4 * c4 < L ? __builtin_nontemporal_load(row + c4) : (cat_f32x4){qnan, qnan, qnan, qnan};
+  }
+  r.x = std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el];
+}
+
+// DPP steps (row_shr:1,2,4,8 inside rows of 16, then row_bcast:15 / row_bcast:31 across rows):
+// an inclusive scan over the 64 lanes; lane 63 holds the whole-wave reduction.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x, uint32_t id, Op op) {
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x111, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x112, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x114, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x118, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x142, 0xa, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane(
+      (int)wave_scan_dpp(x, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; }), 63);
+}
+__device__ __forceinline__ uint32_t wave_or_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(x, 0u, [](uint32_t a, uint32_t b) { return a | b; }), 63);
+}
+
+__device__ __forceinline__ uint32_t order_key_fast(float f) {  // == order_key
+  const float z = f + 0.0f;  // -0 -> +0 (round to nearest), NaN stays NaN
+  const uint32_t u = __float_as_uint(z);
+  const uint32_t k = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+  return z != z ? 0xffffffffu : k;
+}
+
+__device__ __forceinline__ uint64_t lanes_below(int nl) {  // mask of lanes 0 .. nl-1
+  return nl <= 0 ? 0ull : nl >= 64 ? ~0ull : ((1ull << nl) - 1);
+}
+
+template <typename T, int DIR, int E4>
+__device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins, int peel,
+                                         T* __restrict__ out, int64_t el) {
+  if constexpr (DIR == KMP_ENCODE) {
+    const int64_t g = cur.x;
+    int64_t best = -1;
+    if (g >= 0)
+      for (int64_t i = g; i < L; i += class_mod<T>()) {
+        const int ii = (int)i, si = ii >> 8, ln = (ii & 255) >> 2, qi = ii & 3;
+        float fv = 0.f;
+#pragma unroll
+        for (int ss = 0; ss < E4; ++ss)
+          if (ss == si) fv = qi == 0 ? cur.v[ss].x : qi == 1 ? cur.v[ss].y : qi == 2 ? cur.v[ss].z : cur.v[ss].w;
+        const float li = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fv), ln));
+        uint32_t asc = 0;
+        bool fast = li == li;
+        if (fast) {  // #{l_j < l_i} and #{l_j <= l_i} per lane in one word, summed by a DPP scan
+          uint32_t c = 0;
+#pragma unroll
+          for (int s = 0; s < E4; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c += (cur.v[s][q] < li ? 1u : 0u) + (cur.v[s][q] <= li ? 0x10000u : 0u);
+          c = (uint32_t)__builtin_amdgcn_readlane(
+              (int)wave_scan_dpp(c, 0u, [](uint32_t a, uint32_t b) { return a + b; }), 63);
+          asc = c & 0xffffu;
+          fast = (c >> 16) == asc + 1;  // class i is its only tie
+        }
+        if (!fast) {  // ties (ordered by class index) or a NaN logit
+          asc = 0;
+#pragma unroll
+        for (int s = 0; s < E4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lj = cur.v[s][q];
+            // lanes whose class s * 256 + 4 lane + q is below ii
+            const uint64_t before = lanes_below((ii - s * 256 - q + 3) >> 2);
+            uint64_t hit;
+            if (li == li) hit = __ballot(lj < li) | (__ballot(lj == li) & before);
+            else hit = __ballot(lj == lj) | (__ballot(lj != lj) & before);  // NaN sorts after numbers
+            asc += __popcll(hit);
+          }
+        }
+        const int64_t p = L - 1 - (int64_t)asc;
+        best = (best < 0 || p < best) ? p : best;
+      }
+    if (lane == 0) out[el] = (T)(best < 0 ? 0 : best);
+  } else {
+    uint32_t key[E4][4];
+    bool ok[E4][4];
+#pragma unroll
+    for (int s = 0; s < E4; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ok[s][q] = s * 256 + 4 * lane + q < L;
+        key[s][q] = ok[s][q] ? order_key_fast(cur.v[s][q]) : 0u;  // padding keys 0: below every key
+      }
+    auto count = [&](auto pred) {  // wave-uniform #{classes j with pred(key_j)}; pred(0) is false
+      uint32_t c = 0;
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c += __popcll(__ballot(pred(key[s][q])));
+      return c;
+    };
+    const int64_t kk = cur.x;
+    const uint32_t k = (uint32_t)(kk < 0 ? 0 : (kk >= L ? L - 1 : kk));
+    uint32_t t = 0, m = 0;
+    uint64_t hi = 1ull << 32;  // the answer's key lies in [t, hi); m = its rank among those keys
+    if ((int)k < peel) {
+      uint32_t taken = 0;
+      while (true) {
+        uint32_t best = 0;  // valid keys are > 0 (order_key of -inf is 0x007fffff)
+#pragma unroll
+        for (int s = 0; s < E4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if ((uint64_t)key[s][q] < hi) best = max(best, key[s][q]);
+        const uint32_t wmax = wave_max_dpp(best);
+        const uint32_t ties = count([&](uint32_t v) { return v == wmax; });
+        if (taken + ties > k) {
+          t = wmax;
+          m = k - taken;
+          hi = (uint64_t)wmax + 1;
+          break;
+        }
+        taken += ties;
+        hi = wmax;
+      }
+    } else {
+      // the bits below the keys' common prefix: P of them; histogram digit = bits [sh, sh + 8)
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[0][0]);  // class 0 exists
+      uint32_t dif = 0;
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dif |= ok[s][q] ? key[s][q] ^ k0 : 0u;
+      dif = wave_or_dpp(dif);
+      const int P = dif == 0 ? 0 : 32 - __clz((int)dif);
+      const int sh = P > 8 ? P - 8 : 0;
+      // bins in descending digit order: bin 255 - digit
+      *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (ok[s][q]) atomicAdd(bins + (255 - ((key[s][q] >> sh) & 255u)), 1u);
+      __builtin_amdgcn_wave_barrier();
+      const uint4 b = *(const uint4*)(bins + 4 * lane);
+      const uint32_t tot = b.x + b.y + b.z + b.w;
+      const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
+      const uint32_t base = incl - tot;
+      const uint64_t hit = __ballot(base <= k && k < incl);
+      const int ls = (int)__builtin_ctzll(hit);
+      // inside the lane: the bin whose cumulative range holds k
+      uint32_t c_hi = base, cnt = b.x, q = 0;
+      if (k >= c_hi + b.x) {
+        c_hi += b.x; cnt = b.y; q = 1;
+        if (k >= c_hi + b.y) {
+          c_hi += b.y; cnt = b.z; q = 2;
+          if (k >= c_hi + b.z) { c_hi += b.z; cnt = b.w; q = 3; }
+        }
+      }
+      c_hi = (uint32_t)__builtin_amdgcn_readlane((int)c_hi, ls);
+      cnt = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ls);
+      q = (uint32_t)__builtin_amdgcn_readlane((int)q, ls);
+      const uint32_t digit = 255u - (uint32_t)(4 * ls + (int)q);
+      const uint32_t top = sh + 8 >= 32 ? 0u : (k0 >> (sh + 8)) << (sh + 8);
+      t = top | (digit << sh);
+      hi = (uint64_t)t + (1ull << sh);
+      uint32_t c_t = c_hi + cnt;
+      for (int bit = sh - 1; bit >= 0 && c_t - c_hi > 1; --bit) {
+        const uint32_t cand = t | (1u << bit);
+        const uint32_t c = count([&](uint32_t v) { return v >= cand; });
+        if (c >= k + 1) {
+          t = cand;
+          c_t = c;
+        } else {
+          hi = cand;
+          c_hi = c;
+        }
+      }
+      m = k - c_hi;
+    }
+    // the m-th highest class index among the classes with key in [t, hi); padding keys (0) are
+    // below every valid key (>= 0x007fffff), so the range starts at 1 at the least
+    const uint32_t tlo = t > 0 ? t : 1u;
+    int64_t cls = 0;
+    for (int s = E4 - 1; s >= 0; --s) {
+      uint64_t w[4];
+      uint32_t tot = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[q] = __ballot(key[s][q] >= tlo && (uint64_t)key[s][q] < hi);
+        tot += __popcll(w[q]);
+      }
+      if (m >= tot) {
+        m -= tot;
+        continue;
+      }
+      uint64_t lanes = w[0] | w[1] | w[2] | w[3];
+      while (true) {  // lanes from the highest; within a lane q from 3 down
+        const int l = 63 - __clzll(lanes);
+        int q = 3;
+        for (; q >= 0; --q)
+          if ((w[q] >> l) & 1) {
+            if (m == 0) break;
+            --m;
+          }
+        if (q >= 0) {
+          cls = s * 256 + 4 * l + q;
+          break;
+        }
+        lanes &= ~(1ull << l);
+      }
+      break;
+    }
+    if (lane == 0) out[el] = (T)cls;
+  }
+}
+
+template <typename T, int DIR, int E4, int PF>
+__global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const float* __restrict__ logits, int64_t n,
+                                                                          int64_t L, const T* __restrict__ x,
+                                                                          T* __restrict__ out, int peel) {
+  __shared__ __attribute__((aligned(16))) uint32_t bins_all[kCatWaves][256];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
+  uint32_t* bins = bins_all[wv];
+  const int64_t ws = (int64_t)gridDim.x * kCatWaves;
+  const int64_t el0 = (int64_t)blockIdx.x * kCatWaves + wv;
+  if (el0 >= n) return;
+  CatRow<E4> ring[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (el0 + u * ws < n) cat_load<T, E4>(logits, L, x, el0 + u * ws, lane, ring[u]);
+  for (int64_t base = el0; base < n; base += PF * ws) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int64_t e = base + u * ws;
+      if (e >= n) break;
+      const CatRow<E4> cur = ring[u];
+      const int64_t ep = e + PF * ws;
+      if (ep < n) cat_load<T, E4>(logits, L, x, ep, lane, ring[u]);
+      cat_rank<T, DIR, E4>(cur, L, lane, bins, peel, out, e);
+    }
+  }
+}
+
 }  // namespace kmp
 
 using namespace kmp;
@@ -194,8 +473,27 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
   KMP_REQUIRE(logits && x && out, "null pointer");
   int64_t g = (n + kCatWaves - 1) / kCatWaves;
   const unsigned grid = (unsigned)(g > 65536 ? 65536 : g);
+  // vector form: 8 waves per SIMD over the chip, each walking its elements one load ahead
+  const char* ev = std::getenv("KMP_CAT_VEC");
+  const bool vec = (!ev || std::atoi(ev)) && L % 4 == 0 && L <= 512 && ((uintptr_t)logits & 15) == 0;
+  const unsigned vgrid = (unsigned)(g > 2048 ? 2048 : g);
+  const char* pv = std::getenv("KMP_CAT_PEEL");  // decode ranks below this peel maxima
+  const int peel = pv ? std::atoi(pv) : 4;
   return dispatch_int_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
+    if (vec) {
+      constexpr int PF = kCatPF;
+      hipStream_t st = (hipStream_t)stream;
+      if (direction == KMP_ENCODE && L <= 256)
+        categorical_vec_kernel<T, KMP_ENCODE, 1, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+      else if (direction == KMP_ENCODE)
+        categorical_vec_kernel<T, KMP_ENCODE, 2, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+      else if (L <= 256)
+        categorical_vec_kernel<T, KMP_DECODE, 1, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+      else
+        categorical_vec_kernel<T, KMP_DECODE, 2, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+      return check_launch("categorical_vec");
+    }
     if (direction == KMP_ENCODE)
       categorical_kernel<T, KMP_ENCODE><<<grid, 64 * kCatWaves, 0, (hipStream_t)stream>>>(logits, n, L, (const T*)x,
                                                                                           (T*)out);

@@ -224,12 +224,17 @@ def test_categorical_matches_golden(kom, name, chunk):
     assert torch.equal(rec, hi)
 
 
-def test_categorical_coder_vs_oracle(kom):
+@pytest.mark.parametrize('vec', ['1', '0'])
+def test_categorical_coder_vs_oracle(kom, monkeypatch, vec):
+    """Rank coder vs the oracle's stable argsort; vec='1' serves L % 4 == 0, L <= 512 with the 16-byte
+    vector kernels (KMP_CAT_VEC), '0' with the scalar ones."""
     import oracle
+    monkeypatch.setenv('KMP_CAT_VEC', vec)
     rng = np.random.default_rng(7)
     for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32),
                   (64, np.uint8), (128, np.uint16), (512, np.uint16), (1, np.uint8), (2, np.uint8),
-                  (65, np.uint8), (511, np.uint16), (-200, np.uint8), (-500, np.uint16)):
+                  (65, np.uint8), (511, np.uint16), (-200, np.uint8), (-500, np.uint16), (4, np.uint32),
+                  (260, np.uint8), (8, np.uint8), (256, np.int32)):
         heavy_ties = L < 0  # few distinct values: long runs of equal keys ordered by class index
         L = abs(L)
         logits = rng.standard_normal((513, L)).astype(np.float32)
@@ -242,6 +247,7 @@ def test_categorical_coder_vs_oracle(kom):
             logits[6, :4] = [np.nan, -0.0, 0.0, np.nan]      # NaN after every number, -0 == +0
             logits[7, :4] = [np.inf, -np.inf, np.nan, np.inf]
         x = rng.integers(0, min(L + 3, np.iinfo(dt).max), size=513).astype(dt)
+        x[::3] = rng.integers(0, min(L, 10), size=x[::3].size)  # small ranks / classes (the peel)
         got = kom.utils.encode_categorical(logits, x)
         want = oracle.common.encode_categorical(logits, x)
         assert np.array_equal(got, want), L

@@ -9,6 +9,19 @@ from kompressor_amd import _nd
 wl = sys.argv[1] if len(sys.argv) > 1 else 'volume'
 p = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+if wl == 'categorical':  # rank coder, 1M elements x 256 logits (tools/bench_rows.py's row)
+    torch.manual_seed(0)
+    logits = torch.rand((1 << 20, 256), device='cuda')
+    gt = torch.randint(0, 256, (1 << 20,), device='cuda', dtype=torch.uint8)
+    small = torch.randint(0, 4, (1 << 20,), device='cuda', dtype=torch.uint8)
+    for _ in range(reps):
+        enc = kom.volume.encode_categorical(logits, gt)
+        dec = kom.volume.decode_categorical(logits, enc)
+        kom.volume.decode_categorical(logits, small)
+    torch.cuda.synchronize()
+    assert torch.equal(dec, gt)
+    print('ok', os.environ.get('KMP_TAG', ''))
+    sys.exit(0)
 ndim = 3 if wl == 'volume' else 2
 shape, dt = ((512, 64, 64, 64, 1), np.uint16) if ndim == 3 else ((1024, 256, 256, 1), np.uint8)
 host = np.random.default_rng(0).integers(0, np.iinfo(dt).max + 1, size=shape, dtype=np.int64).astype(dt)
