@@ -108,3 +108,32 @@ def test_linear_fused_p1(kom, shape, variant, monkeypatch):
     assert kom._lib.lib.kmp_last_launch().decode() in ('linear3dp_decode', 'linear3r_decode')
     lo2, (maps2, _) = V.encode_chunks(pred, V.encode_values_uint16, hi, chunk=5, padding=1)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
+
+
+@pytest.mark.parametrize('shape,dtype', [((4, 64, 64, 64, 1), np.uint16), ((2, 17, 30, 16, 1), np.uint16),
+                                         ((2, 12, 33, 32, 1), np.uint16), ((1, 9, 14, 128, 1), np.uint8),
+                                         ((3, 10, 9, 64, 1), np.uint8)])
+@pytest.mark.parametrize('sg,uld', [('1', '1'), ('0', '1'), ('1', '0')])
+def test_linear_fused_p0(kom, shape, dtype, sg, uld, monkeypatch):
+    """The fused LinearPredictor p = 0 volume kernel (kmp_codec_linear3d.hip) with each weight
+    source -- uniform (scalar) loads from W / b (KMP_L3_SGPR=1, default) or the LDS copy (0) -- and
+    with the decode's unconditional (KMP_L3_ULD=1, default) or guarded loads:
+    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, chunked."""
+    monkeypatch.setenv('KMP_L3_SGPR', sg)
+    monkeypatch.setenv('KMP_L3_ULD', uld)
+    hi = _data(shape, dtype, 9)
+    w, b = _weights(3, 0, 10, dtype)
+    pred = kom.LinearPredictor(w, b, 0, 3)
+    V, OV = kom.volume, oracle.volume
+    enc, dec, oenc = ((V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16) if dtype == np.uint16
+                      else (V.encode_values_uint8, V.decode_values_uint8, OV.encode_values_uint8))
+    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(0, w, b, 3), oenc, hi, padding=0)
+    lo, (maps, dims) = V.encode(pred, enc, hi, padding=0)
+    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3d_encode'
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, c) in enumerate(zip(maps, want_maps)):
+        assert np.array_equal(a, c), f'map {i}'
+    assert np.array_equal(V.decode(pred, dec, lo, (maps, dims), padding=0), hi)
+    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3d_decode'
+    rec = V.decode_chunks(pred, dec, lo, (maps, dims), chunk=6, padding=0)
+    assert np.array_equal(rec, hi)
