@@ -218,24 +218,44 @@ def timed_steps(run_enc, run_dec, steps, dist):
     return elapsed
 
 
+_SLEEP_RATE = []
+
+
+def _sleep_cycles(seconds):
+    """torch.cuda._sleep cycles for ``seconds`` of device time (rate calibrated once with events)."""
+    if not _SLEEP_RATE:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        torch.cuda._sleep(1_000_000)
+        e1.record()
+        torch.cuda.synchronize()
+        _SLEEP_RATE.append(1_000_000 / max(e0.elapsed_time(e1) / 1e3, 1e-6))  # cycles per second
+    return int(seconds * _SLEEP_RATE[0]) + 1
+
+
 def direction_times(run_enc, run_dec, n, dist):
-    """Average kernel duration per direction from HIP events on the launch stream, each over
-    ``n`` back-to-back launches of that direction (one event pair per run, so the markers do
-    not add to every launch); max over ranks.  This is what ``roofline.achieved`` divides by
-    and what the committed rocprofv3 kernel statistics must agree with."""
+    """Average kernel duration per direction from HIP events on the launch stream, over ``n``
+    encode / decode pairs alternating as the timed loop runs them (an event between every two
+    launches, so each interval is one kernel plus its launch boundary, in the cache state of the
+    timed region); max over ranks.  This is what ``roofline.achieved`` divides by and what the
+    committed rocprofv3 kernel statistics must agree with."""
     stream = torch.cuda.current_stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * n + 1)]
     torch.cuda.synchronize()
+    # keep the GPU busy (untimed) while the host enqueues all 2n launches, so the events time the
+    # kernels back to back on the device and not the host's launch rate (an eager launch costs
+    # ~20-45 us of Python / ctypes, as long as a C2 kernel)
+    torch.cuda._sleep(_sleep_cycles(2 * n * 100e-6))
     ev[0].record(stream)
-    for _ in range(n):
+    for i in range(n):
         run_enc()
-    ev[1].record(stream)
-    for _ in range(n):
+        ev[2 * i + 1].record(stream)
         run_dec()
-    ev[2].record(stream)
+        ev[2 * i + 2].record(stream)
     torch.cuda.synchronize()
-    t_enc = ev[0].elapsed_time(ev[1]) / n / 1e3
-    t_dec = ev[1].elapsed_time(ev[2]) / n / 1e3
+    t_enc = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(n)) / n / 1e3
+    t_dec = sum(ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(n)) / n / 1e3
     if dist:
         tt = torch.tensor([t_enc, t_dec], dtype=torch.float64, device='cuda')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
