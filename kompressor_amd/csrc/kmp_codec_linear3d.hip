@@ -44,12 +44,15 @@ struct L3 {
   int32_t txn, rows, nwv;
   int32_t xcd_per;
   int32_t uld;
+  int32_t full;  // Lcy == Ey and Lcx == Ex: interior planes take the FULL body
 };
 
+// astype(T) for u8/u16: trunc, saturate, NaN -> 0.  v_cvt_u32_f32 truncates and saturates to
+// [0, 2^32-1] with NaN -> 0, so one integer min finishes it (cvt_sat, kmp_wave.h): 2 VALU per value,
+// where fminf(fmaxf()) compiled to med3 + cvt plus a canonicalising v_max on some of them
 template <typename T>
-__device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: trunc, saturate, NaN -> 0
-  constexpr float hi = sizeof(T) == 2 ? 65535.0f : 255.0f;
-  return (uint32_t)fminf(fmaxf(v, 0.0f), hi);
+__device__ __forceinline__ uint32_t cast_t(float v) {
+  return cvt_sat<T>(v);
 }
 
 // Node values are kept as f32 pairs laid out for the packed FMAs: for the 4 cells X+4g .. X+4g+3
@@ -102,8 +105,20 @@ __device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 
 constexpr int kXch = 5;  // channels exchanged downwards: 3, 9, 10, 16 (plane c), 17 (plane c-1)
 constexpr int kWtWords = 324;  // 19 * 8 weights stored twice + 19 biases, rounded up to 16 B
 
-template <typename T, bool DEC, bool SG>
-__global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
+// All-zero weights and bias: a channel of a cell plane outside the tile (plane c-1 at c = 0, plane
+// c at c >= Lcz) evaluated with these is 0.0 -> 0, which is what the aggregation's mask gives it
+__constant__ float kZeroWeights[8 * 19 + 19];
+
+// FULL: the tile's cells fill the stored lowres rows and columns (Lcy == Ey, Lcx == Ex: every
+// even-sized tile, e.g. C3's 64^3) and the weights are read as scalars (SG).  Then the y+1
+// validity and every x validity but the row's first cell (X-1 = -1) are compile-time true, and a
+// missing cell plane (z) is zeroed at the source by reading its channels' weights from
+// kZeroWeights (uniform), so the aggregation masks only the row-above channels on row 0 and the
+// left cell on lane 0 of a row: 929 instead of 1 030 VALU instructions per encode wave, 93 instead
+// of 104 VGPRs (5 waves per SIMD instead of 4)
+template <typename T, bool DEC, bool SG, bool FULL, int WPE, bool ULD = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) linear3d_kernel(L3 a) {
+  static_assert(!FULL || SG, "FULL reads the weights as scalars");
   constexpr int VX = 8 / (int)sizeof(T);
   static_assert(VX == 4 || VX == 8, "u16 / u8");
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -145,12 +160,17 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   const int Yc = live ? Y : a.Ey - 1;
   const bool first = r == 0;
   const bool last = r == a.rows - 1 || Y == a.Ey - 1;
-  const bool vy1 = Y < a.Lcy;
+  const bool vy1 = FULL || Y < a.Lcy;  // FULL: Lcy == Ey, and lanes past Ey are not live
   const bool vy0 = Y >= 1;
   const bool need_dn = live && last && vy1;
   const int ydn = lsrc(Yc + 1, a.Ly, a.Ey);
   const bool xlast = tx == a.txn - 1;
   const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+  // FULL: the channels of cell plane c (P) and c-1 (Q) from the weights, or from kZeroWeights where
+  // that plane is outside the tile (uniform pointers)
+  const CFloat Zc = (CFloat)kZeroWeights;
+  const CFloat WcP = (FULL && !vz1) ? Zc : Wc, BcP = (FULL && !vz1) ? Zc + 152 : Bc;
+  const CFloat WcQ = (FULL && !vz0) ? Zc : Wc, BcQ = (FULL && !vz0) ? Zc + 152 : Bc;
 
   const int hplane = a.H * a.W_;
   const int lplane = a.Ey * a.Ex;
@@ -186,7 +206,10 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
   uint4 e1, o0, o1;
   uint2 mv[7];
   if constexpr (DEC) {
-   if (a.uld) {  // decode with unconditional clamped loads (masks discard the edge values)
+   // ULD: the unconditional form at compile time -- with the runtime choice the guarded form's
+   // control flow joins the paths and the compiler waits for every load (map rows included) before
+   // the first channel
+   if (ULD || a.uld) {  // decode with unconditional clamped loads (masks discard the edge values)
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int q = c - 1 + t;
@@ -281,7 +304,7 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
 #define KMP_CH(OUT, PLANE, K)                                             \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                         \
     uint32_t o[4];                                                        \
-    channel<T, K, G, SG>(NP, NP1, PLANE, g, Wt, Wc, Bc, o);               \
+    channel<T, K, G, SG>(NP, NP1, PLANE, g, Wt, PLANE ? WcP : WcQ, PLANE ? BcP : BcQ, o); \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j]; \
   }
 
@@ -326,10 +349,12 @@ __global__ void __launch_bounds__(256) linear3d_kernel(L3 a) {
 
   bool vx[VX + 1];
 #pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  for (int q = 0; q <= VX; ++q) vx[q] = (FULL && q >= 1) || ((X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
   const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
-  auto m = [&](const uint32_t (&v)[VX + 1], int q, bool zok, bool yok) { return (zok && yok && vx[q]) ? v[q] : 0u; };
+  auto m = [&](const uint32_t (&v)[VX + 1], int q, bool zok, bool yok) {
+    return ((FULL || zok) && yok && vx[q]) ? v[q] : 0u;  // FULL: a missing z plane's channels are 0 already
+  };
   auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };  // cell X-1 (all lanes)
   auto put8 = [&](int k, const uint32_t (&res)[VX]) {  // encode: one map row
     int par[3];
@@ -477,6 +502,7 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)waves;
   const int64_t nblk = B * (ze - zb);
   a.xcd_per = (l3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  a.full = l3_env("KMP_L3_FULL", 1) && g.Lc[1] == g.E[1] && g.Lc[2] == g.E[2];
   lds = (size_t)(l3::kWtWords + waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * waves));
@@ -499,8 +525,12 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
     a.maps = maps;
     a.W = pred->weights;
     a.b = pred->bias;
-    if (l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, false, true><<<grid, block, lds, stream>>>(a);
-    else l3::linear3d_kernel<T, false, false><<<grid, block, lds, stream>>>(a);
+    if (!l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, false, false, false, 1><<<grid, block, lds, stream>>>(a);
+    else if (a.full && true && l3_env("KMP_L3_WPE", 5) == 5)
+      l3::linear3d_kernel<T, false, true, true, 5, true><<<grid, block, lds, stream>>>(a);
+    else if (a.full && true) l3::linear3d_kernel<T, false, true, true, 1, true><<<grid, block, lds, stream>>>(a);
+    else if (a.full) l3::linear3d_kernel<T, false, true, true, 5><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, false, true, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -524,8 +554,12 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
     a.W = pred->weights;
     a.b = pred->bias;
     a.uld = l3_env("KMP_L3_ULD", 1) && a.Lcz > 0 && a.Lcy > 0;  // clamped map planes / rows exist
-    if (l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, true, true><<<grid, block, lds, stream>>>(a);
-    else l3::linear3d_kernel<T, true, false><<<grid, block, lds, stream>>>(a);
+    if (!l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, true, false, false, 1><<<grid, block, lds, stream>>>(a);
+    else if (a.full && a.uld && l3_env("KMP_L3_WPE", 5) == 5)
+      l3::linear3d_kernel<T, true, true, true, 5, true><<<grid, block, lds, stream>>>(a);
+    else if (a.full && a.uld) l3::linear3d_kernel<T, true, true, true, 1, true><<<grid, block, lds, stream>>>(a);
+    else if (a.full) l3::linear3d_kernel<T, true, true, true, 5><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, true, true, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_decode");
   }
   return KMP_ERR_UNSUPPORTED;

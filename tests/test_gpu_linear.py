@@ -113,14 +113,20 @@ def test_linear_fused_p1(kom, shape, variant, monkeypatch):
 @pytest.mark.parametrize('shape,dtype', [((4, 64, 64, 64, 1), np.uint16), ((2, 17, 30, 16, 1), np.uint16),
                                          ((2, 12, 33, 32, 1), np.uint16), ((1, 9, 14, 128, 1), np.uint8),
                                          ((3, 10, 9, 64, 1), np.uint8)])
-@pytest.mark.parametrize('sg,uld', [('1', '1'), ('0', '1'), ('1', '0')])
-def test_linear_fused_p0(kom, shape, dtype, sg, uld, monkeypatch):
+@pytest.mark.parametrize('sg,uld,full,wpe', [('1', '1', '1', '5'), ('1', '1', '1', '4'), ('1', '1', '0', '5'),
+                                              ('0', '1', '1', '5'), ('1', '0', '1', '5')])
+def test_linear_fused_p0(kom, shape, dtype, sg, uld, full, wpe, monkeypatch):
     """The fused LinearPredictor p = 0 volume kernel (kmp_codec_linear3d.hip) with each weight
-    source -- uniform (scalar) loads from W / b (KMP_L3_SGPR=1, default) or the LDS copy (0) -- and
-    with the decode's unconditional (KMP_L3_ULD=1, default) or guarded loads:
-    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, chunked."""
+    source -- uniform (scalar) loads from W / b (KMP_L3_SGPR=1, default) or the LDS copy (0) --,
+    with the decode's unconditional (KMP_L3_ULD=1, default) or guarded loads, and with the FULL
+    body (even y / x: only row-0 / lane-0 masks, missing z planes through zero weights; 5 or 4 waves
+    per SIMD) or the general one (KMP_L3_FULL=0): residuals and lowres bit-exact to the oracle's fma
+    chain + aggregation, lossless, chunked.  The shapes cover FULL with an odd depth (the last output
+    plane has no cell plane c: zero weights for P) and the general body (odd heights)."""
     monkeypatch.setenv('KMP_L3_SGPR', sg)
     monkeypatch.setenv('KMP_L3_ULD', uld)
+    monkeypatch.setenv('KMP_L3_FULL', full)
+    monkeypatch.setenv('KMP_L3_WPE', wpe)
     hi = _data(shape, dtype, 9)
     w, b = _weights(3, 0, 10, dtype)
     pred = kom.LinearPredictor(w, b, 0, 3)

@@ -4,6 +4,8 @@
 // 2. split8: read 256 MiB at 16 B/lane, write 8 output streams of 32 MiB at 8 B/lane per lane
 //    (the fused encode's store shape), one 2x2x2 block class per stream
 // 3. merge8: the inverse (decode's shape)
+// ./tools/probe_bw c2: only the C2-sized probes -- 64 MiB -> 64 MiB copies alternating X -> M and
+//    M -> R like bench.py's encode / decode pairs (the 192 MiB working set fits the 256 MiB MALL)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -42,6 +44,19 @@ __global__ void split16(const u32x4* __restrict__ a, u32x4* __restrict__ out, in
     const int64_t o = (row >> 2) * 256 + col;
     __builtin_nontemporal_store(v0, out + (int64_t)s * per + o);
     __builtin_nontemporal_store(v1, out + (int64_t)(s + 4) * per + o);
+  }
+}
+
+// merge16: the inverse of split16 (a decode lane reading 16 B of each map row)
+__global__ void merge16(const u32x4* __restrict__ in, u32x4* __restrict__ b, int64_t n2, int64_t per) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / 256, col = i % 256;
+    const int s = row & 3;
+    const int64_t o = (row >> 2) * 256 + col;
+    const u32x4 v0 = __builtin_nontemporal_load(in + (int64_t)s * per + o);
+    const u32x4 v1 = __builtin_nontemporal_load(in + (int64_t)(s + 4) * per + o);
+    __builtin_nontemporal_store(v0, b + (row * 512 + col));
+    __builtin_nontemporal_store(v1, b + (row * 512 + 256 + col));
   }
 }
 
@@ -120,7 +135,83 @@ __global__ void __launch_bounds__(256) codec_shape(const uint16_t* __restrict__ 
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'c') {  // C2- (64 MiB) or C3-sized (256 MiB: "c3") ceilings
+    const bool c3 = argv[1][1] == '3';
+    const size_t sb = (c3 ? 256ull : 64ull) << 20;
+    void *x, *m, *r;
+    hipMalloc(&x, sb);
+    hipMalloc(&m, sb);
+    hipMalloc(&r, sb);
+    hipMemset(x, 1, sb);
+    hipMemset(m, 2, sb);
+    hipMemset(r, 3, sb);
+    hipEvent_t t0, t1;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    for (int blocks : {1024, 2048, 4096, 8192, 16384}) {
+      for (int alt : {0, 1}) {
+        auto pair = [&] {
+          copy16<<<blocks, 256>>>((const u32x4*)x, (u32x4*)m, sb / 16);
+          copy16<<<blocks, 256>>>((const u32x4*)(alt ? m : x), (u32x4*)(alt ? r : m), sb / 16);
+        };
+        for (int w = 0; w < 3; ++w) pair();
+        hipEventRecord(t0);
+        const int reps = 50;
+        for (int i = 0; i < reps; ++i) pair();
+        hipEventRecord(t1);
+        hipEventSynchronize(t1);
+        float ms;
+        hipEventElapsedTime(&ms, t0, t1);
+        const double us = ms * 1e3 / (2 * reps);
+        printf("%s copy16 %s grid=%-6d %7.1f us per copy  %7.0f GB/s (read+write %zu MiB)\n", c3 ? "c3" : "c2",
+               alt ? "X->M, M->R" : "X->M twice", blocks, us, 2.0 * sb / (us * 1e3), 2 * (sb >> 20));
+      }
+    }
+    if (c3) {  // the codec's store / load shapes, alternating like bench.py: split8 X->M, merge8 M->R
+      const int64_t n16 = sb / 16, per = n16 / 4;
+      for (int shape = 0; shape < 2; ++shape)
+      for (int blocks : {4096, 8192, 16384}) {
+        auto enc = [&] {
+          if (shape) split16<<<blocks, 256>>>((const u32x4*)x, (u32x4*)m, n16 / 2, n16 / 8);
+          else split8<<<blocks, 256>>>((const u32x4*)x, (u32x2*)m, n16, per);
+        };
+        auto dec = [&] {
+          if (shape) merge16<<<blocks, 256>>>((const u32x4*)m, (u32x4*)r, n16 / 2, n16 / 8);
+          else merge8<<<blocks, 256>>>((const u32x2*)m, (u32x4*)r, n16, per);
+        };
+        auto pair = [&] {
+          enc();
+          dec();
+        };
+        for (int w = 0; w < 3; ++w) pair();
+        hipEvent_t ev[41];
+        for (auto& e : ev) hipEventCreate(&e);
+        hipEventRecord(ev[0]);
+        for (int i = 0; i < 20; ++i) {  // an event between every two launches: per-direction times
+          enc();
+          hipEventRecord(ev[2 * i + 1]);
+          dec();
+          hipEventRecord(ev[2 * i + 2]);
+        }
+        hipEventSynchronize(ev[40]);
+        double se = 0, sd = 0;
+        for (int i = 0; i < 20; ++i) {
+          float a, b;
+          hipEventElapsedTime(&a, ev[2 * i], ev[2 * i + 1]);
+          hipEventElapsedTime(&b, ev[2 * i + 1], ev[2 * i + 2]);
+          se += a;
+          sd += b;
+        }
+        se *= 1e3 / 20;
+        sd *= 1e3 / 20;
+        printf("c3 %s grid=%-6d %7.1f / %7.1f us  %7.0f / %7.0f GB/s (read+write %zu MiB)\n",
+               shape ? "split16 X->M / merge16 M->R" : "split8 X->M / merge8 M->R", blocks,
+               se, sd, 2.0 * sb / (se * 1e3), 2.0 * sb / (sd * 1e3), 2 * (sb >> 20));
+      }
+    }
+    return 0;
+  }
   const size_t bytes = 256ull << 20;
   const int64_t n16 = bytes / 16;
   void *a, *b;
