@@ -227,6 +227,18 @@ int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
                                 const int32_t dims[3], const void* const preds[7], void* highres_out,
                                 kmp_stream_t stream);
 
+/* The two above with the prediction maps' dtype given separately: ``pred_dtype`` is the sample
+   dtype or KMP_F32 -- a network's float32 output, which the reference's coders read as
+   jnp.int32(pred) (truncating; out-of-range saturates here), utils.py:28-55. */
+int kmp_encode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder, int32_t pred_dtype,
+                                      const void* highres, int64_t B, const int64_t shape[3], int64_t C,
+                                      const void* const preds[7], void* lowres_out, void* const maps_out[7],
+                                      kmp_stream_t stream);
+int kmp_decode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder, int32_t pred_dtype,
+                                      const void* lowres, const void* const maps[7], int64_t B, const int64_t shape[3],
+                                      int64_t C, const int32_t dims[3], const void* const preds[7], void* highres_out,
+                                      kmp_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Bit-plane container payload (kmp_pack.hip; SURVEY.md §8f f-3 -- no reference counterpart, */
 /* the reference returns the residual arrays unreduced, volume/encode_decode.py:56; format    */

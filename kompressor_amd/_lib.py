@@ -102,6 +102,10 @@ _PROTOS = {
     'kmp_rice_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
                                                    _vp, _vp]),
+    'kmp_encode_with_predictions_typed': (ctypes.c_int, [_i32, _i32, _i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp,
+                                                         _vpp, _vp]),
+    'kmp_decode_with_predictions_typed': (ctypes.c_int, [_i32, _i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64,
+                                                         _i32p, _vpp, _vp, _vp]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

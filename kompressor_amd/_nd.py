@@ -375,14 +375,19 @@ def d_window_from_lowres(lo, dims, padding, nsp):
 
 
 def _preds_fit(preds, dtype, B, L, ch, nsp):
-    """True when predictions_fn's maps can feed the fused coder kernels directly: contiguous
-    device tensors of the sample dtype in the untrimmed map shapes."""
+    """The prediction maps' dtype code when predictions_fn's maps can feed the fused coder kernels
+    directly -- contiguous device tensors in the untrimmed map shapes, all of the sample dtype or all
+    float32 (a network's output, which the coder reads as ``jnp.int32(pred)``, utils.py:28-55) --
+    else None."""
+    pdt = preds[0].dtype if isinstance(preds[0], torch.Tensor) else None
+    if pdt not in (dtype, torch.float32):
+        return None
     for m, par in zip(preds, PARITY[nsp]):
         want = (B, *[(l - 1 if p else l) for l, p in zip(L, par)], *ch)
-        if not (isinstance(m, torch.Tensor) and m.is_cuda and m.dtype == dtype and m.is_contiguous()
+        if not (isinstance(m, torch.Tensor) and m.is_cuda and m.dtype == pdt and m.is_contiguous()
                 and tuple(m.shape) == want):
-            return False
-    return True
+            return None
+    return dev.dtype_code(preds[0])
 
 
 def _workspace(nbytes):
@@ -531,12 +536,14 @@ def encode(predictions_fn, encode_fn, highres, padding, nsp):
             validate_lowres_shape((h.shape[0], *L, *_ch(h.shape, nsp)), nsp)
             with _trace.stage('kmp.predictions_fn'):
                 pred_maps = _callback_maps(predictions_fn(d_window_from_highres(h, padding, nsp)), nsp)
-            if _preds_fit(pred_maps, h.dtype, h.shape[0], L, _ch(h.shape, nsp), nsp):
+            pdt = _preds_fit(pred_maps, h.dtype, h.shape[0], L, _ch(h.shape, nsp), nsp)
+            if pdt is not None:
                 lowres, encoded, dims = _alloc_encoded(h, coder, nsp)
-                check(lib.kmp_encode_with_predictions(nsp, dev.dtype_code(h), coder, h.data_ptr(), h.shape[0],
-                                                      _lib.i64x3(_sp(h.shape, nsp)), _C(h.shape, nsp),
-                                                      _lib.ptrs(pred_maps), lowres.data_ptr(), _lib.ptrs(encoded),
-                                                      dev.stream()), 'encode_with_predictions')
+                check(lib.kmp_encode_with_predictions_typed(nsp, dev.dtype_code(h), coder, pdt, h.data_ptr(),
+                                                            h.shape[0], _lib.i64x3(_sp(h.shape, nsp)),
+                                                            _C(h.shape, nsp), _lib.ptrs(pred_maps), lowres.data_ptr(),
+                                                            _lib.ptrs(encoded), dev.stream()),
+                      'encode_with_predictions')
                 return (dev.from_device(lowres, kind),
                         (tuple(dev.from_device(m, kind) for m in encoded), tuple(dims)))
         else:
@@ -577,13 +584,14 @@ def decode(predictions_fn, decode_fn, lowres, encoded, padding, nsp):
         L = [e + d for e, d in zip(_sp(lo.shape, nsp), dims)]
         with _trace.stage('kmp.predictions_fn'):
             pred_maps = _callback_maps(predictions_fn(d_window_from_lowres(lo, dims, padding, nsp)), nsp)
-        if _preds_fit(pred_maps, lo.dtype, lo.shape[0], L, _ch(lo.shape, nsp), nsp):
+        pdt = _preds_fit(pred_maps, lo.dtype, lo.shape[0], L, _ch(lo.shape, nsp), nsp)
+        if pdt is not None:
             lo = lo.contiguous()
             out = dev.empty((lo.shape[0], *[2 * l - 1 - d for l, d in zip(L, dims)], *_ch(lo.shape, nsp)), lo.dtype)
-            check(lib.kmp_decode_with_predictions(nsp, dev.dtype_code(lo), coder, lo.data_ptr(), _lib.ptrs(maps),
-                                                  lo.shape[0], _lib.i64x3(_sp(lo.shape, nsp)), _C(lo.shape, nsp),
-                                                  _lib.i32xn(dims), _lib.ptrs(pred_maps), out.data_ptr(),
-                                                  dev.stream()), 'decode_with_predictions')
+            check(lib.kmp_decode_with_predictions_typed(nsp, dev.dtype_code(lo), coder, pdt, lo.data_ptr(),
+                                                        _lib.ptrs(maps), lo.shape[0], _lib.i64x3(_sp(lo.shape, nsp)),
+                                                        _C(lo.shape, nsp), _lib.i32xn(dims), _lib.ptrs(pred_maps),
+                                                        out.data_ptr(), dev.stream()), 'decode_with_predictions')
             return dev.from_device(out, kind)
     lo_p = d_pad_lowres(lo, dims, nsp)
     maps_p = d_pad_maps(maps, dims, nsp)

@@ -131,7 +131,7 @@ static MapExt map_exts(const Geo& g, int nsp) {
 
 // 32-bit index versions (every array below 2^31 elements), C == 1: one output block per thread,
 // x fastest, the 2^d highres block addressed from one base.
-template <typename T, int CODER, bool DEC, int NM>
+template <typename T, int CODER, bool DEC, int NM, typename P = T>
 __global__ void __launch_bounds__(kThreads) code_preds_kernel32(const T* __restrict__ src, CMapPtrs maps_in,
                                                               MapPtrs maps_out, CMapPtrs preds, T* __restrict__ dst,
                                                               MapExt me, int32_t n0, int32_t n1, int32_t n2,
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(kThreads) code_preds_kernel32(const T* __restr
       const int32_t* u = me.u[k];
       const int32_t* par = me.par[k];
       const int32_t hidx = hbase + (par[0] * n1 + par[1]) * n2 + par[2];
-      const T pred = ((const T*)preds.p[k])[((b * u[0] + oz) * u[1] + oy) * u[2] + ox];
+      const P pred = ((const P*)preds.p[k])[((b * u[0] + oz) * u[1] + oy) * u[2] + ox];
       const int32_t midx = ((b * e[0] + oz) * e[1] + oy) * e[2] + ox;
       if constexpr (DEC) {
         const TO enc = ((const TO*)maps_in.p[k])[midx];
@@ -176,7 +176,28 @@ __host__ __device__ constexpr int class_index(int nsp, int pz, int py, int px) {
                     : (py ? (px ? 2 : 0) : 1);
 }
 
-template <typename T, int CODER, bool DEC, int NSP>
+// One item's prediction row: V = 16 / sizeof(T) values of the prediction dtype P (the sample
+// dtype: one 16-byte access; float32: sizeof(P) / sizeof(T) of them), as int32 the way the
+// reference's coder reads its operand (jnp.int32: floats truncate, saturating)
+template <typename T, typename P>
+__device__ __forceinline__ void load_pred_row(const P* p, int32_t nv, int32_t (&out)[Vec16<T>::V]) {
+  constexpr int V = Vec16<T>::V, VP = Vec16<P>::V;
+  static_assert(V % VP == 0, "whole 16-byte prediction chunks");
+  if (nv == V) {
+#pragma unroll
+    for (int c = 0; c < V / VP; ++c) {
+      Vec16<P> v;
+      v.load(p + c * VP);
+#pragma unroll
+      for (int i = 0; i < VP; ++i) out[c * VP + i] = to_i32(v.e[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] = i < nv ? to_i32(p[i]) : 0;
+  }
+}
+
+template <typename T, int CODER, bool DEC, int NSP, typename P = T>
 __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __restrict__ src, CMapPtrs maps_in,
                                                                  MapPtrs maps_out, CMapPtrs preds, T* __restrict__ dst,
                                                                  MapExt me, int32_t n0, int32_t n1, int32_t n2,
@@ -238,10 +259,11 @@ __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __re
             }
           }
           auto code_row = [&](int k, int32_t nv, const Vec16<T>& gt) {
-            Vec16<T> pr, res;
-            load_row((const T*)preds.p[k] + pred_off(k), nv, pr);
+            Vec16<T> res;
+            int32_t pr[V];
+            load_pred_row<T, P>((const P*)preds.p[k] + pred_off(k), nv, pr);
 #pragma unroll
-            for (int i = 0; i < V; ++i) res.e[i] = (T)code_encode<CODER>(to_i32(pr.e[i]), to_i32(gt.e[i]));
+            for (int i = 0; i < V; ++i) res.e[i] = (T)code_encode<CODER>(pr[i], to_i32(gt.e[i]));
             store_row((T*)maps_out.p[k] + cls_off(k), nv, res);
           };
           if (nx0 > 0) {
@@ -251,11 +273,12 @@ __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __re
           if (nx1 > 0) code_row(k1, nx1, od);
         } else {
           auto decode_row = [&](int k, int32_t nv, Vec16<T>& outv) {
-            Vec16<T> pr, en;
-            load_row((const T*)preds.p[k] + pred_off(k), nv, pr);
+            Vec16<T> en;
+            int32_t pr[V];
+            load_pred_row<T, P>((const P*)preds.p[k] + pred_off(k), nv, pr);
             load_row((const T*)maps_in.p[k] + cls_off(k), nv, en);
 #pragma unroll
-            for (int i = 0; i < V; ++i) outv.e[i] = (T)code_decode<CODER>(to_i32(pr.e[i]), to_i32((TO)en.e[i]));
+            for (int i = 0; i < V; ++i) outv.e[i] = (T)code_decode<CODER>(pr[i], to_i32((TO)en.e[i]));
           };
           Vec16<T> ev, od;
           if (nx0 > 0) {
@@ -284,7 +307,7 @@ __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __re
   }
 }
 
-template <typename T, int CODER>
+template <typename T, int CODER, typename P = T>
 __global__ void __launch_bounds__(kThreads) encode_preds_kernel(const T* __restrict__ hi, Geo g, int nsp, int64_t C,
                                                               CMapPtrs preds, T* __restrict__ lowres, MapPtrs maps,
                                                               int64_t total) {
@@ -303,14 +326,14 @@ __global__ void __launch_bounds__(kThreads) encode_preds_kernel(const T* __restr
       int64_t u[3], e[3];
       map_ext(g, nsp, k, u, e);
       if (oz >= e[0] || oy >= e[1] || ox >= e[2]) continue;
-      const T pred = ((const T*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
+      const P pred = ((const P*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
       ((TO*)maps.p[k])[(((b * e[0] + oz) * e[1] + oy) * e[2] + ox) * C + c] =
           code_encode<CODER>(to_i32(pred), to_i32(hv(par[0], par[1], par[2])));
     }
   }
 }
 
-template <typename T, int CODER>
+template <typename T, int CODER, typename P = T>
 __global__ void __launch_bounds__(kThreads) decode_preds_kernel(const T* __restrict__ lowres, CMapPtrs maps, Geo g,
                                                               int nsp, int64_t C, CMapPtrs preds, T* __restrict__ hi,
                                                               int64_t total) {
@@ -329,7 +352,7 @@ __global__ void __launch_bounds__(kThreads) decode_preds_kernel(const T* __restr
       int64_t u[3], e[3];
       map_ext(g, nsp, k, u, e);
       if (oz >= e[0] || oy >= e[1] || ox >= e[2]) continue;
-      const T pred = ((const T*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
+      const P pred = ((const P*)preds.p[k])[(((b * u[0] + oz) * u[1] + oy) * u[2] + ox) * C + c];
       const TO enc = ((const TO*)maps.p[k])[(((b * e[0] + oz) * e[1] + oy) * e[2] + ox) * C + c];
       hout(par[0], par[1], par[2]) = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
     }
@@ -344,6 +367,15 @@ static int dispatch_coder(int dtype, int coder, F&& f) {  // the built-in coder 
   if (dtype == KMP_U32 && coder == KMP_CODER_U32) return f(uint32_t{}, std::integral_constant<int, KMP_CODER_U32>{});
   return fail(KMP_ERR_UNSUPPORTED, "callback coder kernels support (uint8, U8), (uint16, U16), (int32, RAW), "
                                    "(uint32, U32); got dtype " + std::to_string(dtype) + " coder " + std::to_string(coder));
+}
+
+// the prediction maps' dtype: the sample dtype itself, or float32 (a network's output)
+template <typename T, typename F>
+static int dispatch_pred(int dtype, int pred_dtype, F&& f) {
+  if (pred_dtype == dtype) return f(T{});
+  if (pred_dtype == KMP_F32) return f(float{});
+  return fail(KMP_ERR_UNSUPPORTED, "prediction maps must have the sample dtype or float32; got dtype " +
+                                       std::to_string(pred_dtype));
 }
 
 static int window_launch(int nsp, int dtype, const void* src, int mult, const int64_t* S, int64_t B, int64_t C,
@@ -405,6 +437,14 @@ int kmp_window_from_lowres(int32_t nsp, int32_t dtype, const void* lowres, int64
 int kmp_encode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const void* highres, int64_t B,
                                 const int64_t shape[3], int64_t C, const void* const preds[7], void* lowres_out,
                                 void* const maps_out[7], kmp_stream_t stream) {
+  return kmp_encode_with_predictions_typed(nsp, dtype, coder, dtype, highres, B, shape, C, preds, lowres_out, maps_out,
+                                           stream);
+}
+
+int kmp_encode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder, int32_t pred_dtype,
+                                      const void* highres, int64_t B, const int64_t shape[3], int64_t C,
+                                      const void* const preds[7], void* lowres_out, void* const maps_out[7],
+                                      kmp_stream_t stream) {
   KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
   KMP_REQUIRE(highres && shape && preds && lowres_out && maps_out && B >= 0 && C >= 1, "bad argument");
   for (int a = 0; a < nsp; ++a) KMP_REQUIRE(shape[a] >= 2, "spatial dims must be >= 2");
@@ -421,26 +461,29 @@ int kmp_encode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
   const bool small = C == 1 && B * g.n[0] * g.n[1] * g.n[2] < ((int64_t)1 << 31) &&
                      B * g.L[0] * g.L[1] * g.L[2] < ((int64_t)1 << 31);
   return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
-    using T = decltype(tag);
-    constexpr int CODER = decltype(coder_c)::value;
+   using T = decltype(tag);
+   constexpr int CODER = decltype(coder_c)::value;
+   return cb::dispatch_pred<T>(dtype, pred_dtype, [&](auto ptag) {
+    using P = decltype(ptag);
     if (small && !std::getenv("KMP_DISABLE_ROWS")) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
-      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, false, 3> : cb::rows_code_preds_kernel<T, CODER, false, 2>;
+      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, false, 3, P> : cb::rows_code_preds_kernel<T, CODER, false, 2, P>;
       k<<<cb::grid_for(items), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)highres, CMapPtrs{}, mp, pp, (T*)lowres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
           (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)nch, (int32_t)items);
     } else if (small) {
       const cb::MapExt me = cb::map_exts(g, nsp);
-      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, false, 7> : cb::code_preds_kernel32<T, CODER, false, 3>;
+      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, false, 7, P> : cb::code_preds_kernel32<T, CODER, false, 3, P>;
       k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)highres, CMapPtrs{}, mp, pp, (T*)lowres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
           (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)total);
     } else {
-      cb::encode_preds_kernel<T, CODER><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+      cb::encode_preds_kernel<T, CODER, P><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)highres, g, nsp, C, pp, (T*)lowres_out, mp, total);
     }
     return check_launch("encode_with_predictions");
+   });
   });
 }
 
@@ -448,6 +491,14 @@ int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
                                 const void* const maps[7], int64_t B, const int64_t shape[3], int64_t C,
                                 const int32_t dims[3], const void* const preds[7], void* highres_out,
                                 kmp_stream_t stream) {
+  return kmp_decode_with_predictions_typed(nsp, dtype, coder, dtype, lowres, maps, B, shape, C, dims, preds,
+                                           highres_out, stream);
+}
+
+int kmp_decode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder, int32_t pred_dtype,
+                                      const void* lowres, const void* const maps[7], int64_t B, const int64_t shape[3],
+                                      int64_t C, const int32_t dims[3], const void* const preds[7], void* highres_out,
+                                      kmp_stream_t stream) {
   KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
   KMP_REQUIRE(lowres && maps && shape && dims && preds && highres_out && B >= 0 && C >= 1, "bad argument");
   for (int a = 0; a < nsp; ++a) {
@@ -466,26 +517,29 @@ int kmp_decode_with_predictions(int32_t nsp, int32_t dtype, int32_t coder, const
   const bool small = C == 1 && B * g.n[0] * g.n[1] * g.n[2] < ((int64_t)1 << 31) &&
                      B * g.L[0] * g.L[1] * g.L[2] < ((int64_t)1 << 31);
   return cb::dispatch_coder(dtype, coder, [&](auto tag, auto coder_c) {
-    using T = decltype(tag);
-    constexpr int CODER = decltype(coder_c)::value;
+   using T = decltype(tag);
+   constexpr int CODER = decltype(coder_c)::value;
+   return cb::dispatch_pred<T>(dtype, pred_dtype, [&](auto ptag) {
+    using P = decltype(ptag);
     if (small && !std::getenv("KMP_DISABLE_ROWS")) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
-      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, true, 3> : cb::rows_code_preds_kernel<T, CODER, true, 2>;
+      auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, true, 3, P> : cb::rows_code_preds_kernel<T, CODER, true, 2, P>;
       k<<<cb::grid_for(items), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)lowres, mp, MapPtrs{}, pp, (T*)highres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
           (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)nch, (int32_t)items);
     } else if (small) {
       const cb::MapExt me = cb::map_exts(g, nsp);
-      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, true, 7> : cb::code_preds_kernel32<T, CODER, true, 3>;
+      auto k = nsp == 3 ? cb::code_preds_kernel32<T, CODER, true, 7, P> : cb::code_preds_kernel32<T, CODER, true, 3, P>;
       k<<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)lowres, mp, MapPtrs{}, pp, (T*)highres_out, me, (int32_t)g.n[0], (int32_t)g.n[1],
           (int32_t)g.n[2], (int32_t)g.E[0], (int32_t)g.E[1], (int32_t)g.E[2], (int32_t)total);
     } else {
-      cb::decode_preds_kernel<T, CODER><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
+      cb::decode_preds_kernel<T, CODER, P><<<cb::grid_for(total), cb::kThreads, 0, (hipStream_t)stream>>>(
           (const T*)lowres, mp, g, nsp, C, pp, (T*)highres_out, total);
     }
     return check_launch("decode_with_predictions");
+   });
   });
 }
 

@@ -137,6 +137,70 @@ def test_reference_style_predictor(kom, name):
     assert torch.equal(rec.cpu(), hi.cpu())
 
 
+def float_predictions_fn(kom, padding, ndim, seen):
+    """A network-like predictor: float32 maps that are not integers -- fractional, negative, past
+    the sample range, and a few +-inf / NaN / beyond-int32 entries -- recorded in ``seen``."""
+    ns = _ns(kom, ndim)
+    k = 19 if ndim == 3 else 5
+
+    def fn(lowres):
+        features = ns.features_from_lowres(lowres, padding).to(torch.float32)
+        pred = torch.mean(features, dim=ndim + 1, keepdim=True) * 1.37 - 40.25
+        pred = pred.repeat_interleave(k, dim=ndim + 1)
+        pred = pred + torch.linspace(-3.7, 2.9, k, device=pred.device).reshape(
+            *([1] * (ndim + 1)), k, *([1] * (pred.dim() - ndim - 2)))
+        flat = pred.view(-1)
+        flat[::97] = float('nan')
+        flat[5::131] = float('inf')
+        flat[7::151] = -float('inf')
+        flat[11::173] = 3.5e9
+        flat[13::179] = -3.5e9
+        maps = ns.maps_from_predictions(pred.contiguous())
+        seen.append([m.cpu().numpy() for m in maps])
+        return maps
+
+    return fn
+
+
+@pytest.mark.parametrize('name', ['vol_rand_mixed_p1', 'vol_ramp_odd_p0', 'vol_rand_u8_c3_p1', 'vol_ramp_i32_raw_p0',
+                                  'img_rand_p2', 'img_ramp_even_p1', 'img_rand_u16_c2_p1', 'vol_tile_small_p0'])
+@pytest.mark.parametrize('rows', ['1', '0'])
+def test_callback_float32_predictions(kom, name, rows, monkeypatch):
+    """A predictions_fn returning float32 maps (what a trained network gives) with the built-in coder
+    stays on the fused callback coder (kmp_*_with_predictions_typed): residuals bit-exact to the
+    oracle's step sequence on the same maps (the coder reads jnp.int32(pred): truncating, saturating,
+    NaN -> 0), and lossless.  rows=0: the per-element kernel instead of the 16-byte row kernel."""
+    import oracle
+    if rows == '0':
+        monkeypatch.setenv('KMP_DISABLE_ROWS', '1')
+    else:
+        monkeypatch.delenv('KMP_DISABLE_ROWS', raising=False)
+    g = load_golden(name)
+    ndim, p = int(g['ndim']), int(g['padding'])
+    ns, ons = _ns(kom, ndim), (oracle.volume if ndim == 3 else oracle.image)
+    enc, dec = _coders(ns, g['coder'])
+    oenc = getattr(oracle.common, f"encode_values_{g['coder']}")
+    odec = getattr(oracle.common, f"decode_values_{g['coder']}")
+    seen = []
+    fn = float_predictions_fn(kom, p, ndim, seen)
+    hi = torch.from_numpy(g['highres']).cuda()
+    lowres, (maps, dims) = ns.encode(fn, enc, hi, padding=p)
+    assert kom._lib.lib.kmp_last_launch().decode() == 'encode_with_predictions'
+    assert seen[0][0].dtype == np.float32
+    want_lo, (want_maps, want_dims) = ons.encode(lambda w: seen[0], oenc, g['highres'], padding=p)
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lowres.cpu().numpy(), want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        a = a.cpu().numpy()
+        assert a.dtype == b.dtype and a.shape == b.shape, i
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    rec = ns.decode(fn, dec, lowres, (maps, dims), padding=p)
+    assert kom._lib.lib.kmp_last_launch().decode() == 'decode_with_predictions'
+    assert torch.equal(rec.cpu(), hi.cpu())
+    orec = ons.decode(lambda w: seen[1], odec, want_lo, (want_maps, want_dims), padding=p)
+    assert np.array_equal(orec, g['highres'])
+
+
 @pytest.mark.parametrize('name,chunk', [('vol_ramp_odd_p0', 6), ('vol_ramp_odd_p1', 11), ('vol_ramp_odd_p1', (6, 11, 11)),
                                         ('vol_ramp_even_p0', 6), ('vol_rand_mixed_p2', 7), ('vol_tile64_p0', 12),
                                         ('img_ramp_odd_p0', (6, 11)), ('img_ramp_even_p1', 6), ('img_rand_p2', 9)])

@@ -169,6 +169,24 @@ def main():
                  sub.numel() * 4, td)
             del lo, maps
 
+    # the callback path with float32 prediction maps (a network's output; the coder reads int32(pred)):
+    # the fused coder reads them directly (kmp_*_with_predictions_typed); '_steps' is the same call with
+    # an opaque coder, i.e. the reference's step sequence (what float32 maps ran as before)
+    if not want or 'volume_callback_f32' in want:
+        pred = kom.MeanPredictor(0, 3)
+        cbf = lambda lowres: [m.float() for m in pred(lowres)]  # noqa: E731
+        encs, decs = V.encode_values_uint16, V.decode_values_uint16
+        for tag, enc, dec in (('volume_callback_f32', encs, decs),
+                              ('volume_callback_f32_steps', lambda a, b: encs(a, b), lambda a, b: decs(a, b))):
+            lo, (maps, dims) = V.encode(cbf, enc, vol)
+            assert torch.equal(V.decode(cbf, dec, lo, (maps, dims)), vol), tag
+            te = gpu_time(lambda: V.encode(cbf, enc, vol), args.reps)
+            td = gpu_time(lambda: V.decode(cbf, dec, lo, (maps, dims)), args.reps)
+            what = 'fused coder' if tag == 'volume_callback_f32' else "the reference's step sequence"
+            emit(tag + ':encode', f'callback encode, 512 tiles, float32 prediction maps, {what}', vol.numel() * 4, te)
+            emit(tag + ':decode', f'callback decode, 512 tiles, float32 prediction maps, {what}', vol.numel() * 4, td)
+            del lo, maps
+
     # categorical rank coder (utils.py:58-111): 1M elements x 256 float32 logits
     if not want or 'categorical' in want:
         n, L = 1 << 20, 256
