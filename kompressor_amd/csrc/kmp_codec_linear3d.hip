@@ -44,7 +44,7 @@ struct L3 {
   int32_t txn, rows, nwv;
   int32_t xcd_per;
   int32_t uld;
-  int32_t full;  // Lcy == Ey and Lcx == Ex: interior planes take the FULL body
+  int32_t full;  // Lcy == Ey and Lcx == Ex: the FULL kernel serves the call
 };
 
 // astype(T) for u8/u16: trunc, saturate, NaN -> 0.  v_cvt_u32_f32 truncates and saturates to
@@ -114,8 +114,10 @@ __constant__ float kZeroWeights[8 * 19 + 19];
 // validity and every x validity but the row's first cell (X-1 = -1) are compile-time true, and a
 // missing cell plane (z) is zeroed at the source by reading its channels' weights from
 // kZeroWeights (uniform), so the aggregation masks only the row-above channels on row 0 and the
-// left cell on lane 0 of a row: 929 instead of 1 030 VALU instructions per encode wave, 93 instead
-// of 104 VGPRs (5 waves per SIMD instead of 4)
+// left cell on lane 0 of a row: 938 / 927 instead of 1 030 / 1 041 VALU instructions per encode /
+// decode wave, and 5 waves per SIMD (WPE = 5: 96 / 92 VGPRs, the encode with a 20-byte spill;
+// WPE = 4 measured the same, profiles/round2/ab_linear3d_full.log).  ULD: the decode's unconditional
+// loads compiled in (see there)
 template <typename T, bool DEC, bool SG, bool FULL, int WPE, bool ULD = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) linear3d_kernel(L3 a) {
   static_assert(!FULL || SG, "FULL reads the weights as scalars");
@@ -526,10 +528,9 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
     a.W = pred->weights;
     a.b = pred->bias;
     if (!l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, false, false, false, 1><<<grid, block, lds, stream>>>(a);
-    else if (a.full && true && l3_env("KMP_L3_WPE", 5) == 5)
-      l3::linear3d_kernel<T, false, true, true, 5, true><<<grid, block, lds, stream>>>(a);
-    else if (a.full && true) l3::linear3d_kernel<T, false, true, true, 1, true><<<grid, block, lds, stream>>>(a);
-    else if (a.full) l3::linear3d_kernel<T, false, true, true, 5><<<grid, block, lds, stream>>>(a);
+    else if (a.full && l3_env("KMP_L3_WPE", 5) == 5)
+      l3::linear3d_kernel<T, false, true, true, 5><<<grid, block, lds, stream>>>(a);
+    else if (a.full) l3::linear3d_kernel<T, false, true, true, 1><<<grid, block, lds, stream>>>(a);
     else l3::linear3d_kernel<T, false, true, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_encode");
   }
