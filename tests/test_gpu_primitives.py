@@ -178,3 +178,22 @@ def test_zero_width_pads_and_trims_return_fresh_tensors(kom):
             assert o.untyped_storage().data_ptr() != x.untyped_storage().data_ptr()
             o.view(torch.int16).fill_(7)
             assert torch.equal(x, keep), 'writing an output changed the input'
+
+
+def test_stream_handle_follows_torch_current_stream(kom):
+    """_device.stream() (the raw handle every C-ABI call gets) is torch's current stream, on the
+    default stream and inside a torch.cuda.stream context, and work launched there is ordered on it."""
+    from kompressor_amd import _device as dev
+    assert dev.stream() == torch.cuda.current_stream().cuda_stream
+    side = torch.cuda.Stream()
+    x = torch.from_numpy(np.random.default_rng(5).integers(0, 65536, (4, 16, 16, 16, 1), dtype=np.int64)
+                         .astype(np.uint16)).cuda()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        assert dev.stream() == side.cuda_stream == torch.cuda.current_stream().cuda_stream
+        pred = kom.MeanPredictor(0, 3)
+        lo, enc = kom.volume.encode(pred, kom.volume.encode_values_uint16, x)
+        rec = kom.volume.decode(pred, kom.volume.decode_values_uint16, lo, enc)
+    torch.cuda.current_stream().wait_stream(side)
+    assert torch.equal(rec, x)
+    assert dev.stream() == torch.cuda.current_stream().cuda_stream
