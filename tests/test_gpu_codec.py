@@ -255,6 +255,60 @@ def test_image_batch_round_trip_full_size(kom):
     assert torch.equal(rec, img)
 
 
+@pytest.mark.parametrize('ndim,padding', [(3, 0), (3, 1), (2, 0), (2, 2)])
+def test_empty_batch_is_rejected_like_the_reference(kom, ndim, padding):
+    """A batch of zero tiles: the reference's validators reject it (``assert np.prod(shape) > 0``,
+    volume/utils.py:284-303, image/utils.py:201-218) and so does every path here -- fused and
+    callback, encode and decode, numpy and CUDA inputs -- with AssertionError, before any launch."""
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = _ns(kom, ndim), (oracle.volume if ndim == 3 else oracle.image)
+    shape = (0, 9, 13, 17, 1) if ndim == 3 else (0, 13, 17, 1)
+    lo_shape = (0, 5, 7, 9, 1) if ndim == 3 else (0, 7, 9, 1)
+    x = np.zeros(shape, np.uint16)
+    with pytest.raises(AssertionError):
+        ons.encode(OP.mean_predictions_fn(padding, ndim), ons.encode_values_uint16, x, padding=padding)
+    mean = kom.MeanPredictor(padding, ndim)
+    for pred in (mean, lambda w: mean(w)):
+        for arr in (x, torch.from_numpy(x).cuda()):
+            with pytest.raises(AssertionError):
+                ns.encode(pred, ns.encode_values_uint16, arr, padding=padding)
+        lo = torch.zeros(lo_shape, dtype=torch.uint16, device='cuda')
+        with pytest.raises(AssertionError):
+            ns.decode(pred, ns.decode_values_uint16, lo, ([lo] * (7 if ndim == 3 else 3), (0,) * ndim),
+                      padding=padding)
+
+
+@pytest.mark.parametrize('ndim', [3, 2])
+def test_batch_past_int32_elements(kom, ndim):
+    """More than 2^31 samples in one call (17 tiles of 512^3 uint16; 33 000 images of 256^2 uint8):
+    the batch offsets are 64-bit.  Lossless, and the last tile -- past element 2^31 -- codes exactly
+    as it does alone (single tiles are pinned to the oracle by the golden tests)."""
+    ns = _ns(kom, ndim)
+    if ndim == 3:
+        B, tile, dt, enc, dec = 17, (512, 512, 512, 1), torch.uint16, ns.encode_values_uint16, ns.decode_values_uint16
+        hi = 65536
+    else:
+        B, tile, dt, enc, dec = 33000, (256, 256, 1), torch.uint8, ns.encode_values_uint8, ns.decode_values_uint8
+        hi = 256
+    x = torch.empty((B, *tile), dtype=dt, device='cuda')
+    g = torch.Generator(device='cuda').manual_seed(7)
+    step = 1 if ndim == 3 else 4096
+    for i in range(0, B, step):  # int32 draws a chunk at a time (the uint16 / uint8 batch is 4.6 / 2.2 GB)
+        x[i:i + step] = torch.randint(0, hi, (min(step, B - i), *tile), generator=g, dtype=torch.int32,
+                                      device='cuda').to(dt)
+    assert x.numel() > (1 << 31)
+    pred = kom.MeanPredictor(0, ndim)
+    lo, (maps, dims) = ns.encode(pred, enc, x)
+    lo1, (maps1, dims1) = ns.encode(pred, enc, x[B - 1:].clone())
+    assert tuple(dims) == tuple(dims1) and torch.equal(lo[B - 1:], lo1)
+    for m, m1 in zip(maps, maps1):
+        assert torch.equal(m[B - 1:], m1)
+    del lo1, maps1
+    rec = ns.decode(pred, dec, lo, (maps, dims))
+    assert torch.equal(rec, x)
+
+
 def categorical_predictions_fn(kom, logits, padding, ndim):
     """tests/volume/test_encode_decode.py:57-75 with the fixture's logits: constant logits tiled
     over every cell, maps_from_predictions (HIP, float32), softmax (torch)."""
