@@ -280,10 +280,13 @@ def test_empty_batch_is_rejected_like_the_reference(kom, ndim, padding):
 
 
 @pytest.mark.parametrize('ndim', [3, 2])
-def test_batch_past_int32_elements(kom, ndim):
+@pytest.mark.parametrize('path', ['fused', 'callback'])
+def test_batch_past_int32_elements(kom, ndim, path):
     """More than 2^31 samples in one call (17 tiles of 512^3 uint16; 33 000 images of 256^2 uint8):
-    the batch offsets are 64-bit.  Lossless, and the last tile -- past element 2^31 -- codes exactly
-    as it does alone (single tiles are pinned to the oracle by the golden tests)."""
+    the batch offsets are 64-bit, on the fused kernels and on the callback path (window gather, an
+    opaque predictions_fn, the coder kernels' 64-bit form).  Lossless, and the last tile -- past
+    element 2^31 -- codes exactly as it does alone (single tiles are pinned to the oracle by the
+    golden tests)."""
     ns = _ns(kom, ndim)
     if ndim == 3:
         B, tile, dt, enc, dec = 17, (512, 512, 512, 1), torch.uint16, ns.encode_values_uint16, ns.decode_values_uint16
@@ -298,8 +301,10 @@ def test_batch_past_int32_elements(kom, ndim):
         x[i:i + step] = torch.randint(0, hi, (min(step, B - i), *tile), generator=g, dtype=torch.int32,
                                       device='cuda').to(dt)
     assert x.numel() > (1 << 31)
-    pred = kom.MeanPredictor(0, ndim)
+    mean = kom.MeanPredictor(0, ndim)
+    pred = mean if path == 'fused' else (lambda w: mean(w))
     lo, (maps, dims) = ns.encode(pred, enc, x)
+    assert (kom._lib.lib.kmp_last_launch().decode() == 'encode_with_predictions') == (path == 'callback')
     lo1, (maps1, dims1) = ns.encode(pred, enc, x[B - 1:].clone())
     assert tuple(dims) == tuple(dims1) and torch.equal(lo[B - 1:], lo1)
     for m, m1 in zip(maps, maps1):
