@@ -41,8 +41,7 @@ struct W2 {
 
 template <typename T>
 __device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: trunc, saturate, NaN -> 0
-  constexpr float hi = sizeof(T) == 2 ? 65535.0f : 255.0f;
-  return (uint32_t)fminf(fmaxf(v, 0.0f), hi);
+  return cvt_sat<T>(v);  // saturating v_cvt_u32_f32 + integer min (kmp_wave.h)
 }
 
 // LIN: the LinearPredictor with p = 0 instead of the mean (image/utils.py:58-86 on its 5
