@@ -63,8 +63,20 @@ struct OutRows {
   uint2 mv[7];
 };
 
+// Store policy (STC): default-policy stores allocate in the MALL, non-temporal ones stream past it.
+// The encode's lowres and maps are what the next kernel reads (a decode, a pack, a copy to the
+// host), so by default they are stored cached: at C3 the following decode reads part of its 256 MiB
+// of maps from the MALL (decode 90.7 -> 85.2 us, encode unchanged; profiles/round2/ab_wave3d_store_policy.log).
+// The decode's highres stays non-temporal: cached, its dirty lines drain during the next encode
+// (+7 us).  KMP_W3_ST_ENC=0 restores the non-temporal encode stores.
+template <bool STC>
+__device__ __forceinline__ void stp8(void* p, uint2 v) {
+  if constexpr (STC) *(uint2*)p = v;
+  else st8(p, v);
+}
+
 // WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
-template <typename T, bool DEC, int PL, bool ONE>
+template <typename T, bool DEC, int PL, bool ONE, bool STC>
 __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -324,7 +336,7 @@ __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
       }
       KMP_SPAN((const T*)a.lo_out, (const T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, VX,
                a.nB * a.Ez * lplane);
-      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
+      stp8<STC>((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         int par[3];
@@ -332,7 +344,7 @@ __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
         if (mok_y[k] && (!par[0] || vz1)) {
           KMP_SPAN((const T*)a.maps.p[k], mbase[k] + c * mplane[k], VX,
                    a.nB * (par[0] ? a.Lcz : a.Ez) * mplane[k]);
-          st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+          stp8<STC>((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
         }
       }
     } else {
@@ -359,9 +371,9 @@ __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
 
 // A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; gridDim a multiple
 // of 8 keeps each virtual block on the XCD the tile-per-XCD order gives it)
-template <typename T, bool DEC, int PL, int WPE, bool ONE>
+template <typename T, bool DEC, int PL, int WPE, bool ONE, bool STC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
-  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave3d_plane_body<T, DEC, PL, ONE>(a, v);
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave3d_plane_body<T, DEC, PL, ONE, STC>(a, v);
 }
 
 }  // namespace w3
@@ -421,18 +433,25 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   return nblk < ((int64_t)1 << 31);
 }
 
-template <typename T, bool DEC>
-static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
+template <typename T, bool DEC, bool STC>
+static void launch_wave3d_s(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
   // PL = 2 at 3 waves / SIMD is the measured optimum at C3 (profiles/round1/kprof_wave3d.log):
   // PL = 1 re-reads twice the z halo per output plane; forcing 4 waves / SIMD spills
   if (a.rows == 1) {  // 64 lanes per output row (wide volumes): both halo rows per lane
-    if (pl == 1) w3::wave3d_plane_kernel<T, DEC, 1, 4, true><<<grid, block, 0, stream>>>(a);
-    else w3::wave3d_plane_kernel<T, DEC, 2, 3, true><<<grid, block, 0, stream>>>(a);
+    if (pl == 1) w3::wave3d_plane_kernel<T, DEC, 1, 4, true, STC><<<grid, block, 0, stream>>>(a);
+    else w3::wave3d_plane_kernel<T, DEC, 2, 3, true, STC><<<grid, block, 0, stream>>>(a);
   } else if (pl == 1) {
-    w3::wave3d_plane_kernel<T, DEC, 1, 4, false><<<grid, block, 0, stream>>>(a);
+    w3::wave3d_plane_kernel<T, DEC, 1, 4, false, STC><<<grid, block, 0, stream>>>(a);
   } else {
-    w3::wave3d_plane_kernel<T, DEC, 2, 3, false><<<grid, block, 0, stream>>>(a);
+    w3::wave3d_plane_kernel<T, DEC, 2, 3, false, STC><<<grid, block, 0, stream>>>(a);
   }
+}
+
+template <typename T, bool DEC>
+static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
+  // the decode's stores stay non-temporal; the encode's are cached unless KMP_W3_ST_ENC=0 (stp8)
+  if (!DEC && w3_env("KMP_W3_ST_ENC", 1)) launch_wave3d_s<T, DEC, true>(pl, grid, block, stream, a);
+  else launch_wave3d_s<T, DEC, false>(pl, grid, block, stream, a);
 }
 
 template <typename T>
