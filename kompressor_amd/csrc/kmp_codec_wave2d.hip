@@ -47,7 +47,7 @@ __device__ __forceinline__ uint32_t cast_t(float v) {  // astype(T) for u8/u16: 
 // LIN: the LinearPredictor with p = 0 instead of the mean (image/utils.py:58-86 on its 5
 // per-cell channels): pred[cell, k] = fma chain over the 4 nodes (n = dy*2 + dx) from b[k], cast
 // to T; LR = ch0 (x) + ch1 (x-1), UD = ch2 (y) + ch3 (y-1), C = ch4, with the same counts / shifts.
-template <typename T, bool DEC, bool ONE, bool LIN>
+template <typename T, bool DEC, bool ONE, bool LIN, bool STC>
 __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
@@ -226,10 +226,10 @@ __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
       res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;  // UD (0,1)
       res[2][i] = (el16<T>(o0, 2 * i + 1) - pred[2][i]) & MASK;   // C  (1,1)
     }
-    st8((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
-    if (vy1) st8((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
-    st8((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
-    if (vy1) st8((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+    stp8<STC>((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
+    if (vy1) stp8<STC>((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
+    stp8<STC>((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
+    if (vy1) stp8<STC>((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
   } else {
     uint32_t dv[3][VX];
 #pragma unroll
@@ -245,9 +245,9 @@ __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
 // A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; a multiple of 8
 // workgroups keeps every virtual block on the XCD of the image-per-XCD order): fewer, longer-lived
 // workgroups than one per 16 output rows (KMP_W2_ITERS virtual blocks per workgroup)
-template <typename T, bool DEC, bool ONE, bool LIN>
+template <typename T, bool DEC, bool ONE, bool LIN, bool STC = false>
 __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
-  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_body<T, DEC, ONE, LIN>(a, v);
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_body<T, DEC, ONE, LIN, STC>(a, v);
 }
 
 // uint8 form of the mean kernel (BASELINE config C2), SWAR: the lane's 8 cells travel as 4 words
@@ -462,19 +462,26 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   return nblk < ((int64_t)1 << 31);
 }
 
-template <typename T, bool DEC>
-static void launch_wave2d(bool one, bool lin, dim3 grid, dim3 block, hipStream_t s, const w2::W2& a) {
+template <typename T, bool DEC, bool STC>
+static void launch_wave2d_s(bool one, bool lin, dim3 grid, dim3 block, hipStream_t s, const w2::W2& a) {
   if (one) {
-    if (lin) w2::wave2d_kernel<T, DEC, true, true><<<grid, block, 0, s>>>(a);
-    else w2::wave2d_kernel<T, DEC, true, false><<<grid, block, 0, s>>>(a);
+    if (lin) w2::wave2d_kernel<T, DEC, true, true, STC><<<grid, block, 0, s>>>(a);
+    else w2::wave2d_kernel<T, DEC, true, false, STC><<<grid, block, 0, s>>>(a);
   } else {
-    if (lin) w2::wave2d_kernel<T, DEC, false, true><<<grid, block, 0, s>>>(a);
+    if (lin) w2::wave2d_kernel<T, DEC, false, true, STC><<<grid, block, 0, s>>>(a);
     // SWAR u8 form: decode 24.0 vs 24.8 us at C2 on one box; encode 26.2 vs 25.4 (kept behind a
     // knob: the encode is bound by its row loads, not VALU) -- profiles/round1/ab_wave2d_swar.log
     else if (std::is_same<T, uint8_t>::value && !w2_env("KMP_DISABLE_SWAR", 0) && (DEC || w2_env("KMP_W2_SWAR_ENC", 0)))
       w2::wave2d_u8_kernel<DEC><<<grid, block, 0, s>>>(a);
-    else w2::wave2d_kernel<T, DEC, false, false><<<grid, block, 0, s>>>(a);
+    else w2::wave2d_kernel<T, DEC, false, false, STC><<<grid, block, 0, s>>>(a);
   }
+}
+
+// the encode's lowres / map stores cached (stp8, kmp_wave.h) unless KMP_W2_ST_ENC=0
+template <typename T, bool DEC>
+static void launch_wave2d(bool one, bool lin, dim3 grid, dim3 block, hipStream_t s, const w2::W2& a) {
+  if (!DEC && w2_env("KMP_W2_ST_ENC", 1)) launch_wave2d_s<T, DEC, true>(one, lin, grid, block, s, a);
+  else launch_wave2d_s<T, DEC, false>(one, lin, grid, block, s, a);
 }
 
 template <typename T>

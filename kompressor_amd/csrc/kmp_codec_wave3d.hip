@@ -63,17 +63,11 @@ struct OutRows {
   uint2 mv[7];
 };
 
-// Store policy (STC): default-policy stores allocate in the MALL, non-temporal ones stream past it.
-// The encode's lowres and maps are what the next kernel reads (a decode, a pack, a copy to the
-// host), so by default they are stored cached: at C3 the following decode reads part of its 256 MiB
-// of maps from the MALL (decode 90.7 -> 85.2 us, encode unchanged; profiles/round2/ab_wave3d_store_policy.log).
-// The decode's highres stays non-temporal: cached, its dirty lines drain during the next encode
-// (+7 us).  KMP_W3_ST_ENC=0 restores the non-temporal encode stores.
-template <bool STC>
-__device__ __forceinline__ void stp8(void* p, uint2 v) {
-  if constexpr (STC) *(uint2*)p = v;
-  else st8(p, v);
-}
+// Store policy (STC, stp8 in kmp_wave.h): the encode's lowres and maps are what the next kernel
+// reads (a decode, a pack, a copy to the host), so by default they are stored cached: at C3 the
+// following decode reads part of its 256 MiB of maps from the MALL (decode 90.7 -> 85.2 us, encode
+// unchanged; profiles/round2/ab_wave3d_store_policy.log).  The decode's highres stays non-temporal:
+// cached, its dirty lines drain during the next encode (+7 us).  KMP_W3_ST_ENC=0: non-temporal.
 
 // WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
 template <typename T, bool DEC, int PL, bool ONE, bool STC>

@@ -32,6 +32,14 @@ __device__ __forceinline__ void st8(void* p, uint2 v) {
   __builtin_nontemporal_store(w, (u32x2*)p);
 }
 
+// STC: a default-policy (MALL-allocating) store, for outputs the next kernel reads; otherwise the
+// streaming (non-temporal) st8
+template <bool STC>
+__device__ __forceinline__ void stp8(void* p, uint2 v) {
+  if constexpr (STC) *(uint2*)p = v;
+  else st8(p, v);
+}
+
 template <typename T>
 __device__ __forceinline__ uint32_t el16(const uint4& v, int e) {  // element e of 16 bytes
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
