@@ -1,6 +1,6 @@
 """Copy a gpu_round.sh run's evidence into profiles/<round>/ and refresh profiles/pmc_traffic.json.
     python tools/summarize_round.py gpurun_out/TAG profiles/round1"""
-import csv, glob, json, os, shutil, sys
+import csv, glob, json, os, shutil, sys  # noqa: E401
 from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
@@ -29,7 +29,10 @@ def pmc(kind):
         shutil.copy(f[0], os.path.join(dst, f'{tag}_pmc_{ctr}{kind}.csv'))
         for r in csv.DictReader(open(f[0])):
             if 'kmp' in r['Kernel_Name']:
-                direction = 'decode' if (', true' in r['Kernel_Name'] or '<true>' in r['Kernel_Name']) else 'encode'
+                # the DEC template argument: first of wave2d_u8_kernel<DEC>, second of <T, DEC, ...>
+                args = [a.strip() for a in r['Kernel_Name'].split('<', 1)[1].split('>', 1)[0].split(',')]
+                dec = args[0] if 'u8_kernel' in r['Kernel_Name'] else args[1]
+                direction = 'decode' if dec == 'true' else 'encode'
                 vals[(direction, r['Counter_Name'])].append(float(r['Counter_Value']))
     out = {}
     for d in ('encode', 'decode'):
