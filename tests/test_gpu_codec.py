@@ -137,9 +137,10 @@ def test_reference_style_predictor(kom, name):
     assert torch.equal(rec.cpu(), hi.cpu())
 
 
-def float_predictions_fn(kom, padding, ndim, seen):
+def float_predictions_fn(kom, padding, ndim, seen, special=True):
     """A network-like predictor: float32 maps that are not integers -- fractional, negative, past
-    the sample range, and a few +-inf / NaN / beyond-int32 entries -- recorded in ``seen``."""
+    the sample range, and (``special``) a few +-inf / NaN / beyond-int32 entries placed by flat
+    index, so not translation-invariant -- recorded in ``seen``."""
     ns = _ns(kom, ndim)
     k = 19 if ndim == 3 else 5
 
@@ -149,12 +150,13 @@ def float_predictions_fn(kom, padding, ndim, seen):
         pred = pred.repeat_interleave(k, dim=ndim + 1)
         pred = pred + torch.linspace(-3.7, 2.9, k, device=pred.device).reshape(
             *([1] * (ndim + 1)), k, *([1] * (pred.dim() - ndim - 2)))
-        flat = pred.view(-1)
-        flat[::97] = float('nan')
-        flat[5::131] = float('inf')
-        flat[7::151] = -float('inf')
-        flat[11::173] = 3.5e9
-        flat[13::179] = -3.5e9
+        if special:
+            flat = pred.view(-1)
+            flat[::97] = float('nan')
+            flat[5::131] = float('inf')
+            flat[7::151] = -float('inf')
+            flat[11::173] = 3.5e9
+            flat[13::179] = -3.5e9
         maps = ns.maps_from_predictions(pred.contiguous())
         seen.append([m.cpu().numpy() for m in maps])
         return maps
@@ -199,6 +201,16 @@ def test_callback_float32_predictions(kom, name, rows, monkeypatch):
     assert torch.equal(rec.cpu(), hi.cpu())
     orec = ons.decode(lambda w: seen[1], odec, want_lo, (want_maps, want_dims), padding=p)
     assert np.array_equal(orec, g['highres'])
+    # the chunked drivers call predictions_fn per chunk window: chunk invariance needs a predictor of
+    # the neighbourhood alone, so the one without the index-placed special values
+    local = float_predictions_fn(kom, p, ndim, [], special=False)
+    lo1, (maps1, dims1) = ns.encode(local, enc, hi, padding=p)
+    lo2, (maps2, _) = ns.encode_chunks(local, enc, hi, chunk=5, padding=p)
+    assert torch.equal(lo2, lo1)
+    for i, (a, b) in enumerate(zip(maps2, maps1)):
+        assert torch.equal(a, b), f'chunked map {i}'
+    assert torch.equal(ns.decode_chunks(local, dec, lo1, (maps1, dims1), chunk=(6, 7) if ndim == 2 else 6,
+                                        padding=p), hi)
 
 
 @pytest.mark.parametrize('name,chunk', [('vol_ramp_odd_p0', 6), ('vol_ramp_odd_p1', 11), ('vol_ramp_odd_p1', (6, 11, 11)),
