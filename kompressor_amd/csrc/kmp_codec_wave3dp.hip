@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t node_el(const typename NodeRow<DEC>::V& v, i
 }
 
 // WPE: the amdgpu_waves_per_eu register budget (1 = the compiler's choice)
-template <typename T, bool DEC, int P, int PL, int WPE>
+template <typename T, bool DEC, int P, int PL, int WPE, bool STC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3dp_kernel(W3P a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr int NB = 2 * P + 2;     // neighbourhood extent per axis
@@ -287,12 +287,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         res[5][i] = (el16<T>(Oc.e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
         res[6][i] = (el16<T>(own, 2 * i + 1) - pred[6][i]) & MASK;    // X  (0,0,1)
       }
-      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
+      stp8<STC>((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         int par[3];
         map_parity(3, k, par);
-        if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+        if (mok_y[k] && (!par[0] || vz1)) stp8<STC>((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
       }
     } else {
       const OutRows& Oc = O[u];
@@ -327,7 +327,7 @@ struct RollStep {
   OutRows o;
 };
 
-template <typename T, bool DEC, int P>
+template <typename T, bool DEC, int P, bool STC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 3 : 1)))
 wave3dr_kernel(W3P a) {
   constexpr int PD = 1;  // prefetch distance in output planes (2 measured no faster: r2ar)
@@ -563,12 +563,12 @@ wave3dr_kernel(W3P a) {
           res[5][i] = (el16<T>(Oc.e1, 2 * i) - pred[5][i]) & MASK;      // Y  (0,1,0)
           res[6][i] = (el16<T>(own, 2 * i + 1) - pred[6][i]) & MASK;    // X  (0,0,1)
         }
-        st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
+        stp8<STC>((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(lov));
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           int par[3];
           map_parity(3, k, par);
-          if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
+          if (mok_y[k] && (!par[0] || vz1)) stp8<STC>((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res[k]));
         }
       } else {
         const uint2 own = Sc.cur;
@@ -673,31 +673,47 @@ static int w3p_roll(int P, int bytes) {
   return zr >= 2 ? (zr + 1) / 2 * 2 : 0;
 }
 
+// the encode's lowres / map stores: cached (MALL-allocating, stp8 in kmp_wave.h; alternating encode /
+// decode pairs at C3: p = 1 -0.5 us, p = 2 -10 us per pair, profiles/round2/ab_wave3dp_store_policy.log) unless
+// KMP_W3P_ST_ENC=0 (non-temporal)
+static bool w3p_stc(bool dec) { return !dec && w3p_env("KMP_W3P_ST_ENC", 1); }
+
+template <typename T, bool DEC, bool STC>
+static void launch_wave3dr_s(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
+  if (P == 1) w3p::wave3dr_kernel<T, DEC, 1, STC><<<grid, block, 0, stream>>>(a);
+  else w3p::wave3dr_kernel<T, DEC, 2, STC><<<grid, block, 0, stream>>>(a);
+}
 template <typename T, bool DEC>
 static void launch_wave3dr(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
-  if (P == 1) w3p::wave3dr_kernel<T, DEC, 1><<<grid, block, 0, stream>>>(a);
-  else w3p::wave3dr_kernel<T, DEC, 2><<<grid, block, 0, stream>>>(a);
+  if (w3p_stc(DEC)) launch_wave3dr_s<T, DEC, true>(P, grid, block, stream, a);
+  else launch_wave3dr_s<T, DEC, false>(P, grid, block, stream, a);
+}
+
+template <typename T, bool DEC, bool STC>
+static void launch_wave3dp_s(int P, int pl, int wpe, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
+  if (P == 1) {
+    if (pl == 1) {
+      if (wpe == 4) w3p::wave3dp_kernel<T, DEC, 1, 1, 4, STC><<<grid, block, 0, stream>>>(a);
+      else w3p::wave3dp_kernel<T, DEC, 1, 1, 1, STC><<<grid, block, 0, stream>>>(a);
+    } else {
+      if (wpe == 4) w3p::wave3dp_kernel<T, DEC, 1, 2, 4, STC><<<grid, block, 0, stream>>>(a);
+      else w3p::wave3dp_kernel<T, DEC, 1, 2, 1, STC><<<grid, block, 0, stream>>>(a);
+    }
+  } else {
+    if (pl == 1) {
+      if (wpe == 3) w3p::wave3dp_kernel<T, DEC, 2, 1, 3, STC><<<grid, block, 0, stream>>>(a);
+      else w3p::wave3dp_kernel<T, DEC, 2, 1, 1, STC><<<grid, block, 0, stream>>>(a);
+    } else {
+      if (wpe == 3) w3p::wave3dp_kernel<T, DEC, 2, 2, 3, STC><<<grid, block, 0, stream>>>(a);
+      else w3p::wave3dp_kernel<T, DEC, 2, 2, 1, STC><<<grid, block, 0, stream>>>(a);
+    }
+  }
 }
 
 template <typename T, bool DEC>
 static void launch_wave3dp(int P, int pl, int wpe, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
-  if (P == 1) {
-    if (pl == 1) {
-      if (wpe == 4) w3p::wave3dp_kernel<T, DEC, 1, 1, 4><<<grid, block, 0, stream>>>(a);
-      else w3p::wave3dp_kernel<T, DEC, 1, 1, 1><<<grid, block, 0, stream>>>(a);
-    } else {
-      if (wpe == 4) w3p::wave3dp_kernel<T, DEC, 1, 2, 4><<<grid, block, 0, stream>>>(a);
-      else w3p::wave3dp_kernel<T, DEC, 1, 2, 1><<<grid, block, 0, stream>>>(a);
-    }
-  } else {
-    if (pl == 1) {
-      if (wpe == 3) w3p::wave3dp_kernel<T, DEC, 2, 1, 3><<<grid, block, 0, stream>>>(a);
-      else w3p::wave3dp_kernel<T, DEC, 2, 1, 1><<<grid, block, 0, stream>>>(a);
-    } else {
-      if (wpe == 3) w3p::wave3dp_kernel<T, DEC, 2, 2, 3><<<grid, block, 0, stream>>>(a);
-      else w3p::wave3dp_kernel<T, DEC, 2, 2, 1><<<grid, block, 0, stream>>>(a);
-    }
-  }
+  if (w3p_stc(DEC)) launch_wave3dp_s<T, DEC, true>(P, pl, wpe, grid, block, stream, a);
+  else launch_wave3dp_s<T, DEC, false>(P, pl, wpe, grid, block, stream, a);
 }
 
 template <typename T>
