@@ -36,7 +36,7 @@ struct W2P {
   int32_t rrun;   // wave2dr_kernel: output rows per wave (a multiple of rows)
 };
 
-template <typename T, bool DEC, int P>
+template <typename T, bool DEC, int P, bool STC = false>
 __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr int NB = 2 * P + 2;
@@ -208,10 +208,10 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
       res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;  // UD (0,1)
       res[2][i] = (el16<T>(o0, 2 * i + 1) - pred[2][i]) & MASK;   // C  (1,1)
     }
-    st8((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
-    if (vy1) st8((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
-    st8((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
-    if (vy1) st8((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+    stp8<STC>((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
+    if (vy1) stp8<STC>((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
+    stp8<STC>((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
+    if (vy1) stp8<STC>((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
   } else {
     uint32_t dv[3][VX];
 #pragma unroll
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
 // p+1 rows below).  So a step loads one node row and its output rows per lane, against the
 // plane-group kernel's node row + up to two halo rows; the node rows of step s+2 and the output
 // rows of step s+1 are in flight while step s computes.
-template <typename T, bool DEC, int P>
+template <typename T, bool DEC, int P, bool STC = false>
 __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr int NB = 2 * P + 2;
@@ -409,10 +409,10 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
           res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;      // UD (0,1)
           res[2][i] = (el16<T>(Ocur.o0, 2 * i + 1) - pred[2][i]) & MASK;  // C  (1,1)
         }
-        st8((T*)a.lo_out + m_ud, pack8<T, VX>(n));
-        if (vy1) st8((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
-        st8((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
-        if (vy1) st8((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+        stp8<STC>((T*)a.lo_out + m_ud, pack8<T, VX>(n));
+        if (vy1) stp8<STC>((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
+        stp8<STC>((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
+        if (vy1) stp8<STC>((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
       } else {
         uint32_t dv[3][VX];
 #pragma unroll
@@ -499,15 +499,24 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   return nblk < ((int64_t)1 << 31);
 }
 
-template <typename T, bool DEC>
-static void launch_wave2dp(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
+template <typename T, bool DEC, bool STC>
+static void launch_wave2dp_s(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
   if (a.rrun > 0) {
-    if (P == 1) w2p::wave2dr_kernel<T, DEC, 1><<<grid, block, 0, s>>>(a);
-    else w2p::wave2dr_kernel<T, DEC, 2><<<grid, block, 0, s>>>(a);
+    if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
+    else w2p::wave2dr_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
     return;
   }
-  if (P == 1) w2p::wave2dp_kernel<T, DEC, 1><<<grid, block, 0, s>>>(a);
-  else w2p::wave2dp_kernel<T, DEC, 2><<<grid, block, 0, s>>>(a);
+  if (P == 1) w2p::wave2dp_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
+  else w2p::wave2dp_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
+}
+
+// the encode's lowres / map stores: cached (MALL-allocating, stp8 in kmp_wave.h; alternating pairs at
+// C2: p = 1 -0.9 us, p = 2 +-0, profiles/round2/ab_wave2dp_store_policy.log) unless
+// KMP_W2P_ST_ENC=0 (non-temporal)
+template <typename T, bool DEC>
+static void launch_wave2dp(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
+  if (!DEC && w2p_env("KMP_W2P_ST_ENC", 1)) launch_wave2dp_s<T, DEC, true>(P, grid, block, s, a);
+  else launch_wave2dp_s<T, DEC, false>(P, grid, block, s, a);
 }
 
 template <typename T>
