@@ -19,7 +19,11 @@
 //   rice_unpack_kernel lane j loads planes 8p + j < k and transposes back to the samples' low
 //                      bits; the unary part: the lane finds the end of terminator 8j - 1 (a
 //                      popcount walk + a binary-search select in one word), then reads its 8
-//                      quotients off the stream with ctz, one 32-bit word load per crossing
+//                      quotients off a 64-bit window of the stream with ctz (a word-by-word walk
+//                      when the 8 codes are longer than 64 bits)
+// All three are VALU-bound, not latency-bound: the SQ counters give VALU instructions x 4 cycles
+// (wave64 on a 16-lane SIMD) / 1024 SIMDs = the kernel time (profiles/round2/rice_kernels.log), and
+// U steps per wave with their loads batched (U = 2, 4, 8) measured no faster.
 #include "kmp_bits.h"
 
 namespace kmp {
@@ -121,15 +125,18 @@ __global__ void __launch_bounds__(256) rice_plan_kernel(const void* __restrict__
     // S_k = sum_i (z_i >> k) = 2 S_{k+1} + count_k; words(k) = 2k + ceil((64 + S_k) / 32).  An S_k
     // past kSumCap costs more than 2W + 2 words (the k = W - 1 cost bound), so capping it keeps the
     // argmin exact (ties: the smallest k, as the descending loop keeps the last <=)
-    uint32_t S = 0, best = 0xffffffffu;
-    int kbest = 0;
+    // (W <= 16: S_0 <= 64 (2^16 - 1) needs no cap.)  The argmin as one min per k over the key
+    // 32 words(k) + k = ((S_k + 95) & ~31) + 65 k: the fewest words, ties to the smallest k
+    uint32_t S = 0, key = 0xffffffffu;
 #pragma unroll
     for (int k = W - 1; k >= 0; --k) {
       const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      S = min(2u * S + c, kSumCap);
-      const uint32_t words = 2u * k + ((64u + S + 31u) >> 5);
-      if (words <= best) { best = words; kbest = k; }
+      S = 2u * S + c;
+      if constexpr (W > 16) S = min(S, kSumCap);
+      key = min(key, ((S + 95u) & ~31u) + 65u * (uint32_t)k);
     }
+    const uint32_t best = key >> 5;
+    const int kbest = (int)(key & 31u);
     const bool zero = S == 0;  // S_0 == sum of z: an all-zero block
     const int64_t blk = st * 8 + (lane >> 3);
     if ((lane & 7) == 0 && blk < nb) {
@@ -286,23 +293,38 @@ __global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __rest
         }
         pos = wi < uw ? 32u * wi + select32(word, r - acc) + 1u : 32u * uw;
       }
-      // ``cur``: the stream bits from position ``base`` up to the end of word ``wi``
       int wi = (int)(pos >> 5);
-      uint32_t cur = wi < uw ? us[wi] >> (pos & 31u) : 0u;
-      uint32_t base = pos;
+      // the 64 stream bits from ``pos`` (three words funnel-shifted); when they hold the lane's 8
+      // terminators -- a mean quotient below 7 at the block's k, nearly always -- the quotients are
+      // 8 branch-free ctz steps, otherwise the word-by-word walk below
+      const uint32_t sh = pos & 31u;
+      const uint32_t a = wi < uw ? us[wi] : 0u, b = wi + 1 < uw ? us[wi + 1] : 0u, c = wi + 2 < uw ? us[wi + 2] : 0u;
+      uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
+      if (__builtin_popcountll(win) >= 8) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        while (cur == 0u && wi + 1 < uw) {  // only zeros left in this word: continue in the next
-          ++wi;
-          cur = us[wi];
-          base = 32u * wi;
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(win);
+          q[e] = t;
+          win = (win >> t) >> 1;
         }
-        if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
-        const uint32_t t = __builtin_ctz(cur);
-        q[e] = base + t - pos;  // the zeros between the code's start and its terminator
-        pos = base + t + 1u;
-        cur = t == 31u ? 0u : cur >> (t + 1u);
-        base = pos;
+      } else {
+        // ``cur``: the stream bits from position ``base`` up to the end of word ``wi``
+        uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
+        uint32_t base = pos;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          while (cur == 0u && wi + 1 < uw) {  // only zeros left in this word: continue in the next
+            ++wi;
+            cur = us[wi];
+            base = 32u * wi;
+          }
+          if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
+          const uint32_t t = __builtin_ctz(cur);
+          q[e] = base + t - pos;  // the zeros between the code's start and its terminator
+          pos = base + t + 1u;
+          cur = t == 31u ? 0u : cur >> (t + 1u);
+          base = pos;
+        }
       }
     }
     uint32_t wout[Sw<W>::NW];

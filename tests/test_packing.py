@@ -124,6 +124,39 @@ def test_rice_matches_spec(kom, dtype, shape, spread):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.uint32])
+def test_rice_long_unary_runs(kom, dtype):
+    """Blocks whose unary part is lopsided: the 8 samples of one lane (8 consecutive samples) are
+    large and the rest of the block small, so that lane's 8 codes span more than 64 stream bits and
+    the unpack kernel leaves its 64-bit window path for the word-by-word walk; every lane position,
+    several magnitudes, and single spikes.  Byte-exact to the spec, lossless."""
+    rng = np.random.default_rng(11)
+    W = np.dtype(dtype).itemsize * 8
+    top = (1 << min(W, 16)) - 1
+    blocks = []
+    for lane in range(8):
+        for mag in (40, 255, 3000, top):
+            b = rng.integers(0, 3, size=64)
+            b[8 * lane:8 * lane + 8] = rng.integers(mag // 2, mag + 1, size=8)
+            blocks.append(b)
+            s1 = np.zeros(64, np.int64)
+            s1[8 * lane + int(rng.integers(0, 8))] = mag  # one spike, the rest zero
+            blocks.append(s1)
+    x = (np.concatenate(blocks) * np.where(rng.random(64 * len(blocks)) < 0.5, 1, -1)).astype(np.int64)
+    x = (x % (1 << W)).astype(dtype)  # signed residuals in the coder's modular form
+    blob = kom.packing.pack(x)
+    params, bw, payload = ORC.pack(x)
+    head = 40 + 8 * x.ndim
+    nb = len(params)
+    p8 = (nb + 7) // 8 * 8
+    assert np.array_equal(blob[head:head + nb], params)
+    assert np.array_equal(blob[head + p8:head + p8 + nb], bw)
+    got = blob[head + 2 * p8:head + 2 * p8 + 4 * payload.size].view(np.uint32)
+    assert np.array_equal(got, payload)
+    assert np.array_equal(kom.packing.unpack(blob), x)
+
+
+@pytest.mark.gpu
 def test_rice_torch_round_trip_large(kom):
     """A full C3-sized coded map (512 x 32^3 uint16, device-resident): lossless through the Rice
     kernels, and the numpy spec agrees on a slice of blocks."""
