@@ -193,8 +193,9 @@ __global__ void __launch_bounds__(256) rice_pack_kernel(const void* __restrict__
     const uint32_t incl = group8_incl(len, j);
     const uint32_t tot = (uint32_t)__shfl((int)incl, (g << 3) | 7, 64);  // the block's unary bits
     const uint32_t uw = (tot + 31u) >> 5;
-    // zero the block's stream, OR in one terminator per sample, copy the words out
-    for (uint32_t i = j; i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
+    // zero the block's uw stream words (all a terminator can land in: pos < tot), OR in one
+    // terminator per sample, copy the words out
+    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(256) rice_pack_kernel(const void* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       pos += q[e];
-      if (param > 0 && pos < 32u * UMAX) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
+      if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
       pos += 1u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
