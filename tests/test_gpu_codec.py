@@ -619,3 +619,36 @@ def test_trace_ranges_do_not_change_results(kom, monkeypatch):
     assert torch.equal(kom.volume.decode(cb, kom.volume.decode_values_uint16, lo, enc, padding=1), x)
     lo2, enc2 = kom.volume.encode_chunks(pred, kom.volume.encode_values_uint16, x, chunk=6, padding=1)
     assert torch.equal(lo2, lo)
+
+
+@pytest.mark.parametrize('case', [
+    ('KMP_W3_ST_ENC', (2, 64, 64, 64, 1), np.uint16, 0, 'wave3d'),   # the metric kernel
+    ('KMP_W2_ST_ENC', (3, 256, 256, 1), np.uint8, 0, 'wave2d'),
+    ('KMP_W3P_ST_ENC', (2, 20, 24, 32, 1), np.uint16, 1, 'wave3d'),  # wave3dp / wave3dr
+    ('KMP_W3P_ST_ENC', (2, 20, 24, 32, 1), np.uint16, 2, 'wave3d'),
+    ('KMP_W2P_ST_ENC', (3, 40, 128, 1), np.uint8, 1, 'wave2d'),      # wave2dp / wave2dr
+    ('KMP_W2P_ST_ENC', (3, 40, 128, 1), np.uint16, 2, 'wave2d'),
+])
+@pytest.mark.parametrize('cached', ['0', '1'])
+def test_encode_store_policy_is_output_neutral(kom, case, cached, monkeypatch):
+    """The encode kernels' lowres / map stores are cached (MALL-allocating) by default and
+    non-temporal with KMP_*_ST_ENC=0 (INTEGRATION.md knobs): both policies give the oracle's bytes
+    and a lossless decode, and the wave kernel family served the call."""
+    knob, shape, dtype, p, family = case
+    monkeypatch.setenv(knob, cached)
+    import oracle
+    from oracle import predictors as OP
+    ndim = len(shape) - 2
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    coder = 'uint16' if dtype == np.uint16 else 'uint8'
+    enc, dec = getattr(ns, f'encode_values_{coder}'), getattr(ns, f'decode_values_{coder}')
+    x = np.random.default_rng(29).integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    want_lo, (want_maps, _) = ons.encode(OP.mean_predictions_fn(p, ndim), getattr(oracle.common, f'encode_values_{coder}'),
+                                         x, padding=p)
+    pred = kom.MeanPredictor(p, ndim)
+    lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
+    assert _last_launch(kom).startswith(family) and _last_launch(kom).endswith('_encode'), _last_launch(kom)
+    assert np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        assert np.array_equal(a, b), (knob, cached, i)
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
