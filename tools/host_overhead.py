@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Host-side cost of one API call: cProfile over N back-to-back calls of the callback-path encode
-and decode (128 C3 tiles, opaque predictions_fn), the fused encode, and a graph-replayed
-CodecPlan (kompressor_amd.graphs), with one synchronisation at the end, so the Python / ctypes /
+and decode (128 C3 tiles, opaque predictions_fn), the fused encode, and graph-replayed
+CodecPlans (kompressor_amd.graphs) of the fused and the callback path, with one synchronisation at the end, so the Python / ctypes /
 allocator time per call is visible next to the kernels' time.
 
     python tools/host_overhead.py [N]
@@ -26,12 +26,16 @@ lo, enc = V.encode(cb, V.encode_values_uint16, vol)
 torch.cuda.synchronize()
 plan = kom.graphs.CodecPlan(pred, tuple(vol.shape), vol.dtype)
 plan.highres.copy_(vol)
+cplan = kom.graphs.CodecPlan(cb, tuple(vol.shape), vol.dtype, padding=0)  # the callback path, captured
+cplan.highres.copy_(vol)
 for name, fn in (('encode', lambda: V.encode(cb, V.encode_values_uint16, vol)),
                  ('decode', lambda: V.decode(cb, V.decode_values_uint16, lo, enc)),
                  ('fused_encode', lambda: V.encode(pred, V.encode_values_uint16, vol)),
                  ('chunks_encode', lambda: V.encode_chunks(pred, V.encode_values_uint16, vol, chunk=32)),
                  ('graph_encode', lambda: plan.encode()),
-                 ('graph_decode', lambda: plan.decode())):
+                 ('graph_decode', lambda: plan.decode()),
+                 ('graph_callback_encode', lambda: cplan.encode()),
+                 ('graph_callback_decode', lambda: cplan.decode())):
     for _ in range(10):
         fn()
     torch.cuda.synchronize()
