@@ -676,24 +676,28 @@ __device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t o
 // 512 C3 windows).  A z-rolling variant of this kernel (3-slot node ring, next plane prefetched
 // in registers, each cell plane summed once) measured slower, 100-108 us: the plane-parallel grid
 // hides the load latency as well and has 8x the workgroups.
-template <typename T, int P>
+// PPB output planes per workgroup (1 or 2): with 2, the cell plane between them is summed once
+// for both (3 cell planes for 2 outputs instead of 4) -- the kernel is VALU-bound
+// (profiles/round2/sq_callback_kernels.txt)
+template <typename T, int P, int PPB>
 __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
     const T* __restrict__ win, E3<int32_t> S, int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs, int32_t xcd_per,
     int32_t nodes_bytes, int32_t xs_bytes) {
+  static_assert(PPB == 1 || PPB == 2, "one or two output planes per workgroup");
   constexpr int KK = 2 * P + 2;
   constexpr float NN = (float)(KK * KK * KK);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int32_t nplanes = Lcz + 1;
+  const int32_t nplanes = Lcz + 1, ngrp = (nplanes + PPB - 1) / PPB;
   int32_t blk = (int32_t)blockIdx.x;
   if (xcd_per > 0) {  // consecutive planes of one window on one XCD: shared node planes hit its L2
     const int32_t x = blk % 8, k = blk / 8;
     blk = ((k / xcd_per) * 8 + x) * xcd_per + (k % xcd_per);
   }
-  const int32_t oz = blk % nplanes;
-  const int64_t b = blk / nplanes;
+  const int32_t oz = (blk % ngrp) * PPB;  // the first output plane; cell slot s is plane oz - 1 + s
+  const int64_t b = blk / ngrp;
   const int32_t S1 = S.e[1], S2 = S.e[2], plane = S1 * S2;
   const int32_t zlo = oz >= 1 ? oz - 1 : 0;
-  const int32_t zhi = oz + KK < S.e[0] ? oz + KK : S.e[0];  // node planes [zlo, zhi)
+  const int32_t zhi = oz + PPB - 1 + KK < S.e[0] ? oz + PPB - 1 + KK : S.e[0];  // node planes [zlo, zhi)
 
   // ---- node planes -> LDS: the aligned 16-byte blocks covering the byte range; the partial
   // blocks at either end copy only the window's own bytes ----
@@ -713,7 +717,7 @@ __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
   }
   const T* nodes = (const T*)(smem + shift);  // [z - zlo][y][x]
   uint32_t* xs = (uint32_t*)(smem + nodes_bytes);  // p >= 1: [z - zlo][y][cx] sums over x
-  // [slot: z = oz - 1 + slot][cy][cx], after a pad of >= Lcx + 1 words
+  // [slot: z = oz - 1 + slot][cy][cx], PPB + 1 slots, after a pad of >= Lcx + 1 words
   uint32_t* cells = (uint32_t*)(smem + nodes_bytes + xs_bytes) + mp_pad_words(Lcx);
   __syncthreads();
 
@@ -732,16 +736,17 @@ __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
     }
     __syncthreads();
   }
-  // cell planes oz - 1 (slot 0) and oz (slot 1), rows of both planes through the row mapping
+  // cell planes oz - 1 .. oz + PPB - 1 (slots 0 .. PPB), rows of all through the row mapping
   const int32_t wv = threadIdx.x >> 6;
   for (int32_t xc = 0; xc < Lcx; xc += 64) {
     const RowMap m = row_map(Lcx - xc < 64 ? Lcx - xc : 64);
     const int32_t cx = xc + m.lx;
-    for (int32_t r0 = wv * m.R; r0 < 2 * Lcy; r0 += 4 * m.R) {
+    for (int32_t r0 = wv * m.R; r0 < (PPB + 1) * Lcy; r0 += 4 * m.R) {
       const int32_t r = r0 + m.lr;
-      const int32_t slot = r >= Lcy, cy = r - slot * Lcy;
+      const int32_t slot = PPB == 1 ? (int32_t)(r >= Lcy) : (int32_t)(r >= Lcy) + (int32_t)(r >= 2 * Lcy);
+      const int32_t cy = r - slot * Lcy;
       const int32_t z = oz - 1 + slot;
-      if (!m.lane_ok || r >= 2 * Lcy || z < 0 || z >= Lcz) continue;  // (a missing plane is never read)
+      if (!m.lane_ok || r >= (PPB + 1) * Lcy || z < 0 || z >= Lcz) continue;  // (a missing plane is never read)
       uint32_t s = 0;
       if constexpr (P == 0) {
         const T* q = nodes + (z - zlo) * plane + cy * S2 + cx;
@@ -758,6 +763,7 @@ __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
   __syncthreads();
 
   mean_maps_plane<T>(cells, oz, b, Lcz, Lcy, Lcx, outs, 1, 0);
+  if (PPB == 2 && oz + 1 < nplanes) mean_maps_plane<T>(cells, oz + 1, b, Lcz, Lcy, Lcx, outs, 2, 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1400,22 +1406,39 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
       // one workgroup per output plane when the plane's window planes fit LDS
       const int64_t plane = S.e[1] * S.e[2];
-      const int64_t nodes_bytes = 16 * (ceil_div((2 * padding + 3) * plane * (int64_t)sizeof(T), 16) + 1);
-      const int64_t xs_bytes = padding > 0 ? 4 * (2 * padding + 3) * S.e[1] * cells.e[2] : 0;
-      const int64_t lds_plane = nodes_bytes + xs_bytes + 8 * cells.e[1] * cells.e[2] + 8 * mp_pad_words(cells.e[2]);
-      const int64_t nblk_plane = B * (cells.e[0] + 1);
+      // PPB output planes per workgroup: 1, or 2 when KMP_MP_PPB=2 and its LDS fits
+      auto lds_for = [&](int q, int64_t& nb_, int64_t& xs_) {
+        nb_ = 16 * (ceil_div((2 * padding + 2 + q) * plane * (int64_t)sizeof(T), 16) + 1);
+        xs_ = padding > 0 ? 4 * (2 * padding + 2 + q) * S.e[1] * cells.e[2] : 0;
+        return nb_ + xs_ + 4 * (q + 1) * cells.e[1] * cells.e[2] + 8 * mp_pad_words(cells.e[2]);
+      };
+      const char* ppb_env = std::getenv("KMP_MP_PPB");
+      int64_t nodes_bytes = 0, xs_bytes = 0;
+      int ppb = ppb_env && std::atoi(ppb_env) == 2 ? 2 : 1;
+      int64_t lds_plane = lds_for(ppb, nodes_bytes, xs_bytes);
+      if (ppb == 2 && lds_plane > 64 * 1024) {
+        ppb = 1;
+        lds_plane = lds_for(ppb, nodes_bytes, xs_bytes);
+      }
+      const int64_t ngrp = ceil_div(cells.e[0] + 1, (int64_t)ppb);
+      const int64_t nblk_plane = B * ngrp;
       if (nsp == 3 && C == 1 && padding <= 2 && lds_plane <= 64 * 1024 && nblk_plane < ((int64_t)1 << 31) &&
           (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31) &&
           !std::getenv("KMP_MP_LDS")) {
         auto launch = [&](auto kern) {
           kern<<<(unsigned)nblk_plane, kThreads, (size_t)lds_plane, (hipStream_t)stream>>>(
               (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2], outs,
-              B % 8 == 0 ? (int32_t)(cells.e[0] + 1) : 0, (int32_t)nodes_bytes, (int32_t)xs_bytes);
+              B % 8 == 0 ? (int32_t)ngrp : 0, (int32_t)nodes_bytes, (int32_t)xs_bytes);
           return check_launch("mean_predict_plane");
         };
-        if (padding == 0) return launch(mean_predict_plane_kernel<T, 0>);
-        if (padding == 1) return launch(mean_predict_plane_kernel<T, 1>);
-        return launch(mean_predict_plane_kernel<T, 2>);
+        if (ppb == 2) {
+          if (padding == 0) return launch(mean_predict_plane_kernel<T, 0, 2>);
+          if (padding == 1) return launch(mean_predict_plane_kernel<T, 1, 2>);
+          return launch(mean_predict_plane_kernel<T, 2, 2>);
+        }
+        if (padding == 0) return launch(mean_predict_plane_kernel<T, 0, 1>);
+        if (padding == 1) return launch(mean_predict_plane_kernel<T, 1, 1>);
+        return launch(mean_predict_plane_kernel<T, 2, 1>);
       }
       if (rows_ok(C, {vol(B, S, C), total}) && padding <= 1) {
         const int32_t XO = (int32_t)std::min<int64_t>(cells.e[2] + 1, 64);

@@ -124,15 +124,17 @@ def test_coders_keep_torch(kom):
                                          ((1, 5, 41, 7, 1), np.uint16)])
 @pytest.mark.parametrize('padding', [0, 1, 2])
 def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
-    """The LDS-staged mean predictor (one workgroup per output plane; 3D, C == 1) on C3 tiles and
-    ragged windows, against the oracle and the element-gather kernel it replaced (KMP_MP_LDS=1)."""
+    """The LDS-staged mean predictor (one output plane per workgroup, or two with KMP_MP_PPB=2 where
+    the LDS fits; 3D, C == 1) on C3 tiles and ragged windows, against the oracle, both forms and the
+    element-gather kernel it replaced (KMP_MP_LDS=1)."""
     import os
     hi = _rand(shape, dtype, 11)
     lo = oracle.volume.lowres_from_highres(oracle.volume.pad_highres(hi)[0])
     window = oracle.volume.pad_neighborhood(lo, padding)
     want = oracle.predictors.mean_predictions_fn(padding, 3)(window)
     runs = {}
-    for env, val, name in ((None, None, 'mean_predict_plane'), ('KMP_MP_LDS', '1', 'mean_predict_maps')):
+    for env, val, name in ((None, None, 'mean_predict_plane'), ('KMP_MP_PPB', '2', 'mean_predict_plane'),
+                           ('KMP_MP_LDS', '1', 'mean_predict_maps')):
         if env:
             os.environ[env] = val
         try:
