@@ -74,11 +74,23 @@ def _write(path, meta, blob):
     return _HEAD.size + len(js) + host.size
 
 
-def save(path, lowres, encoded, predictor=None, padding=0, ndim=None, method='rice', sample_dtype=None):
+def _builtin_padding(predictor, padding):
+    """The padding a file records: a built-in predictor carries its own (a conflicting explicit
+    ``padding`` is an error); an external predictions_fn needs it passed (default 0)."""
+    if isinstance(predictor, (MeanPredictor, LinearPredictor)):
+        if padding is not None and int(padding) != predictor.padding:
+            raise AssertionError(f'padding={padding} conflicts with the predictor\'s padding {predictor.padding}')
+        return predictor.padding
+    return 0 if padding is None else int(padding)
+
+
+def save(path, lowres, encoded, predictor=None, padding=None, ndim=None, method='rice', sample_dtype=None):
     """Write an ``encode`` result ``(lowres, (maps, dims))`` to ``path``; returns the file size.
-    ``predictor`` is recorded so :func:`decompress` can decode without being told."""
+    ``predictor`` is recorded so :func:`decompress` can decode without being told.  ``padding``
+    defaults to a built-in predictor's own padding (0 for an external predictions_fn)."""
     maps, dims = encoded
     ndim = ndim or len(dims)
+    padding = _builtin_padding(predictor, padding)
     lo_t = dev.to_device(lowres)[0]
     meta = {'format': 'kompressor_amd', 'ndim': ndim, 'padding': padding, 'dims': [int(d) for d in dims],
             'method': method, 'lowres_shape': list(lo_t.shape), 'lowres_dtype': _NP_NAME[lo_t.dtype],
@@ -170,6 +182,8 @@ def decompress(path, predictor=None, as_numpy=True):
         raise AssertionError(f'{path} was coded with an external predictions_fn '
                              f'({meta["predictor"]["name"] if meta["predictor"] else "unknown"}): pass it')
     ndim, padding = meta['ndim'], meta['padding']
+    if isinstance(pred, (MeanPredictor, LinearPredictor)) and pred.padding != padding:
+        raise AssertionError(f'{path} was coded with padding {padding}; the predictor passed has {pred.padding}')
     nmaps = _nd.NMAPS[ndim]
     levels = meta.get('levels') or [{'dims': list(bundle_dims)}]  # save(): one level, dims in the bundle
     if len(arrays) != nmaps * len(levels):

@@ -296,8 +296,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMP_L3
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int ry = u / GPR, cx = (u % GPR) * 16 + 4 * mq;
-        const uint32_t c0 = cvt_sat<T>(acc[u][0]), c1 = cvt_sat<T>(acc[u][1]);
-        const uint32_t c2 = cvt_sat<T>(acc[u][2]), c3 = cvt_sat<T>(acc[u][3]);
+        const uint32_t c0 = cvt_sat_mfma<T>(acc[u][0]), c1 = cvt_sat_mfma<T>(acc[u][1]);
+        const uint32_t c2 = cvt_sat_mfma<T>(acc[u][2]), c3 = cvt_sat_mfma<T>(acc[u][3]);
         *(uint2*)(tile + mj * tstride + ry * a.Ex + cx) = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the wave reads back its own tile

@@ -101,6 +101,17 @@ __device__ __forceinline__ uint32_t cvt_sat(float v) {
   return u < hi ? u : hi;
 }
 
+// cvt_sat for a value an MFMA just wrote: the same result from compiler-visible instructions
+// (clamp, then an in-range conversion), because the compiler's hazard recognizer does not look
+// inside inline asm -- an asm read of an MFMA destination can issue before the result is written
+// (seen: linear3dm decode with the asm form read stale accumulators).  fmaxf(NaN, 0) = 0, and
+// [0, max] truncates like the saturating conversion.
+template <typename T>
+__device__ __forceinline__ uint32_t cvt_sat_mfma(float v) {
+  constexpr float hi = sizeof(T) == 2 ? 65535.0f : 255.0f;
+  return (uint32_t)__builtin_fminf(__builtin_fmaxf(v, 0.0f), hi);
+}
+
 // Lane l reads lane l + d (shdn) / l - d (shup); out-of-range lanes keep their own value.  A
 // distance known to be 1 after inlining is one DPP move (wave_shl:1 / wave_shr:1, whole-wave
 // shifts on CDNA) instead of an LDS-crossbar ds_bpermute with its address computation.

@@ -58,12 +58,15 @@ def decode_shard(predictions_fn, decode_fn, lowres, encoded, padding=0, ndim=3):
 
 def all_gather_tiles(local, n_units, group=None):
     """Reassemble the full ``[n_units, ...]`` batch on every rank from each rank's
-    :func:`shard_range` slice ``local``.  One all-gather of equal-size byte slabs (uneven
-    shards are padded to the largest and the padding dropped), so any dtype travels
-    (RCCL has no uint16); no-op copy for a single process."""
+    :func:`shard_range` slice ``local``, as a new tensor (never an alias of ``local``).  Byte
+    views travel, so any dtype does (RCCL has no uint16).  Equal shards: one
+    ``all_gather_into_tensor`` straight into the result.  Uneven shards over RCCL: the list form
+    with each rank's exact slice of the result as its receive buffer (torch issues it as coalesced
+    broadcasts), so no padding and no concatenation copy afterwards; over gloo (CPU tests) the
+    shards are padded to the largest and the padding dropped."""
     world, rank = world_and_rank(group)
     if world == 1:
-        return local
+        return local.clone()
     dist = _dist()
     b, e = shard_range(n_units, rank, world)
     if local.shape[0] != e - b:
@@ -71,18 +74,24 @@ def all_gather_tiles(local, n_units, group=None):
     per = -(-n_units // world)
     row = tuple(local.shape[1:])
     send = local.contiguous()
-    if send.shape[0] != per:
-        pad = torch.empty((per, *row), dtype=local.dtype, device=local.device)
-        pad[:send.shape[0]].copy_(send)
-        send = pad
+    sb = send.view(torch.uint8).reshape(-1)
+    nccl = dist.get_backend(group) == 'nccl'
+    if n_units == per * world or nccl:
+        out = torch.empty((n_units, *row), dtype=local.dtype, device=local.device)
+        ob = out.view(torch.uint8).reshape(-1)
+        if n_units == per * world and nccl:
+            dist.all_gather_into_tensor(ob, sb, group=group)
+        else:
+            unit = ob.numel() // max(n_units, 1)
+            views = [ob[unit * rb:unit * re_] for rb, re_ in (shard_range(n_units, r, world) for r in range(world))]
+            dist.all_gather(views, sb, group=group)
+        return out
+    # gloo, uneven shards: equal-size padded slabs
+    pad = torch.empty((per, *row), dtype=local.dtype, device=local.device)
+    pad[:send.shape[0]].copy_(send)
     full = torch.empty((per * world, *row), dtype=local.dtype, device=local.device)
-    sb, fb = send.view(torch.uint8).reshape(-1), full.view(torch.uint8).reshape(-1)
-    if dist.get_backend(group) == 'nccl':
-        dist.all_gather_into_tensor(fb, sb, group=group)
-    else:  # gloo (CPU tests): list form
-        dist.all_gather(list(fb.chunk(world)), sb, group=group)
-    if n_units == per * world:
-        return full
+    dist.all_gather(list(full.view(torch.uint8).reshape(-1).chunk(world)), pad.view(torch.uint8).reshape(-1),
+                    group=group)
     parts = []
     for r in range(world):
         rb, re_ = shard_range(n_units, r, world)

@@ -130,6 +130,29 @@ def test_external_predictor_must_be_passed(kom, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('kind,p', [('mean', 1), ('mean', 2), ('linear', 1), ('linear', 0)])
+def test_save_records_the_predictors_padding(kom, tmp_path, kind, p):
+    """save() of an encode() result made with a padded built-in predictor records the predictor's
+    own padding (the default ``padding=None``), so decompress() decodes it without being told;
+    a conflicting explicit padding is refused."""
+    x = structured((2, 32, 32, 32, 1), np.uint16, 2.0, seed=p)
+    if kind == 'mean':
+        pred = kom.MeanPredictor(p, 3)
+    else:
+        n, k = (2 * p + 2) ** 3, 19
+        w = (np.full((n, k), 1.0 / n) + np.random.default_rng(p).standard_normal((n, k)) * 0.01).astype(np.float32)
+        pred = kom.LinearPredictor(w, np.zeros(k, np.float32), p, 3)
+    lo, enc = kom.volume.encode(pred, kom.volume.encode_values_uint16, x, padding=p)
+    path = str(tmp_path / f'{kind}{p}.kmp')
+    kom.container.save(path, lo, enc, predictor=pred)
+    assert kom.container.load(path)[2]['padding'] == p
+    assert np.array_equal(kom.container.decompress(path), x)
+    if p:
+        with pytest.raises(AssertionError, match='padding'):
+            kom.container.save(path, lo, enc, predictor=pred, padding=0)
+
+
+@pytest.mark.gpu
 def test_corrupt_files_raise(kom, tmp_path):
     x = structured((2, 32, 32, 32, 1), np.uint16, 2.0)
     path = tmp_path / 'c.kmp'

@@ -82,14 +82,16 @@ def test_linear_chunks(kom):
 
 
 @pytest.mark.parametrize('shape', [(8, 64, 64, 64, 1), (2, 17, 30, 16, 1), (1, 9, 14, 128, 1), (2, 12, 33, 32, 1),
-                                   (1, 6, 8, 8, 1)])
+                                   (1, 6, 8, 8, 1), (1, 10, 40, 32, 1), (2, 9, 32, 128, 1)])
 @pytest.mark.parametrize('variant', ['rolling_mfma', 'valu', 'plane_mfma'])
 def test_linear_fused_p1(kom, shape, variant, monkeypatch):
     """The fused LinearPredictor p = 1 volume kernels: residuals and lowres bit-exact to the
-    oracle's fma chain + aggregation, lossless, z-region (chunked) launches -- for the rolling
-    matrix-core kernel (kmp_codec_linear3r.hip, the default where eligible: 16 channels on
-    v_mfma_f32_16x16x4_f32, the same k-ordered chain, so the same bits), the per-plane packed-FMA
-    kernel (kmp_codec_linear3dp.hip) and its MFMA plane-c sweep (KMP_L3P_MFMA=1)."""
+    oracle's fma chain + aggregation, lossless, z-region (chunked) launches -- for the per-plane
+    matrix-core kernel (linear3dm_kernel, the default where Ex is 16 / 32 / 64: the 14 plane-c
+    channels on v_mfma_f32_16x16x4_f32, the same k-ordered chain, so the same bits), the per-plane
+    packed-FMA kernel (KMP_L3P_MFMA=0) and the rolling matrix-core kernel (KMP_L3R=1).  The shapes
+    cover every Ex the MFMA kernel takes, a partial last wave (Ey 20 at Ex 16) and the VALU kernel's
+    other widths."""
     monkeypatch.setenv('KMP_L3R', '1' if variant == 'rolling_mfma' else '0')
     monkeypatch.setenv('KMP_L3P_MFMA', '1' if variant == 'plane_mfma' else '0')
     hi = _data(shape, np.uint16, 7)
@@ -99,13 +101,17 @@ def test_linear_fused_p1(kom, shape, variant, monkeypatch):
     want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
                                                 padding=1)
     lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, hi, padding=1)
-    assert kom._lib.lib.kmp_last_launch().decode() in ('linear3dp_encode', 'linear3r_encode')
+    ex, ey = lo.shape[3], lo.shape[2]   # the stored lowres extents (Ex, Ey of the kernels)
+    mfma_ok = ex in (16, 32, 64) and ey <= 1024 // ex
+    kern = {'rolling_mfma': ('linear3r', 'linear3dp'), 'valu': ('linear3dp',)}.get(
+        variant, ('linear3w',) if mfma_ok else ('linear3dp',))
+    assert kom._lib.lib.kmp_last_launch().decode() in [k + '_encode' for k in kern]
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, c) in enumerate(zip(maps, want_maps)):
         bad = np.argwhere(a != c)
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
     assert np.array_equal(V.decode(pred, V.decode_values_uint16, lo, (maps, dims), padding=1), hi)
-    assert kom._lib.lib.kmp_last_launch().decode() in ('linear3dp_decode', 'linear3r_decode')
+    assert kom._lib.lib.kmp_last_launch().decode() in [k + '_decode' for k in kern]
     lo2, (maps2, _) = V.encode_chunks(pred, V.encode_values_uint16, hi, chunk=5, padding=1)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
 

@@ -40,7 +40,8 @@ def test_single_process_is_identity():
     x = torch.arange(24, dtype=torch.int32).reshape(6, 2, 2)
     assert world_and_rank() == (1, 0)
     assert local_shard(x).data_ptr() == x.data_ptr()
-    assert all_gather_tiles(x, 6) is x
+    y = all_gather_tiles(x, 6)
+    assert torch.equal(y, x) and y.data_ptr() != x.data_ptr()   # a new tensor, never an alias
 
 
 def _worker(rank, world, port, cases, q):
