@@ -474,8 +474,7 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
   int64_t g = (n + kCatWaves - 1) / kCatWaves;
   const unsigned grid = (unsigned)(g > 65536 ? 65536 : g);
   // vector form: 8 waves per SIMD over the chip, each walking its elements one load ahead
-  const char* ev = std::getenv("KMP_CAT_VEC");
-  const bool vec = (!ev || std::atoi(ev)) && L % 4 == 0 && L <= 512 && ((uintptr_t)logits & 15) == 0;
+  const bool vec = L % 4 == 0 && L <= 512 && ((uintptr_t)logits & 15) == 0;
   const unsigned vgrid = (unsigned)(g > 2048 ? 2048 : g);
   const char* pv = std::getenv("KMP_CAT_PEEL");  // decode ranks below this peel maxima
   const int peel = pv ? std::atoi(pv) : 4;

@@ -67,13 +67,6 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
                          const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
                          hipStream_t stream);
 template <typename T>
-int try_linear3r_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
-                        const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes, hipStream_t stream);
-template <typename T>
-int try_linear3r_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
-                        const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
-                        hipStream_t stream);
-template <typename T>
 int try_wave3d32_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                         const MapPtrs& maps, const kmp_region* region, hipStream_t stream);
 template <typename T>

@@ -343,12 +343,12 @@ static bool geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pr
   lds = (size_t)a.groups * a.group_lds * sizeof(uint32_t);
   if (lds > 64 * 1024) return false;
   const int64_t gblocks = ceil_div(B, a.groups);
-  int64_t want = env_int("KMP_WG_TARGET_2D", 2048);
+  int64_t want = 2048;
   int64_t nslab = ceil_div(want, gblocks);
   if (nslab > g.E[1]) nslab = g.E[1];
   if (nslab < 1) nslab = 1;
   int64_t slab = ceil_div(g.E[1], nslab);
-  const int min_slab = env_int("KMP_MIN_SLAB_2D", 8);
+  const int min_slab = 8;
   if (slab < min_slab) slab = min_slab < g.E[1] ? min_slab : g.E[1];
   nslab = ceil_div(g.E[1], slab);
   a.slab = (int)slab;
@@ -361,7 +361,7 @@ static bool geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pr
 
 template <typename T, bool DEC>
 static void launch(int P, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const F2& a) {
-  const bool nt = env_int("KMP_NT", 1) != 0;
+  const bool nt = true;
   switch (P * 2 + (nt ? 1 : 0)) {
     case 0: fast2d_kernel<T, 0, DEC, 0><<<grid, block, lds, stream>>>(a); break;
     case 1: fast2d_kernel<T, 0, DEC, 1><<<grid, block, lds, stream>>>(a); break;

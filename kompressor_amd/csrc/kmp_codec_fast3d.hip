@@ -453,12 +453,12 @@ static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   if (lds > 64 * 1024) return false;
   // z slabs: enough workgroups to cover the chip a few times over.
   const int64_t zext = ze - zb;
-  int64_t want = env_int("KMP_WG_TARGET", 4096);  // >= 16 slabs / CU: latency hiding beats halo re-reads
+  int64_t want = 4096;  // >= 16 slabs / CU: latency hiding beats halo re-reads
   int64_t nslab = ceil_div(want, B > 0 ? B : 1);
   if (nslab > zext) nslab = zext;
   if (nslab < 1) nslab = 1;
   int64_t slab = ceil_div(zext, nslab);
-  const int min_slab = env_int("KMP_MIN_SLAB", 4);
+  const int min_slab = 4;
   if (slab < min_slab) slab = min_slab < zext ? min_slab : zext;
   nslab = ceil_div(zext, slab);
   a.slab = (int)slab;
@@ -471,7 +471,7 @@ static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
 
 template <typename T, bool DEC>
 static void launch_fast3d(int P, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const F3& a) {
-  const bool nt = env_int("KMP_NT", 1) != 0;  // measured: NT 1-2 % faster (profiles/round1/sweep_volume_p0.log)
+  const bool nt = true;  // measured: NT 1-2 % faster (profiles/round1/sweep_volume_p0.log)
   switch (P * 2 + (nt ? 1 : 0)) {
     case 0: fast3d_kernel<T, 0, DEC, 0><<<grid, block, lds, stream>>>(a); break;
     case 1: fast3d_kernel<T, 0, DEC, 1><<<grid, block, lds, stream>>>(a); break;
@@ -494,8 +494,6 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     st = try_linear3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
-    if (st != KMP_ERR_UNSUPPORTED) return st;
-    st = try_linear3r_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1, MFMA
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1
     if (st != KMP_ERR_UNSUPPORTED) return st;
@@ -530,8 +528,6 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
-    if (st != KMP_ERR_UNSUPPORTED) return st;
-    st = try_linear3r_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;

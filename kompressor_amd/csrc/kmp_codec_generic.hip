@@ -145,7 +145,7 @@ int64_t generic_workspace_bytes(int dtype, int nsp, const Geo& g, int64_t B, int
   int64_t need = B * g.Lc[0] * g.Lc[1] * g.Lc[2] * K * C * dtype_size(dtype);
   if (lin && B > 0) {  // the fused LinearPredictor kernels keep a reordered copy of W [N, K] there
     const int64_t nb = 2 * pred->padding + 2, N = nsp == 3 ? nb * nb * nb : nb * nb;
-    const int64_t wbytes = 2 * N * K * (int64_t)sizeof(float);  // + a {w, w}-splatted part (linear3w_kernel)
+    const int64_t wbytes = N * K * (int64_t)sizeof(float);
     need = need > wbytes ? need : wbytes;
   }
   return need;

@@ -61,32 +61,21 @@ __device__ __forceinline__ uint32_t cast_t(float v) {
 // register pair (pairing cells 0/1 and 2/3 instead needs node pairs (x+1, x+2) assembled by
 // moves in every channel: 214 v_mov per wave, 18 % of a VALU stream the SQ counters show busy
 // 75 % of the cycles).  The chain is unchanged: fma over n = dz*4 + dy*2 + dx from the bias.
-// The weights: SG (default) reads W [8][19] and b with uniform loads into scalar registers, the
-// packed operand {w, w} built by the FMA's operand selection -- no LDS copy, no barrier before the
-// first channel, and 106 / 100 VGPRs instead of 146 (4-5 waves per SIMD instead of 3): C3 168 / 222
-// -> 143 / 191 us per direction (profiles/round2/ab_linear3d_sgpr.log).  KMP_L3_SGPR=0: ``Wt``, the
-// LDS copy, channel-major [19][8] with every weight stored twice, then the bias [19].
+// The weights: W [8][19] and b are read with uniform loads into scalar registers, the packed
+// operand {w, w} built by the FMA's operand selection -- no LDS copy, no barrier before the first
+// channel, and 106 / 100 VGPRs instead of 146 with an LDS copy (4-5 waves per SIMD instead of 3): C3
+// 168 / 222 -> 143 / 191 us per direction (profiles/round2/ab_linear3d_sgpr.log; the LDS form was
+// removed in round 3).
 typedef const __attribute__((address_space(4))) float* CFloat;  // uniform loads (scalar registers)
 
-template <typename T, int K, int G, bool SG>
+template <typename T, int K, int G>
 __device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 (&NP1)[3][G][3], int pl, int g,
-                                        const float* Wt, CFloat Wc, CFloat Bc, uint32_t (&out)[4]) {
+                                        CFloat Wc, CFloat Bc, uint32_t (&out)[4]) {
   f32x2 w2[8];
-  float bk;
-  if constexpr (SG) {  // W [8][19] and b read with uniform (scalar) loads
+  // W [8][19] and b read with uniform (scalar) loads
 #pragma unroll
-    for (int n = 0; n < 8; ++n) w2[n] = (f32x2){Wc[n * 19 + K], Wc[n * 19 + K]};
-    bk = Bc[K];
-  } else {
-    // weights stored pre-splat ({w, w} per n): each 16-byte read is two ready operand pairs
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = *(const float4*)(Wt + K * 16 + 4 * q);
-      w2[2 * q] = (f32x2){v.x, v.y};
-      w2[2 * q + 1] = (f32x2){v.z, v.w};
-    }
-    bk = Wt[19 * 16 + K];
-  }
+  for (int n = 0; n < 8; ++n) w2[n] = (f32x2){Wc[n * 19 + K], Wc[n * 19 + K]};
+  const float bk = Bc[K];
   f32x2 a02 = {bk, bk}, a13 = {bk, bk};
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
@@ -103,14 +92,13 @@ __device__ __forceinline__ void channel(const f32x2 (&NP)[3][G][3], const f32x2 
 }
 
 constexpr int kXch = 5;  // channels exchanged downwards: 3, 9, 10, 16 (plane c), 17 (plane c-1)
-constexpr int kWtWords = 324;  // 19 * 8 weights stored twice + 19 biases, rounded up to 16 B
 
 // All-zero weights and bias: a channel of a cell plane outside the tile (plane c-1 at c = 0, plane
 // c at c >= Lcz) evaluated with these is 0.0 -> 0, which is what the aggregation's mask gives it
 __constant__ float kZeroWeights[8 * 19 + 19];
 
 // FULL: the tile's cells fill the stored lowres rows and columns (Lcy == Ey, Lcx == Ex: every
-// even-sized tile, e.g. C3's 64^3) and the weights are read as scalars (SG).  Then the y+1
+// even-sized tile, e.g. C3's 64^3).  Then the y+1
 // validity and every x validity but the row's first cell (X-1 = -1) are compile-time true, and a
 // missing cell plane (z) is zeroed at the source by reading its channels' weights from
 // kZeroWeights (uniform), so the aggregation masks only the row-above channels on row 0 and the
@@ -118,29 +106,16 @@ __constant__ float kZeroWeights[8 * 19 + 19];
 // decode wave, and 5 waves per SIMD (WPE = 5: 96 / 92 VGPRs, the encode with a 20-byte spill;
 // WPE = 4 measured the same, profiles/round2/ab_linear3d_full.log).  ULD: the decode's unconditional
 // loads compiled in (see there)
-template <typename T, bool DEC, bool SG, bool FULL, int WPE, bool ULD = false>
+template <typename T, bool DEC, bool FULL, int WPE, bool ULD = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) linear3d_kernel(L3 a) {
-  static_assert(!FULL || SG, "FULL reads the weights as scalars");
   constexpr int VX = 8 / (int)sizeof(T);
   static_assert(VX == 4 || VX == 8, "u16 / u8");
   constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   using V = typename std::conditional<DEC, uint2, uint4>::type;
-  // LDS: weights (channel-major [19][8] + bias [19]), then the exchange rows [wave][kXch][Ex]
+  // LDS: the exchange rows [wave][kXch][Ex]
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  float* Wt = (float*)smem;
-  uint32_t* xrow = smem + kWtWords;
+  uint32_t* xrow = smem;
   const CFloat Wc = (CFloat)a.W, Bc = (CFloat)a.b;
-  if constexpr (!SG) {
-    for (int t = threadIdx.x; t < 19 * 9; t += blockDim.x) {
-      if (t < 152) {  // W[n][k] -> Wt[k][n] twice
-        Wt[(t % 19) * 16 + 2 * (t / 19)] = a.W[t];
-        Wt[(t % 19) * 16 + 2 * (t / 19) + 1] = a.W[t];
-      } else {
-        Wt[304 + (t - 152)] = a.b[t - 152];
-      }
-    }
-    __syncthreads();
-  }
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
@@ -202,8 +177,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // read a valid neighbour whose values the masks discard): no zero-initialised registers and no
   // exec-mask branches, 208 -> 190 us at C3 (same box, ab_linear3d_loads.log).  The decode does
   // the same (map planes clamped to the last one that exists): with the weights in scalar registers
-  // 190-205 -> 178-187 us (profiles/round2/ab_linear3d_uld.log); KMP_L3_ULD=0 keeps the guarded
-  // loads, which measured 1-3 % faster with the LDS weight copy. ----
+  // 190-205 -> 178-187 us (profiles/round2/ab_linear3d_uld.log); the guarded form remains only for
+  // tiles without a cell plane / row to clamp to (Lcz or Lcy == 0). ----
   V own[3], dn[3];
   uint4 e1, o0, o1;
   uint2 mv[7];
@@ -306,7 +281,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #define KMP_CH(OUT, PLANE, K)                                             \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                         \
     uint32_t o[4];                                                        \
-    channel<T, K, G, SG>(NP, NP1, PLANE, g, Wt, PLANE ? WcP : WcQ, PLANE ? BcP : BcQ, o); \
+    channel<T, K, G>(NP, NP1, PLANE, g, PLANE ? WcP : WcQ, PLANE ? BcP : BcQ, o); \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j]; \
   }
 
@@ -504,8 +479,8 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)waves;
   const int64_t nblk = B * (ze - zb);
   a.xcd_per = (l3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
-  a.full = l3_env("KMP_L3_FULL", 1) && g.Lc[1] == g.E[1] && g.Lc[2] == g.E[2];
-  lds = (size_t)(l3::kWtWords + waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
+  a.full = g.Lc[1] == g.E[1] && g.Lc[2] == g.E[2];
+  lds = (size_t)(waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * waves));
   return nblk < ((int64_t)1 << 31);
@@ -527,11 +502,8 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
     a.maps = maps;
     a.W = pred->weights;
     a.b = pred->bias;
-    if (!l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, false, false, false, 1><<<grid, block, lds, stream>>>(a);
-    else if (a.full && l3_env("KMP_L3_WPE", 5) == 5)
-      l3::linear3d_kernel<T, false, true, true, 5><<<grid, block, lds, stream>>>(a);
-    else if (a.full) l3::linear3d_kernel<T, false, true, true, 1><<<grid, block, lds, stream>>>(a);
-    else l3::linear3d_kernel<T, false, true, false, 1><<<grid, block, lds, stream>>>(a);
+    if (a.full) l3::linear3d_kernel<T, false, true, 5><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, false, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -554,13 +526,10 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
     a.lo_in = lowres;
     a.W = pred->weights;
     a.b = pred->bias;
-    a.uld = l3_env("KMP_L3_ULD", 1) && a.Lcz > 0 && a.Lcy > 0;  // clamped map planes / rows exist
-    if (!l3_env("KMP_L3_SGPR", 1)) l3::linear3d_kernel<T, true, false, false, 1><<<grid, block, lds, stream>>>(a);
-    else if (a.full && a.uld && l3_env("KMP_L3_WPE", 5) == 5)
-      l3::linear3d_kernel<T, true, true, true, 5, true><<<grid, block, lds, stream>>>(a);
-    else if (a.full && a.uld) l3::linear3d_kernel<T, true, true, true, 1, true><<<grid, block, lds, stream>>>(a);
-    else if (a.full) l3::linear3d_kernel<T, true, true, true, 5><<<grid, block, lds, stream>>>(a);
-    else l3::linear3d_kernel<T, true, true, false, 1><<<grid, block, lds, stream>>>(a);
+    a.uld = a.Lcz > 0 && a.Lcy > 0;  // clamped map planes / rows exist
+    if (a.full && a.uld) l3::linear3d_kernel<T, true, true, 5, true><<<grid, block, lds, stream>>>(a);
+    else if (a.full) l3::linear3d_kernel<T, true, true, 5><<<grid, block, lds, stream>>>(a);
+    else l3::linear3d_kernel<T, true, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_decode");
   }
   return KMP_ERR_UNSUPPORTED;

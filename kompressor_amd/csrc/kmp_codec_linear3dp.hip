@@ -15,9 +15,19 @@
 // the channels of row Y-1 come from the lane above, across waves through LDS), in two sweeps over
 // the neighbourhood: per node row (dz, dy) one 2 x 16-byte LDS read of the lane's 7 nodes feeds
 // every channel of the sweep.  The chain runs on packed f32 VALU FMAs with the weights in scalar
-// registers (uniform loads): on CDNA4 the f32 MFMA rate equals the packed-VALU f32 rate, and the
-// MFMA layout would pad 19 channels to 32 and transpose cells <-> fragments; the per-channel chain
-// order is n ascending, so the f32 values are bit-identical to the oracle's fma chain.
+// registers (uniform loads); the per-channel chain order is n ascending, so the f32 values are
+// bit-identical to the oracle's fma chain.
+//
+// Why not the matrix cores: on MI355X the f32 MFMA (v_mfma_f32_16x16x4_f32 / 32x32x2) runs on the
+// same f32 datapath as the VALU -- tools/probe_mfma_valu.hip (profiles/round3/probe_mfma_valu.log):
+// one instruction stream interleaving f32 MFMAs with packed FMAs takes the SUM of the two streams'
+// times (322-331 us = 244-258 + 72-78), the same stream with bf16 MFMAs about the MAX (198 vs 180 +
+// 75).  So an f32 MFMA only replaces packed FMAs at about the same rate (27.7 vs 23.3 MAC/clk/SIMD
+// in the probe) and cannot overlap the epilogue, while the 19 channels pad to 16-wide tiles and the
+// results need a transpose back to the lanes that own the cells.  Three bit-exact matrix-core forms
+// were built and measured slower at C3 (profiles/round3/ab_linear3_mfma_rejected.log: a per-plane
+// 4-wave kernel 598 / 581 us and a one-wave-per-workgroup kernel 625 / 591 us against this kernel's
+// 551-564 / 509-515 us; round 2's z-rolling kernel 573 / 540) and removed.
 #include <cstdlib>
 
 #include "kmp_wave.h"
@@ -52,8 +62,6 @@ constexpr int kNQ = 5, kNC = 14;
 __constant__ const int kKQ[kNQ] = {5, 13, 14, 17, 18};
 __constant__ const int kKC[kNC] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16};
 
-constexpr int kSplatOff = 64 * 19;  // workspace floats: the plane c-1 weights {w, w}-splatted after Wr
-
 // W [N, 19] -> per sweep [node row][kk][dx] (N = NB^3, rows = NB^2): the order the sweeps consume.
 __global__ void __launch_bounds__(256) linear_reorder_kernel(const float* __restrict__ W, float* __restrict__ Wr,
                                                             int NB) {
@@ -64,10 +72,6 @@ __global__ void __launch_bounds__(256) linear_reorder_kernel(const float* __rest
     const int dx = u % NB, kk = (u / NB) % nk, row = u / (NB * nk);
     const int k = q ? kKQ[kk] : kKC[kk];
     Wr[t] = W[(row * NB + dx) * 19 + k];
-    if (q) {  // the plane c-1 weights again as {w, w} pairs (linear3w_kernel's SGPR operand pairs)
-      Wr[kSplatOff + 2 * t] = Wr[t];
-      Wr[kSplatOff + 2 * t + 1] = Wr[t];
-    }
   }
 }
 
@@ -403,407 +407,11 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   }
 }
 
-// ---- the matrix-core kernel: the default for P = 1 when Ex is 16, 32 or 64 ----
-//
-// One wave per workgroup: a wave owns R = 256 / Ex output rows Y0 .. Y0+R-1 of output plane c of
-// one tile (256 output positions) and needs, besides the stream rows, the channels of
-//   * cell plane c, rows Y0-1 .. Y0+R-1: 14 channels (rows >= Y0) / channels 3, 9, 10, 16 (row
-//     Y0-1, read by the row below) -- on the matrix cores;
-//   * cell plane c-1, rows Y0 .. Y0+R-1: channels 5, 13, 14, 18, and channel 17 of the row above
-//     -- on the VALU (packed FMAs, weights in scalar registers, as linear3dp_kernel).
-// Computing row Y0-1 itself (2 extra 16-cell groups at Ex = 32) removes every cross-wave exchange:
-// no workgroup barrier, ~9 KB of LDS per wave, so a CU holds as many of these waves as the register
-// budget allows and their load / matrix / VALU phases overlap freely.
-//
-// Staging: node planes c-2 .. c+2, node rows Y0-2 .. Y0+R+1 (mirrored into range, lsrc1), node
-// columns -1 .. Ex+2, as f32 in LDS.  Matrix chain, v_mfma_f32_16x16x4_f32 (A lane l = A[l & 15]
-// [l >> 4], B lane l = B[l >> 4][l & 15], D lane l = D[4 (l >> 4) + i][l & 15]):
-//   A[cell j][dx q] = staged node (plane dz, row of the cell + dy, column x0 + j + q), step s = 4 dz + dy,
-//   B[dx q][slot j] = W[4 s + q][KC[j]] (slots 14, 15 weigh 0; 16 VGPRs, loaded once),
-//   C = the bias of slot j, so D lane (j, q) = slot j of cells x0 + 4q .. x0 + 4q + 3.
-// An f32 MFMA is bit-for-bit the k-ordered fmaf chain (cdna_hip_programming.md §3), stepped in
-// n = 4 s + q order from the bias: the values are the oracle's chain (oracle.predictors.
-// linear_fma_chain) and the VALU kernel's.  Every A-operand address is one lane VGPR plus a
-// compile-time offset.  After the chains the staging area becomes the transpose tile that takes the
-// casted plane-c channels to the epilogue's lane-owns-4-cells layout (rows r and r+1 of it give a
-// lane its own cells and the row above).
-__constant__ const int kKCm[16] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16, -1, -1};
-
-template <int EX>
-struct L3WGeo {
-  static constexpr int P = 1, VX = 4, NB = 4, NPL = 5;
-  static constexpr int TXN = EX / VX, R = 64 / TXN, GPR = EX / 16;
-  static constexpr int NGRP = (R + 1) * GPR;  // 16-cell groups: rows Y0-1 .. Y0+R-1
-  static constexpr int SR = R + 4;            // staged node rows Y0-2 .. Y0+R+1
-  static constexpr int PITCH = EX + 4;        // staged node columns -1 .. EX+2, 16-byte rows
-  static constexpr int PLW = SR * PITCH;      // words per staged plane
-  static constexpr int TS = (R + 1) * EX + 8; // u16 per slot of the transpose tile
-  static constexpr int STAGE_W = NPL * PLW;
-  static constexpr int TILE_W = 14 * TS / 2;
-  static constexpr int REGION_W = STAGE_W > TILE_W ? STAGE_W : TILE_W;
-};
-
-#ifndef KMP_L3W_G
-#define KMP_L3W_G 4
-#endif
-#ifndef KMP_L3W_WPE
-#define KMP_L3W_WPE 3
-#endif
-template <bool DEC, int EX, int G>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KMP_L3W_WPE))) linear3w_kernel(L3P a) {
-  using T = uint16_t;
-  using Gm = L3WGeo<EX>;
-  constexpr int P = Gm::P, VX = Gm::VX, NB = Gm::NB, NPL = Gm::NPL;
-  constexpr int TXN = Gm::TXN, R = Gm::R, GPR = Gm::GPR, NGRP = Gm::NGRP;
-  constexpr int PITCH = Gm::PITCH, PLW = Gm::PLW, TS = Gm::TS;
-  constexpr uint32_t MASK = 0xffffu;
-  constexpr int NRD = (NGRP + G - 1) / G;  // rounds of G accumulators
-  using V = typename std::conditional<DEC, uint2, uint4>::type;
-  __shared__ __attribute__((aligned(16))) uint32_t smem[Gm::REGION_W];
-  float* st = (float*)smem;
-
-  const int lane = threadIdx.x;
-  const int tx = lane % TXN;
-  const int r = lane / TXN;
-  const int X = tx * VX;
-  int blk = (int)blockIdx.x;
-  if (a.xcd_per > 0) {
-    const int x = blk % 8, k = blk / 8;
-    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
-  }
-  const int nyw = a.nwv;  // row blocks per plane
-  const int nplanes = a.zend - a.zbegin;
-  const int yw = blk % nyw;
-  const int c = a.zbegin + (blk / nyw) % nplanes;
-  const int64_t b = blk / (nyw * nplanes);
-  const int Y0 = yw * R;
-  const int Y = Y0 + r;
-  const bool live = Y < a.Ey;
-  const int Yc = live ? Y : a.Ey - 1;
-  const bool vy1 = Y < a.Lcy;
-  const bool vy0 = Y >= 1;
-  const bool vz1 = c < a.Lcz, vz0 = c >= 1;
-
-  // the lane's MFMA B operands and bias column (their latency hides behind the node loads)
-  const int mj = lane & 15, mq = lane >> 4;
-  const int mch = kKCm[mj];
-  float wb[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) wb[s] = mch >= 0 ? a.W[(4 * s + mq) * 19 + mch] : 0.0f;
-  const float bias_ch = mch >= 0 ? a.b[mch] : 0.0f;
-
-  const int hplane = a.H * a.W_;
-  const int lplane = a.Ey * a.Ex;
-  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
-  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
-  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
-  const int hx = 2 * X;
-  const int ho_own = 2 * Yc * a.W_ + hx;
-  const int lo_own = Yc * a.Ex + X;
-
-  const T* mbase[7];
-  int mplane[7];
-  bool mok_y[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    int par[3];
-    map_parity(3, k, par);
-    const int ez = par[0] ? a.Lcz : a.Ez, ey = par[1] ? a.Lcy : a.Ey;
-    mplane[k] = ey * a.Ex;
-    mbase[k] = (const T*)a.maps.p[k] + b * (int64_t)ez * mplane[k] + Yc * a.Ex + X;
-    mok_y[k] = live && (!par[1] || vy1);
-  }
-
-  // ---- loads: the staged node rows (lane row r: staged rows r and, for r < 4, R + r), the lane's
-  // own node row of plane c and the stream rows ----
-  V nd[NPL][2];
-  const int jr1 = R + (r & 3);
-  const bool two = r < 4;
-  const int yn0 = lsrc1(min(Y0 - 2 + r, a.Ey + 1), a.Ly, a.Ey);
-  const int yn1 = lsrc1(min(Y0 - 2 + jr1, a.Ey + 1), a.Ly, a.Ey);
-#pragma unroll
-  for (int t = 0; t < NPL; ++t) {
-    const int sz = lsrc1(c - 2 + t, a.Lz, a.Ez);
-    if constexpr (DEC) {
-      const T* p = lin + sz * lplane + X;
-      nd[t][0] = ld8c(p + yn0 * a.Ex);
-      nd[t][1] = two ? ld8c(p + yn1 * a.Ex) : uint2{};
-    } else {
-      const T* p = hin + 2 * sz * hplane + hx;
-      nd[t][0] = ld16c(p + 2 * yn0 * a.W_);
-      nd[t][1] = two ? ld16c(p + 2 * yn1 * a.W_) : uint4{};
-    }
-  }
-
-  // ---- stage ----
-  {
-    constexpr int NHR = 4 * ((VX + 2 * P + 1 + 3) / 4) - VX - P;  // halo columns right of Ex
-    const bool xfirst = tx == 0, xlast = tx == TXN - 1;
-#pragma unroll
-    for (int t = 0; t < NPL; ++t) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) continue;
-        float v[VX];
-#pragma unroll
-        for (int i = 0; i < VX; ++i)
-          v[i] = (float)(DEC ? el8<T>(*(const uint2*)&nd[t][h], i) : el16<T>(*(const uint4*)&nd[t][h], 2 * i));
-        float* row = st + t * PLW + (h ? jr1 : r) * PITCH + P + X;
-#pragma unroll
-        for (int i = 0; i < VX; ++i) row[i] = v[i];
-        if (xfirst) row[-1] = v[0];  // node column -1 mirrors column 0
-        if (xlast) {
-#pragma unroll
-          for (int jj = 0; jj < NHR; ++jj) {
-            const int sx = lsrc1(a.Ex + jj, a.Lx, a.Ex) - X;
-            row[VX + jj] = sx == 3 ? v[3] : sx == 2 ? v[2] : sx == 1 ? v[1] : v[0];
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- the chains: plane c on the matrix cores (rounds of G groups), plane c-1 on the VALU ----
-  uint32_t pk[NGRP][2];
-  uint32_t PQ[kNQ][5];  // channels 5, 13, 14 (row Y), 17 (row Y-1), 18 (row Y) of cell plane c-1
-  {
-    typedef const __attribute__((address_space(4))) f32x2* CW2;
-    const CW2 Wq = (CW2)(a.Wr + kSplatOff);  // [node row s][kk][dx] as {w, w}
-    f32x2 aq[kNQ][2];
-#pragma unroll
-    for (int kk = 0; kk < kNQ; ++kk) {
-      const float bk = a.b[kKQ[kk]];
-      aq[kk][0] = (f32x2){bk, bk};
-      aq[kk][1] = (f32x2){bk, bk};
-    }
-    const float* ab = st + mj + mq;       // A operand: + compile-time plane / row / group offsets
-    const float* vb = st + r * PITCH + X; // the lane's VALU rows: staged row r (+1 for the row-Y chains)
-    // the VALU node rows (4 planes x 5 staged rows), VPR per round, one every VSTEP MFMA steps
-    constexpr int NVR = 20;
-    constexpr int VPR0 = (NVR + NRD - 1) / NRD;
-    constexpr int VPR = VPR0 <= 1 ? 1 : VPR0 <= 2 ? 2 : VPR0 <= 4 ? 4 : VPR0 <= 8 ? 8 : 16;
-    constexpr int VSTEP = 16 / VPR;
-#pragma unroll
-    for (int rd = 0; rd < NRD; ++rd) {
-      typedef float f32x4 __attribute__((ext_vector_type(4)));
-      f32x4 acc[G];
-#pragma unroll
-      for (int i = 0; i < G; ++i) acc[i] = (f32x4){bias_ch, bias_ch, bias_ch, bias_ch};
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int dz = s >> 2, dy = s & 3;
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const int u = rd * G + i;
-          if (u < NGRP) {
-            const int rr = u / GPR, gx = u % GPR;
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab[(1 + dz) * PLW + (rr + dy) * PITCH + gx * 16], wb[s],
-                                                          acc[i], 0, 0, 0);
-          }
-        }
-        // VALU node row vr (of NVR, ascending): plane vz = vr / 5, staged row r + vj (vj = vr % 5);
-        // row r + vj is node row dy' = vj - 1 of the row-Y chains and dy' = vj of channel 17's
-        const int vr = rd * VPR + s / VSTEP;
-        if (s % VSTEP == 0 && vr < NVR) {
-          const int vz = vr / 5, vj = vr % 5;
-          const float* rowp = (const float*)__builtin_assume_aligned(vb + vz * PLW + vj * PITCH, 16);
-          const float4 f0 = *(const float4*)rowp, f1 = *(const float4*)(rowp + 4);
-          const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-#pragma unroll
-          for (int kk = 0; kk < kNQ; ++kk) {
-            const bool k17 = kk == 3;
-            const int ddy = k17 ? vj : vj - 1;
-            if (ddy < 0 || ddy >= NB) continue;
-            const int sw = vz * NB + ddy;  // the chain's node-row index (n = 4 sw + dx)
-#pragma unroll
-            for (int dx = 0; dx < NB; ++dx) {
-              const f32x2 w2 = Wq[(sw * kNQ + kk) * NB + dx];
-              aq[kk][0] = __builtin_elementwise_fma((f32x2){f[dx], f[dx + 1]}, w2, aq[kk][0]);
-              aq[kk][1] = __builtin_elementwise_fma((f32x2){f[dx + 2], f[dx + 3]}, w2, aq[kk][1]);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const int u = rd * G + i;
-        if (u < NGRP) {
-          pk[u][0] = cvt_sat_mfma<T>(acc[i][0]) | (cvt_sat_mfma<T>(acc[i][1]) << 16);
-          pk[u][1] = cvt_sat_mfma<T>(acc[i][2]) | (cvt_sat_mfma<T>(acc[i][3]) << 16);
-        }
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < kNQ; ++kk) {
-      PQ[kk][1] = cvt_sat<T>(aq[kk][0].x);
-      PQ[kk][2] = cvt_sat<T>(aq[kk][0].y);
-      PQ[kk][3] = cvt_sat<T>(aq[kk][1].x);
-      PQ[kk][4] = cvt_sat<T>(aq[kk][1].y);
-    }
-  }
-  __syncthreads();  // the last staged read is done: the staging area becomes the transpose tile
-
-  // the stream rows, issued now (not up front) so they do not hold registers through the chains;
-  // the tile round trip and the other waves of the CU cover their latency
-  uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, o0 = e0, o1 = e0;
-  uint2 own = make_uint2(0, 0);
-  uint2 mv[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
-  if constexpr (DEC) {
-    own = ld8c(lin + c * lplane + lo_own);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int par[3];
-      map_parity(3, k, par);
-      if (mok_y[k] && (!par[0] || vz1)) mv[k] = ld8(mbase[k] + c * mplane[k]);
-    }
-  } else {
-    const T* p = hin + 2 * c * hplane;
-    e0 = ld16(p + ho_own);
-    if (live && vy1) e1 = ld16(p + ho_own + a.W_);
-    if (live && vz1) o0 = ld16(p + hplane + ho_own);
-    if (live && vz1 && vy1) o1 = ld16(p + hplane + ho_own + a.W_);
-  }
-
-  // plane-c channels: the lane's own cells (tile row r + 1) and the row above (tile row r)
-  uint32_t PC[kNC][5], A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1];
-  {
-    uint16_t* tile = (uint16_t*)smem;
-    if (mj < 14) {
-#pragma unroll
-      for (int u = 0; u < NGRP; ++u) {
-        const int rr = u / GPR, cx = (u % GPR) * 16 + 4 * mq;
-        *(uint2*)(tile + mj * TS + rr * EX + cx) = make_uint2(pk[u][0], pk[u][1]);
-      }
-    }
-    __syncthreads();
-    auto rd4 = [&](int slot, int row, uint32_t (&o)[VX + 1]) __attribute__((always_inline)) {
-      const uint2 v = *(const uint2*)(tile + slot * TS + row * EX + X);
-      o[1] = v.x & 0xffffu;
-      o[2] = v.x >> 16;
-      o[3] = v.y & 0xffffu;
-      o[4] = v.y >> 16;
-    };
-#pragma unroll
-    for (int kk = 0; kk < kNC; ++kk) rd4(kk, r + 1, PC[kk]);
-    rd4(3, r, A3);   // channel 3 -> slot 3
-    rd4(8, r, A9);   // channel 9 -> slot 8
-    rd4(9, r, A10);  // channel 10 -> slot 9
-    rd4(13, r, A16); // channel 16 -> slot 13
-  }
-  auto& P0 = PC[0]; auto& P1 = PC[1]; auto& P2 = PC[2]; auto& P4 = PC[4];
-  auto& P6 = PC[5]; auto& P7 = PC[6]; auto& P8 = PC[7]; auto& P11 = PC[10]; auto& P12 = PC[11];
-  auto& P15 = PC[12];
-  auto& Q5 = PQ[0]; auto& Q13 = PQ[1]; auto& Q14 = PQ[2]; auto& QA17 = PQ[3]; auto& Q18 = PQ[4];
-  A9[0] = shup(A9[VX], 1);  // cell (Y-1, X-1): the lane to the left
-  P1[0] = shup(P1[VX], 1);
-  P8[0] = shup(P8[VX], 1);
-  P12[0] = shup(P12[VX], 1);
-  Q13[0] = shup(Q13[VX], 1);
-  if (!live) return;
-
-  bool vx[VX + 1];
-#pragma unroll
-  for (int qq = 0; qq <= VX; ++qq) vx[qq] = (X - 1 + qq) >= 0 && (X - 1 + qq) < a.Lcx;
-  const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
-  const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
-  auto m = [&](const uint32_t (&v)[VX + 1], int qq, bool zok, bool yok) { return (zok && yok && vx[qq]) ? v[qq] : 0u; };
-  auto put8 = [&](int k, const uint32_t (&res)[VX]) {
-    int par[3];
-    map_parity(3, k, par);
-    if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res));
-  };
-  T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
-  uint32_t ownv[VX];
-#pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    if constexpr (DEC) ownv[i] = el8<T>(own, i);
-    else ownv[i] = el16<T>(e0, 2 * i);
-  }
-  auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) outv[i] = (pred[i] + el8<T>(mv[k], i)) & MASK;
-      else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
-    }
-  };
-
-  {  // X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); with the lowres
-    uint32_t pred[VX], outv[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i)
-      pred[i] = (m(P15, i + 1, vz1, vy1) + m(A16, i + 1, vz1, vy0) + m(QA17, i + 1, vz0, vy0) +
-                 m(Q18, i + 1, vz0, vy1)) >> ((nz * ny) >> 1);
-    code(6, pred, e0, 1, outv);
-    if constexpr (DEC) {
-      st16(h0, pack16<T, VX>(ownv, outv));
-    } else {
-      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(ownv));
-      put8(6, outv);
-    }
-  }
-  {  // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
-    uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pY[i] = (m(P11, i + 1, vz1, vy1) + m(P12, i, vz1, vy1) + m(Q13, i, vz0, vy1) + m(Q14, i + 1, vz0, vy1)) >>
-              ((nz * nx) >> 1);
-      pF[i] = (m(P4, i + 1, vz1, vy1) + m(Q5, i + 1, vz0, vy1)) >> (nz >> 1);
-    }
-    code(5, pY, e1, 0, oY);
-    code(2, pF, e1, 1, oF);
-    if constexpr (DEC) {
-      if (vy1) st16(h0 + a.W_, pack16<T, VX>(oY, oF));
-    } else {
-      put8(5, oY);
-      put8(2, oF);
-    }
-  }
-  {  // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
-    uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pZ[i] = (m(P7, i + 1, vz1, vy1) + m(P8, i, vz1, vy1) + m(A9, i, vz1, vy0) + m(A10, i + 1, vz1, vy0)) >>
-              ((ny * nx) >> 1);
-      pU[i] = (m(P2, i + 1, vz1, vy1) + m(A3, i + 1, vz1, vy0)) >> (ny >> 1);
-    }
-    code(4, pZ, o0, 0, oZ);
-    code(1, pU, o0, 1, oU);
-    if constexpr (DEC) {
-      if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
-    } else {
-      put8(4, oZ);
-      put8(1, oU);
-    }
-  }
-  {  // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
-    uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pL[i] = (m(P0, i + 1, vz1, vy1) + m(P1, i, vz1, vy1)) >> (nx >> 1);
-      pC[i] = m(P6, i + 1, vz1, vy1);
-    }
-    code(0, pL, o1, 0, oL);
-    code(3, pC, o1, 1, oC);
-    if constexpr (DEC) {
-      if (vz1 && vy1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
-    } else {
-      put8(0, oL);
-      put8(3, oC);
-    }
-  }
-}
-
 }  // namespace l3p
 
 // the reordered weights live in the caller's workspace (kmp_*_workspace_bytes covers them: the
 // linear predictor's generic workspace is B * cells * 19 samples)
-constexpr size_t kL3pWsBytes = 2 * 64 * 19 * sizeof(float);  // Wr + the splatted plane c-1 weights
+constexpr size_t kL3pWsBytes = 64 * 19 * sizeof(float);
 
 static int l3p_env(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -812,8 +420,7 @@ static int l3p_env(const char* name, int dflt) {
 
 template <typename T>
 static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
-                               const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds,
-                               bool& mfma) {
+                               const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 4;
   if (!std::is_same<T, uint16_t>::value) return false;
   if (l3p_env("KMP_DISABLE_FAST", 0) || l3p_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
@@ -848,18 +455,6 @@ static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   const int npl = 2 * P + 3;
   lds = (size_t)(npl * a.nr * a.pitch + waves * l3p::kXch * g.E[2]) * sizeof(uint32_t);
   if (lds > 64 * 1024) return false;
-  // the matrix-core kernel (one wave per workgroup): Ex 16 / 32 / 64
-  mfma = l3p_env("KMP_L3P_MFMA", 1) && P == 1 && (g.E[2] == 16 || g.E[2] == 32 || g.E[2] == 64);
-  if (mfma) {
-    const int64_t R = 64 / txn, nyw = ceil_div(g.E[1], R);
-    a.nwv = (int)nyw;
-    const int64_t nblk = B * (ze - zb) * nyw;
-    a.xcd_per = (l3p_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)((ze - zb) * nyw) : 0;
-    grid = dim3((unsigned)nblk);
-    block = dim3(64);
-    lds = 0;  // static
-    return nblk < ((int64_t)1 << 31);
-  }
   const int64_t nblk = B * (ze - zb);
   a.xcd_per = (l3p_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
   grid = dim3((unsigned)nblk);
@@ -875,8 +470,7 @@ int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
-    bool mfma = false;
-    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds, mfma)) return KMP_ERR_UNSUPPORTED;
+    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -888,11 +482,8 @@ int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    if (!mfma) l3p::linear3dp_kernel<T, false, 1><<<grid, block, lds, stream>>>(a);
-    else if (a.Ex == 16) l3p::linear3w_kernel<false, 16, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    else if (a.Ex == 32) l3p::linear3w_kernel<false, 32, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    else l3p::linear3w_kernel<false, 64, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    return check_launch(mfma ? "linear3w_encode" : "linear3dp_encode");
+    l3p::linear3dp_kernel<T, false, 1><<<grid, block, lds, stream>>>(a);
+    return check_launch("linear3dp_encode");
   }
   return KMP_ERR_UNSUPPORTED;
 }
@@ -905,8 +496,7 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
-    bool mfma = false;
-    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds, mfma)) return KMP_ERR_UNSUPPORTED;
+    if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
       if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
@@ -919,11 +509,8 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    if (!mfma) l3p::linear3dp_kernel<T, true, 1><<<grid, block, lds, stream>>>(a);
-    else if (a.Ex == 16) l3p::linear3w_kernel<true, 16, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    else if (a.Ex == 32) l3p::linear3w_kernel<true, 32, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    else l3p::linear3w_kernel<true, 64, KMP_L3W_G><<<grid, block, lds, stream>>>(a);
-    return check_launch(mfma ? "linear3w_decode" : "linear3dp_decode");
+    l3p::linear3dp_kernel<T, true, 1><<<grid, block, lds, stream>>>(a);
+    return check_launch("linear3dp_decode");
   }
   return KMP_ERR_UNSUPPORTED;
 }

@@ -244,13 +244,13 @@ __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
 
 // A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; a multiple of 8
 // workgroups keeps every virtual block on the XCD of the image-per-XCD order): fewer, longer-lived
-// workgroups than one per 16 output rows (KMP_W2_ITERS virtual blocks per workgroup)
+// workgroups than one per 16 output rows (2 virtual blocks per workgroup)
 template <typename T, bool DEC, bool ONE, bool LIN, bool STC = false>
 __global__ void __launch_bounds__(256) wave2d_kernel(W2 a) {
   for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_body<T, DEC, ONE, LIN, STC>(a, v);
 }
 
-// uint8 form of the mean kernel (BASELINE config C2), SWAR: the lane's 8 cells travel as 4 words
+// uint8 decode form of the mean kernel (BASELINE config C2), SWAR: the lane's 8 cells travel as 4 words
 // of two 16-bit lanes each, so every node / mean / prediction / residual step is one 32-bit op
 // for two cells (node pair sums <= 510, means <= 255: no carry between the halves; residuals add
 // 256 per half before subtracting, so no borrow).  Bytes are split / merged with v_perm.  The
@@ -265,11 +265,9 @@ __device__ __forceinline__ uint32_t shift_pairs(uint32_t hi, uint32_t lo) {  // 
   return __builtin_amdgcn_alignbit(hi, lo, 16);
 }
 
-template <bool DEC>
-__device__ __forceinline__ void wave2d_u8_body(const W2& a, int vblk) {
+__device__ __forceinline__ void wave2d_u8_dec_body(const W2& a, int vblk) {
   constexpr int VX = 8;
   constexpr uint32_t B8 = 0x00ff00ffu;
-  using V = typename std::conditional<DEC, uint2, uint4>::type;
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
@@ -298,41 +296,23 @@ __device__ __forceinline__ void wave2d_u8_body(const W2& a, int vblk) {
 
   const int64_t himg = (int64_t)a.H * a.W;
   const int hx = 2 * X;
-  const uint8_t* hin = DEC ? nullptr : (const uint8_t*)a.hi_in + b * himg;
-  uint8_t* hout = DEC ? (uint8_t*)a.hi_out + b * himg : nullptr;
-  const uint8_t* lin = DEC ? (const uint8_t*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
+  uint8_t* hout = (uint8_t*)a.hi_out + b * himg;
+  const uint8_t* lin = (const uint8_t*)a.lo_in + b * (int64_t)a.Ey * a.Ex;
   const int64_t m_lr = (b * a.Lcy + Yc) * a.Ex + X;
   const int64_t m_ud = (b * a.Ey + Yc) * a.Ex + X;
 
-  V own{}, halo{};
-  uint4 o0 = make_uint4(0, 0, 0, 0);
+  uint2 own{}, halo{};
   uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
-  if constexpr (DEC) {
-    if (live) own = ld8c(lin + Yc * a.Ex + X);
-    if (need_halo) halo = ld8c(lin + yh * a.Ex + X);
-    if (live && vy1) mv[0] = ld8((const uint8_t*)a.maps.p[0] + m_lr);
-    if (live) mv[1] = ld8((const uint8_t*)a.maps.p[1] + m_ud);
-    if (live && vy1) mv[2] = ld8((const uint8_t*)a.maps.p[2] + m_lr);
-  } else {
-    if (live) own = ld16c(hin + 2 * Yc * a.W + hx);
-    if (need_halo) halo = ld16c(hin + 2 * yh * a.W + hx);
-    if (live && vy1) o0 = ld16(hin + (2 * Yc + 1) * a.W + hx);
-  }
+  if (live) own = ld8c(lin + Yc * a.Ex + X);
+  if (need_halo) halo = ld8c(lin + yh * a.Ex + X);
+  if (live && vy1) mv[0] = ld8((const uint8_t*)a.maps.p[0] + m_lr);
+  if (live) mv[1] = ld8((const uint8_t*)a.maps.p[1] + m_ud);
+  if (live && vy1) mv[2] = ld8((const uint8_t*)a.maps.p[2] + m_lr);
 
   // nodes as pairs: N[k] = {n[2k], n[2k+1]}
-  uint32_t N[4], NH[4], XO[4] = {0, 0, 0, 0};
-  if constexpr (DEC) {
-    N[0] = lo_pair(own.x); N[1] = hi_pair(own.x); N[2] = lo_pair(own.y); N[3] = hi_pair(own.y);
-    NH[0] = lo_pair(halo.x); NH[1] = hi_pair(halo.x); NH[2] = lo_pair(halo.y); NH[3] = hi_pair(halo.y);
-  } else {
-    const uint32_t w[4] = {own.x, own.y, own.z, own.w}, h[4] = {halo.x, halo.y, halo.z, halo.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      N[k] = w[k] & B8;
-      XO[k] = (w[k] >> 8) & B8;  // row 2Y odd x: the UD map's ground truth
-      NH[k] = h[k] & B8;
-    }
-  }
+  uint32_t N[4], NH[4];
+  N[0] = lo_pair(own.x); N[1] = hi_pair(own.x); N[2] = lo_pair(own.y); N[3] = hi_pair(own.y);
+  NH[0] = lo_pair(halo.x); NH[1] = hi_pair(halo.x); NH[2] = lo_pair(halo.y); NH[3] = hi_pair(halo.y);
   uint32_t nx1 = shdn(N[0], 1), nhx1 = shdn(NH[0], 1);  // node X+8 (low half)
   if (xlast) {  // the mirrored node Ex-1 (even pad), or no cell at all (odd)
     nx1 = N[3] >> 16;
@@ -377,20 +357,7 @@ __device__ __forceinline__ void wave2d_u8_body(const W2& a, int vblk) {
     const uint32_t su = M0[k] + M1[k];
     PU[k] = ud2 ? (su >> 1) & 0x7fff7fffu : su;
   }
-  if constexpr (!DEC) {
-    const uint32_t o[4] = {o0.x, o0.y, o0.z, o0.w};
-    uint32_t rl[4], ru[4], rc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      rl[k] = ((o[k] & B8) + 0x01000100u - PL[k]) & B8;          // LR (1,0): row 2Y+1, even x
-      ru[k] = (XO[k] + 0x01000100u - PU[k]) & B8;                // UD (0,1): row 2Y, odd x
-      rc[k] = (((o[k] >> 8) & B8) + 0x01000100u - M1[k]) & B8;   // C  (1,1): row 2Y+1, odd x
-    }
-    st8((uint8_t*)a.lo_out + m_ud, make_uint2(pack_pairs(N[0], N[1]), pack_pairs(N[2], N[3])));
-    if (vy1) st8((uint8_t*)a.maps.p[0] + m_lr, make_uint2(pack_pairs(rl[0], rl[1]), pack_pairs(rl[2], rl[3])));
-    st8((uint8_t*)a.maps.p[1] + m_ud, make_uint2(pack_pairs(ru[0], ru[1]), pack_pairs(ru[2], ru[3])));
-    if (vy1) st8((uint8_t*)a.maps.p[2] + m_lr, make_uint2(pack_pairs(rc[0], rc[1]), pack_pairs(rc[2], rc[3])));
-  } else {
+  {
     const uint32_t el[4] = {lo_pair(mv[0].x), hi_pair(mv[0].x), lo_pair(mv[0].y), hi_pair(mv[0].y)};
     const uint32_t eu[4] = {lo_pair(mv[1].x), hi_pair(mv[1].x), lo_pair(mv[1].y), hi_pair(mv[1].y)};
     const uint32_t ec[4] = {lo_pair(mv[2].x), hi_pair(mv[2].x), lo_pair(mv[2].y), hi_pair(mv[2].y)};
@@ -407,9 +374,8 @@ __device__ __forceinline__ void wave2d_u8_body(const W2& a, int vblk) {
   }
 }
 
-template <bool DEC>
-__global__ void __launch_bounds__(256) wave2d_u8_kernel(W2 a) {
-  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_u8_body<DEC>(a, v);
+__global__ void __launch_bounds__(256) wave2d_u8_dec_kernel(W2 a) {
+  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave2d_u8_dec_body(a, v);
 }
 
 }  // namespace w2
@@ -453,7 +419,7 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.ybeg = (int)yb;
   a.yend = (int)ye;
   const int64_t nblk = B * ngrp;
-  const int64_t iters = std::max(1, w2_env("KMP_W2_ITERS", 2));  // 2: +5 % encode, +1.5 % decode at C2 (ab_wave2d_iters.log)
+  const int64_t iters = 2;  // 2: +5 % encode, +1.5 % decode at C2 (ab_wave2d_iters.log)
   int64_t nwg = ceil_div(nblk, iters);
   if (a.xcd_per > 0) nwg = ceil_div(nwg, (int64_t)8) * 8;  // keep v % 8 == blockIdx % 8
   a.nvblk = (int)nblk;
@@ -469,10 +435,10 @@ static void launch_wave2d_s(bool one, bool lin, dim3 grid, dim3 block, hipStream
     else w2::wave2d_kernel<T, DEC, true, false, STC><<<grid, block, 0, s>>>(a);
   } else {
     if (lin) w2::wave2d_kernel<T, DEC, false, true, STC><<<grid, block, 0, s>>>(a);
-    // SWAR u8 form: decode 24.0 vs 24.8 us at C2 on one box; encode 26.2 vs 25.4 (kept behind a
-    // knob: the encode is bound by its row loads, not VALU) -- profiles/round1/ab_wave2d_swar.log
-    else if (std::is_same<T, uint8_t>::value && !w2_env("KMP_DISABLE_SWAR", 0) && (DEC || w2_env("KMP_W2_SWAR_ENC", 0)))
-      w2::wave2d_u8_kernel<DEC><<<grid, block, 0, s>>>(a);
+    // SWAR u8 decode: 24.0 vs 24.8 us at C2 on one box; the SWAR encode measured slower (26.2 vs
+    // 25.4: bound by its row loads, not VALU) and was removed -- profiles/round1/ab_wave2d_swar.log
+    else if (DEC && std::is_same<T, uint8_t>::value && !w2_env("KMP_DISABLE_SWAR", 0))
+      w2::wave2d_u8_dec_kernel<<<grid, block, 0, s>>>(a);
     else w2::wave2d_kernel<T, DEC, false, false, STC><<<grid, block, 0, s>>>(a);
   }
 }

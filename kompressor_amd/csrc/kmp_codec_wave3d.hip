@@ -416,13 +416,10 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.nslab = (int)nslab;
   const int64_t nblk = B * nslab * nyg;
   a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
-  a.nt_nodes = w3_env("KMP_W3_NT_NODES", 0);
+  a.nt_nodes = 0;
   a.nB = B;
-  const int64_t iters = std::max(1, w3_env("KMP_W3_ITERS", 1));
-  int64_t nwg = ceil_div(nblk, iters);
-  if (a.xcd_per > 0) nwg = ceil_div(nwg, (int64_t)8) * 8;  // keep v % 8 == blockIdx % 8
   a.nvblk = (int)nblk;
-  grid = dim3((unsigned)std::min(nwg, nblk));
+  grid = dim3((unsigned)nblk);  // one workgroup per block (grid-stride blocks measured slower, round 2)
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);
 }

@@ -616,12 +616,11 @@ static int w3p_env(const char* name, int dflt) {
 
 // Output planes per workgroup and register budget, per (p, direction): the measured optimum at C3
 // (profiles/round1/w3p_sweep.log; 64^3 u16 tiles): p = 1 PL 2 (decode at 4 waves / SIMD),
-// p = 2 encode PL 1, decode PL 2 at 3 waves / SIMD.  KMP_W3P_PL / KMP_W3P_WPE override.
+// p = 2 encode PL 1, decode PL 2 at 3 waves / SIMD.  KMP_W3P_PL overrides the planes.
 static void w3p_cfg(int P, bool dec, int& pl, int& wpe) {
   pl = (P == 2 && !dec) ? 1 : 2;
   wpe = dec ? (P == 1 ? 4 : 3) : 1;
   pl = w3p_env("KMP_W3P_PL", pl) == 1 ? 1 : 2;
-  wpe = w3p_env("KMP_W3P_WPE", wpe);
 }
 
 template <typename T>

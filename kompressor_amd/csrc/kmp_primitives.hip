@@ -1342,15 +1342,13 @@ int kmp_maps_from_predictions(int32_t nsp, int32_t dtype, const void* preds, int
       constexpr int V = 16 / (int)sizeof(T);
       const int K = nsp == 3 ? 19 : 5, NS = nsp == 3 ? 2 : 1;
       const int32_t XO = (int32_t)std::min<int64_t>(ce.e[2] + 1, 64);
-      const char* yb_env = std::getenv("KMP_MFP_YB");
-      const int32_t YB = yb_env ? std::max(1, std::atoi(yb_env)) : std::max(1, std::min(8, kThreads / XO));
+      const int32_t YB = std::max(1, std::min(8, kThreads / XO));
       const int32_t nyb = (int32_t)ceil_div(ce.e[1] + 1, YB), nxb = (int32_t)ceil_div(ce.e[2] + 1, XO);
       const int32_t nchunk = (int32_t)ceil_div((int64_t)(XO + 1) * K, V);
       const int32_t RP = nchunk * V;
       // enough workgroups to fill the chip: split the z roll into nzc runs of ZC output planes
       const int64_t fz = nsp == 3 ? ce.e[0] + 1 : 1;
-      const char* want_env = std::getenv("KMP_MFP_WANT");
-      const int64_t want = ceil_div(want_env ? std::atoi(want_env) : 4096, B * nyb * nxb);
+      const int64_t want = ceil_div(4096, B * nyb * nxb);
       const int32_t ZC = (int32_t)ceil_div(fz, std::max<int64_t>(1, std::min<int64_t>(want, fz)));
       const int32_t nzc = (int32_t)ceil_div(fz, ZC);
       const size_t lds = (size_t)NS * (YB + 1) * RP * sizeof(T);
@@ -1406,7 +1404,9 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
       // one workgroup per output plane when the plane's window planes fit LDS
       const int64_t plane = S.e[1] * S.e[2];
-      // PPB output planes per workgroup: 1, or 2 when KMP_MP_PPB=2 and its LDS fits
+      // PPB output planes per workgroup: 2 where its LDS fits (the cell plane between the two output
+      // planes summed once: p = 0 101 -> 94 us, p = 1 300 -> 270 us at 512 C3 windows,
+      // profiles/round2/ab_mean_predict_ppb.log), else 1; KMP_MP_PPB=1 forces one
       auto lds_for = [&](int q, int64_t& nb_, int64_t& xs_) {
         nb_ = 16 * (ceil_div((2 * padding + 2 + q) * plane * (int64_t)sizeof(T), 16) + 1);
         xs_ = padding > 0 ? 4 * (2 * padding + 2 + q) * S.e[1] * cells.e[2] : 0;
@@ -1414,7 +1414,7 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
       };
       const char* ppb_env = std::getenv("KMP_MP_PPB");
       int64_t nodes_bytes = 0, xs_bytes = 0;
-      int ppb = ppb_env && std::atoi(ppb_env) == 2 ? 2 : 1;
+      int ppb = ppb_env && std::atoi(ppb_env) == 1 ? 1 : 2;
       int64_t lds_plane = lds_for(ppb, nodes_bytes, xs_bytes);
       if (ppb == 2 && lds_plane > 64 * 1024) {
         ppb = 1;
@@ -1423,13 +1423,12 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
       const int64_t ngrp = ceil_div(cells.e[0] + 1, (int64_t)ppb);
       const int64_t nblk_plane = B * ngrp;
       if (nsp == 3 && C == 1 && padding <= 2 && lds_plane <= 64 * 1024 && nblk_plane < ((int64_t)1 << 31) &&
-          (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31) &&
-          !std::getenv("KMP_MP_LDS")) {
+          (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31)) {
         auto launch = [&](auto kern) {
           kern<<<(unsigned)nblk_plane, kThreads, (size_t)lds_plane, (hipStream_t)stream>>>(
               (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2], outs,
               B % 8 == 0 ? (int32_t)ngrp : 0, (int32_t)nodes_bytes, (int32_t)xs_bytes);
-          return check_launch("mean_predict_plane");
+          return check_launch(ppb == 2 ? "mean_predict_plane2" : "mean_predict_plane");
         };
         if (ppb == 2) {
           if (padding == 0) return launch(mean_predict_plane_kernel<T, 0, 2>);

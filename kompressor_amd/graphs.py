@@ -107,15 +107,20 @@ class CodecPlan:
         self.lowres, (maps, dims) = result
         self.maps, self.dims = list(maps), tuple(dims)
 
-    def encode(self, highres=None):
+    def encode(self, highres=None, copy=False):
         """Replay the encode (after copying ``highres`` into the static input, if given);
-        returns ``(lowres, (maps, dims))`` -- the plan's static buffers."""
+        returns ``(lowres, (maps, dims))``.  Unlike the eager ``encode``, these are the plan's
+        static buffers: the next replay overwrites them in place, so a caller that keeps a result
+        across two calls must clone it -- or pass ``copy=True`` to get fresh tensors."""
         if highres is not None:
             self.highres.copy_(dev.to_device(highres)[0])
         self._g_enc.replay()
+        if copy:
+            return self.lowres.clone(), (tuple(m.clone() for m in self.maps), tuple(self.dims))
         return self.lowres, (tuple(self.maps), tuple(self.dims))
 
-    def decode(self):
-        """Replay the decode of the static lowres / maps into ``plan.out``."""
+    def decode(self, copy=False):
+        """Replay the decode of the static lowres / maps into ``plan.out`` and return it -- a static
+        buffer the next replay overwrites (``copy=True`` returns a fresh tensor)."""
         self._g_dec.replay()
-        return self.out
+        return self.out.clone() if copy else self.out

@@ -163,10 +163,13 @@ def _with_halo(x, own, need, ranges, needs, group):
     for r in range(world):
         lo_need = ranges[r][0] - needs[r][0]
         hi_need = needs[r][1] - ranges[r][1]
-        if (r > 0 and lo_need > ranges[r - 1][1] - ranges[r - 1][0]) or \
-                (r < world - 1 and hi_need > ranges[r + 1][1] - ranges[r + 1][0]):
-            raise AssertionError(f'slab of rank {r - 1 if lo_need > 0 and r > 0 else r + 1} is thinner than the halo '
-                                 f'rank {r} needs: use fewer ranks')
+        if r > 0 and lo_need > ranges[r - 1][1] - ranges[r - 1][0]:
+            thin = r - 1   # the lower neighbour cannot supply the planes above rank r
+        elif r < world - 1 and hi_need > ranges[r + 1][1] - ranges[r + 1][0]:
+            thin = r + 1   # the upper neighbour cannot supply the planes below rank r
+        else:
+            continue
+        raise AssertionError(f'slab of rank {thin} is thinner than the halo rank {r} needs: use fewer ranks')
     local, sends, recvs = _exchange(x, own, need, world, rank, group, ranges)
     if rank > 0:  # rank r-1 needs my first planes above its own
         n_up = needs[rank - 1][1] - ranges[rank - 1][1]

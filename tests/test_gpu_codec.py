@@ -360,11 +360,11 @@ def test_categorical_matches_golden(kom, name, chunk):
 
 
 @pytest.mark.parametrize('vec', ['1', '0'])
-def test_categorical_coder_vs_oracle(kom, monkeypatch, vec):
-    """Rank coder vs the oracle's stable argsort; vec='1' serves L % 4 == 0, L <= 512 with the 16-byte
-    vector kernels (KMP_CAT_VEC), '0' with the scalar ones."""
+def test_categorical_coder_vs_oracle(kom, vec):
+    """Rank coder vs the oracle's stable argsort.  vec='1': 16-byte-aligned logits, so L % 4 == 0,
+    L <= 512 runs the vector kernels and the other L the scalar ones; vec='0': the logits start 4
+    bytes past a 16-byte boundary, which sends every L to the scalar kernels."""
     import oracle
-    monkeypatch.setenv('KMP_CAT_VEC', vec)
     rng = np.random.default_rng(7)
     for L, dt in ((256, np.uint8), (300, np.uint8), (17, np.uint16), (2000, np.uint16), (5, np.int32),
                   (64, np.uint8), (128, np.uint16), (512, np.uint16), (1, np.uint8), (2, np.uint8),
@@ -383,10 +383,17 @@ def test_categorical_coder_vs_oracle(kom, monkeypatch, vec):
             logits[7, :4] = [np.inf, -np.inf, np.nan, np.inf]
         x = rng.integers(0, min(L + 3, np.iinfo(dt).max), size=513).astype(dt)
         x[::3] = rng.integers(0, min(L, 10), size=x[::3].size)  # small ranks / classes (the peel)
-        got = kom.utils.encode_categorical(logits, x)
+        lg = torch.from_numpy(logits).cuda()
+        if vec == '0':
+            buf = torch.empty(logits.size + 4, dtype=torch.float32, device='cuda')
+            lg = buf[1:1 + logits.size].view(logits.shape)
+            lg.copy_(torch.from_numpy(logits))
+            assert lg.data_ptr() % 16 == 4
+        xg = torch.from_numpy(x).cuda()
+        got = kom.utils.encode_categorical(lg, xg).cpu().numpy()
         want = oracle.common.encode_categorical(logits, x)
         assert np.array_equal(got, want), L
-        got = kom.utils.decode_categorical(logits, x)
+        got = kom.utils.decode_categorical(lg, xg).cpu().numpy()
         want = oracle.common.decode_categorical(logits, x)
         assert np.array_equal(got, want), L
 
@@ -547,14 +554,11 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
     (2, 9, 16, 1),         # one lane per row, Ey = 5 < rows
     (1, 40, 1024, 1),      # 64 lanes per row: the one-row wave (generic kernel only)
 ])
-@pytest.mark.parametrize('mode', ['swar_dec', 'swar_both', 'generic'])
+@pytest.mark.parametrize('mode', ['swar_dec', 'generic'])
 def test_wave2d_u8_p0_matches_oracle(kom, shape, mode, monkeypatch):
-    """The p = 0 uint8 image kernels of kmp_codec_wave2d.hip -- the SWAR form (decode by default,
-    encode behind KMP_W2_SWAR_ENC) and the generic per-cell form (KMP_DISABLE_SWAR) -- against
-    the oracle, whole-image and chunked."""
-    if mode == 'swar_both':
-        monkeypatch.setenv('KMP_W2_SWAR_ENC', '1')
-    elif mode == 'generic':
+    """The p = 0 uint8 image kernels of kmp_codec_wave2d.hip -- the SWAR decode (the default) and
+    the generic per-cell form (KMP_DISABLE_SWAR) -- against the oracle, whole-image and chunked."""
+    if mode == 'generic':
         monkeypatch.setenv('KMP_DISABLE_SWAR', '1')
     import oracle
     from oracle import predictors as OP

@@ -36,6 +36,14 @@ def test_plan_matches_eager(kom, ndim, shape, dtype, p):
         assert torch.equal(plan.decode(), x)
         # the eager decode of the plan's outputs agrees too
         assert torch.equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
+    # copy=True: fresh tensors that the next replay does not overwrite
+    lo_c, (maps_c, _) = plan.encode(x, copy=True)
+    rec_c = plan.decode(copy=True)
+    keep = (lo_c.clone(), [m.clone() for m in maps_c], rec_c.clone())
+    plan.encode(torch.zeros_like(x))
+    plan.decode()
+    assert lo_c.data_ptr() != plan.lowres.data_ptr() and torch.equal(lo_c, keep[0])
+    assert all(torch.equal(a, b) for a, b in zip(maps_c, keep[1])) and torch.equal(rec_c, keep[2])
 
 
 def _torch_predictions_fn(kom, ndim, padding):

@@ -83,17 +83,10 @@ def test_linear_chunks(kom):
 
 @pytest.mark.parametrize('shape', [(8, 64, 64, 64, 1), (2, 17, 30, 16, 1), (1, 9, 14, 128, 1), (2, 12, 33, 32, 1),
                                    (1, 6, 8, 8, 1), (1, 10, 40, 32, 1), (2, 9, 32, 128, 1)])
-@pytest.mark.parametrize('variant', ['rolling_mfma', 'valu', 'plane_mfma'])
-def test_linear_fused_p1(kom, shape, variant, monkeypatch):
-    """The fused LinearPredictor p = 1 volume kernels: residuals and lowres bit-exact to the
-    oracle's fma chain + aggregation, lossless, z-region (chunked) launches -- for the per-plane
-    matrix-core kernel (linear3dm_kernel, the default where Ex is 16 / 32 / 64: the 14 plane-c
-    channels on v_mfma_f32_16x16x4_f32, the same k-ordered chain, so the same bits), the per-plane
-    packed-FMA kernel (KMP_L3P_MFMA=0) and the rolling matrix-core kernel (KMP_L3R=1).  The shapes
-    cover every Ex the MFMA kernel takes, a partial last wave (Ey 20 at Ex 16) and the VALU kernel's
-    other widths."""
-    monkeypatch.setenv('KMP_L3R', '1' if variant == 'rolling_mfma' else '0')
-    monkeypatch.setenv('KMP_L3P_MFMA', '1' if variant == 'plane_mfma' else '0')
+def test_linear_fused_p1(kom, shape):
+    """The fused LinearPredictor p = 1 volume kernel (kmp_codec_linear3dp.hip, packed-FMA chain):
+    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, z-region
+    (chunked) launches, over lowres widths 4 .. 64 and partial last waves."""
     hi = _data(shape, np.uint16, 7)
     w, b = _weights(3, 1, 8, np.uint16)
     pred = kom.LinearPredictor(w, b, 1, 3)
@@ -101,17 +94,13 @@ def test_linear_fused_p1(kom, shape, variant, monkeypatch):
     want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
                                                 padding=1)
     lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, hi, padding=1)
-    ex, ey = lo.shape[3], lo.shape[2]   # the stored lowres extents (Ex, Ey of the kernels)
-    mfma_ok = ex in (16, 32, 64) and ey <= 1024 // ex
-    kern = {'rolling_mfma': ('linear3r', 'linear3dp'), 'valu': ('linear3dp',)}.get(
-        variant, ('linear3w',) if mfma_ok else ('linear3dp',))
-    assert kom._lib.lib.kmp_last_launch().decode() in [k + '_encode' for k in kern]
+    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3dp_encode'
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, c) in enumerate(zip(maps, want_maps)):
         bad = np.argwhere(a != c)
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
     assert np.array_equal(V.decode(pred, V.decode_values_uint16, lo, (maps, dims), padding=1), hi)
-    assert kom._lib.lib.kmp_last_launch().decode() in [k + '_decode' for k in kern]
+    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3dp_decode'
     lo2, (maps2, _) = V.encode_chunks(pred, V.encode_values_uint16, hi, chunk=5, padding=1)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
 
@@ -119,20 +108,13 @@ def test_linear_fused_p1(kom, shape, variant, monkeypatch):
 @pytest.mark.parametrize('shape,dtype', [((4, 64, 64, 64, 1), np.uint16), ((2, 17, 30, 16, 1), np.uint16),
                                          ((2, 12, 33, 32, 1), np.uint16), ((1, 9, 14, 128, 1), np.uint8),
                                          ((3, 10, 9, 64, 1), np.uint8)])
-@pytest.mark.parametrize('sg,uld,full,wpe', [('1', '1', '1', '5'), ('1', '1', '1', '4'), ('1', '1', '0', '5'),
-                                              ('0', '1', '1', '5'), ('1', '0', '1', '5')])
-def test_linear_fused_p0(kom, shape, dtype, sg, uld, full, wpe, monkeypatch):
-    """The fused LinearPredictor p = 0 volume kernel (kmp_codec_linear3d.hip) with each weight
-    source -- uniform (scalar) loads from W / b (KMP_L3_SGPR=1, default) or the LDS copy (0) --,
-    with the decode's unconditional (KMP_L3_ULD=1, default) or guarded loads, and with the FULL
-    body (even y / x: only row-0 / lane-0 masks, missing z planes through zero weights; 5 or 4 waves
-    per SIMD) or the general one (KMP_L3_FULL=0): residuals and lowres bit-exact to the oracle's fma
-    chain + aggregation, lossless, chunked.  The shapes cover FULL with an odd depth (the last output
-    plane has no cell plane c: zero weights for P) and the general body (odd heights)."""
-    monkeypatch.setenv('KMP_L3_SGPR', sg)
-    monkeypatch.setenv('KMP_L3_ULD', uld)
-    monkeypatch.setenv('KMP_L3_FULL', full)
-    monkeypatch.setenv('KMP_L3_WPE', wpe)
+def test_linear_fused_p0(kom, shape, dtype):
+    """The fused LinearPredictor p = 0 volume kernel (kmp_codec_linear3d.hip: weights in scalar
+    registers, the decode's unconditional loads, the FULL body for even y / x -- only row-0 / lane-0
+    masks, missing z planes through zero weights -- and the general body for odd heights):
+    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, chunked.  The
+    shapes cover FULL with an odd depth (the last output plane has no cell plane c) and the general
+    body."""
     hi = _data(shape, dtype, 9)
     w, b = _weights(3, 0, 10, dtype)
     pred = kom.LinearPredictor(w, b, 0, 3)

@@ -120,21 +120,36 @@ def test_coders_keep_torch(kom):
     assert int(out.to(torch.int32).sum()) == 0
 
 
+def _mp_lds_bytes(window_shape, itemsize, padding, q):
+    """The LDS of the per-plane mean predictor kernel with q output planes per workgroup
+    (kmp_primitives.hip, kmp_mean_predict_maps): which variant a window gets."""
+    S1, S2 = window_shape[2], window_shape[3]
+    c1, c2 = S1 - 2 * padding - 1, S2 - 2 * padding - 1
+    nb = 16 * (-(-(2 * padding + 2 + q) * S1 * S2 * itemsize // 16) + 1)
+    xs = 4 * (2 * padding + 2 + q) * S1 * c2 if padding else 0
+    return nb + xs + 4 * (q + 1) * c1 * c2 + 8 * 4 * ((c2 + 4) // 4)
+
+
 @pytest.mark.parametrize('shape,dtype', [((2, 64, 64, 64, 1), np.uint16), ((3, 17, 9, 22, 1), np.uint8),
-                                         ((1, 5, 41, 7, 1), np.uint16)])
+                                         ((1, 5, 41, 7, 1), np.uint16),
+                                         ((8, 30, 16, 16, 1), np.uint16),   # B % 8 == 0 (XCD order), even plane count
+                                         ((16, 17, 12, 32, 1), np.uint8)])  # B % 8 == 0, odd plane count
 @pytest.mark.parametrize('padding', [0, 1, 2])
 def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
-    """The LDS-staged mean predictor (one output plane per workgroup, or two with KMP_MP_PPB=2 where
-    the LDS fits; 3D, C == 1) on C3 tiles and ragged windows, against the oracle, both forms and the
-    element-gather kernel it replaced (KMP_MP_LDS=1)."""
+    """The LDS-staged mean predictor (3D, C == 1): two output planes per workgroup by default where
+    the LDS fits ('mean_predict_plane2'), else one ('mean_predict_plane', also forced with
+    KMP_MP_PPB=1), on C3 tiles, ragged windows, and batches that take the XCD-contiguous block order
+    with an even and an odd output-plane count (the last group then holds one plane), against the
+    oracle; both forms give the same bits."""
     import os
     hi = _rand(shape, dtype, 11)
     lo = oracle.volume.lowres_from_highres(oracle.volume.pad_highres(hi)[0])
     window = oracle.volume.pad_neighborhood(lo, padding)
     want = oracle.predictors.mean_predictions_fn(padding, 3)(window)
+    two = _mp_lds_bytes(window.shape, window.itemsize, padding, 2) <= 64 * 1024
     runs = {}
-    for env, val, name in ((None, None, 'mean_predict_plane'), ('KMP_MP_PPB', '2', 'mean_predict_plane'),
-                           ('KMP_MP_LDS', '1', 'mean_predict_maps')):
+    for env, val, name in ((None, None, 'mean_predict_plane2' if two else 'mean_predict_plane'),
+                           ('KMP_MP_PPB', '1', 'mean_predict_plane')):
         if env:
             os.environ[env] = val
         try:
@@ -143,10 +158,9 @@ def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
         finally:
             if env:
                 del os.environ[env]
-    for a, b in zip(runs[(None, None)], want):
-        _eq(a, b)
     for key, got in runs.items():
-        assert all(torch.equal(a, b) for a, b in zip(runs[(None, None)], got)), key
+        for a, b in zip(got, want):
+            _eq(a, b)
 
 
 @pytest.mark.parametrize('ndim', [3, 2])

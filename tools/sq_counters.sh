@@ -3,7 +3,7 @@
 # 8 SQ counters each (MI355X_MICROARCH.md § rocprofv3 PMC slots), summarised per kernel and per
 # wave by tools/sq_summary.py:
 #   bash tools/sq_counters.sh OUTDIR "ktime args" ["ENV=.. ENV=.."]
-# e.g. bash tools/sq_counters.sh gpurun_out/sq_l3p "volume 1 3 linear" "KMP_L3P_MFMA=0"
+# e.g. bash tools/sq_counters.sh gpurun_out/sq_l3p "volume 1 3 linear" "KMP_W3_XCD=1"
 set -o pipefail
 export TMPDIR=/tmp
 O=$1; ARGS=$2; ENVS=$3
