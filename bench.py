@@ -116,7 +116,9 @@ def cpu_baseline(spec, host, padding, ntiles_numpy=0, ntiles_torch=0):
     return {'value': round(r_t, 4), 'unit': 'GB/s', 'cores': threads, 'kind': 'port',
             'sample': f'{nt} of {n} {unit}: torch-CPU restatement of the reference path (oracle/torch_cpu.py, '
                       f'materialised features / predictions like the JAX path) on {threads} threads '
-                      f'(torch.get_num_threads(); the host exposes {len(os.sched_getaffinity(0))} cores), '
+                      f'(torch.get_num_threads() = the OMP_NUM_THREADS CPU share this GPU is allotted on the box; '
+                      f'the host exposes {len(os.sched_getaffinity(0))} cores shared by its 8 GPUs, and the '
+                      f'memory-bound op sequence gains 1.4x from 1 to 16 threads), '
                       f'1 warm-up + median of 5 encode+decode rounds, {t_t:.3f} s/round',
             'single_thread_numpy': {'value': round(r_n, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
                                     'sample': f'{nn} of {n} {unit}: numpy op-for-op restatement (oracle/), '

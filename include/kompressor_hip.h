@@ -265,27 +265,46 @@ int kmp_unpack(int32_t dtype, const uint64_t* payload, int64_t n, const uint8_t*
                void* out, kmp_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
-/* Block-adaptive Rice entropy coding of coded maps (kmp_rice.hip; SURVEY.md §8f f-3 -- no      */
-/* reference counterpart, volume/encode_decode.py:56 returns the residuals unreduced; format    */
-/* spec: oracle/rice.py).  n samples of ``dtype`` (8/16/32-bit), zigzag-mapped, blocks of 64:     */
-/* params[b] = Rice k + 1 (0 = all-zero block), bw[b] = the block's 32-bit payload words.         */
-/* ``workspace`` holds kmp_pack_workspace_bytes(n) bytes; the payload word count lands at         */
-/* kmp_pack_total_offset(n) (uint64) like kmp_pack_plan's.                                        */
+/* Block-adaptive Rice entropy coding of coded maps, bundle format v2 (kmp_rice.hip; SURVEY.md  */
+/* §8f f-3 -- no reference counterpart, volume/encode_decode.py:56 returns the residuals         */
+/* unreduced; byte layout spec: oracle/rice.py pack_bundle).  n samples of ``dtype`` (8/16/32-bit), */
+/* zigzag-mapped, blocks of 64: params[b] = Rice k + 1 (0 = all-zero block), bw[b] = the block's  */
+/* 32-bit payload words; tiles of 32 blocks.  All arrays of a bundle share ONE payload region in  */
+/* tile order; each array keeps a u64 table of its tiles' word offsets into it.                  */
 /* ---------------------------------------------------------------------------------------- */
-/* params / bw of x, and the block offsets + total payload words into the workspace */
-int kmp_rice_plan(int32_t dtype, const void* x, int64_t n, uint8_t* params, uint8_t* bw, void* workspace,
-                  kmp_stream_t stream);
-/* the payload (4-byte aligned) of x, after kmp_rice_plan on the same workspace */
-int kmp_rice_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* params, const void* workspace,
-                  uint32_t* payload, kmp_stream_t stream);
-/* count the blocks whose stored side information no encoder produces -- format 0 (planes):   */
-/* side_a = widths; 1 (rice): side_a = params, side_b = bw -- into the uint64 at workspace +    */
-/* kmp_pack_total_offset(n) + 8, beside the payload length of the last scan (one read for both) */
+typedef struct kmp_rice_array {
+  const void* samples; /* encode: the input samples; decode: the output samples (written)      */
+  int64_t n;           /* samples                                                                */
+  int64_t side_off;    /* byte offset in the bundle of params[nb]; bw[nb] at side_off + pad8(nb)  */
+  int64_t toff_off;    /* byte offset of the u64 tile offsets [kmp_rice_tiles(n)] (8-aligned)    */
+  int64_t rec_off;     /* byte offset of the array's {u64 first word, u64 end word} (8-aligned)  */
+} kmp_rice_array;
+/* tiles of 32 blocks of 64 samples: ceil(ceil(n / 64) / 32) */
+int64_t kmp_rice_tiles(int64_t n);
+/* workspace of the single-pass encode: the look-back states of tiles_total tiles + a ticket */
+int64_t kmp_rice_bundle_workspace_bytes(int64_t tiles_total);
+/* one launch for ``count`` (<= 32) arrays of one dtype, whose tiles are global tiles           */
+/* tile_begin .. + their count of the bundle's ``tiles_total``: samples read once, side          */
+/* information / tile offsets / records / payload written into ``bundle`` (payload region at    */
+/* byte payload_off); the tile of global index tiles_total - 1 writes the bundle's payload words */
+/* (u64 at byte 56) and byte size (u64 at byte 64).  Calls for one bundle go in tile order on    */
+/* one stream (replaces round 2's kmp_rice_plan / kmp_rice_pack and their two scan launches).   */
+int kmp_rice_bundle_encode(int32_t dtype, const kmp_rice_array* arrays, int32_t count, int64_t tile_begin,
+                           int64_t tiles_total, uint8_t* bundle, int64_t payload_off, void* workspace,
+                           kmp_stream_t stream);
+/* the inverse into each array's ``samples``: no scan launch (tile offsets from the table); side */
+/* information checked in the same pass -- every read stays inside the tile's / payload's        */
+/* extent, inconsistent tiles decode as zeros and add 1 to *bad (caller-zeroed device uint64)   */
+/* (replaces round 2's kmp_unpack_plan + kmp_unpack_check + kmp_rice_unpack)                    */
+int kmp_rice_bundle_decode(int32_t dtype, const kmp_rice_array* arrays, int32_t count, int64_t tile_begin,
+                           const uint8_t* bundle, int64_t payload_off, uint64_t payload_words,
+                           unsigned long long* bad, kmp_stream_t stream);
+
+/* Bit-plane side-information check (the planes format): count the blocks whose stored widths   */
+/* no encoder produces (> W) -- format 0 -- or, format 1, Rice params / bw -- into the uint64 at  */
+/* workspace + kmp_pack_total_offset(n) + 8, beside the payload length of the last scan          */
 int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const uint8_t* side_b, int64_t n,
                      void* workspace, kmp_stream_t stream);
-/* the samples, after kmp_unpack_plan(bw, n, workspace) (the block offsets from the stored bw) */
-int kmp_rice_unpack(int32_t dtype, const uint32_t* payload, int64_t n, const uint8_t* params, const uint8_t* bw,
-                    const void* workspace, void* out, kmp_stream_t stream);
 
 /* Categorical rank coder utils.py:58-111: ``logits`` float32 [n, L]; x/out of ``dtype`` [n]. */
 int kmp_categorical(int32_t direction, const float* logits, int64_t n, int64_t L, int32_t dtype, const void* x,

@@ -48,6 +48,11 @@ class Predictor(ctypes.Structure):
                 ('weights', ctypes.c_void_p), ('bias', ctypes.c_void_p)]
 
 
+class RiceArray(ctypes.Structure):  # kmp_rice_array (include/kompressor_hip.h)
+    _fields_ = [('samples', ctypes.c_void_p), ('n', ctypes.c_int64), ('side_off', ctypes.c_int64),
+                ('toff_off', ctypes.c_int64), ('rec_off', ctypes.c_int64)]
+
+
 class Region(ctypes.Structure):
     _fields_ = [('begin', ctypes.c_int64 * 3), ('end', ctypes.c_int64 * 3)]
 
@@ -96,10 +101,11 @@ _PROTOS = {
     'kmp_pack_header': (ctypes.c_int, [_vp, ctypes.c_char_p, _i32, _i64, _i64, _vp, _i64, _i64, _vp]),
     'kmp_unpack_plan': (ctypes.c_int, [_vp, _i64, _vp, _vp]),
     'kmp_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
-    'kmp_rice_plan': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
-    'kmp_rice_pack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     'kmp_unpack_check': (ctypes.c_int, [_i32, _i32, _vp, _vp, _i64, _vp, _vp]),
-    'kmp_rice_unpack': (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    'kmp_rice_tiles': (ctypes.c_int64, [_i64]),
+    'kmp_rice_bundle_workspace_bytes': (ctypes.c_int64, [_i64]),
+    'kmp_rice_bundle_encode': (ctypes.c_int, [_i32, _vp, _i32, _i64, _i64, _vp, _i64, _vp, _vp]),
+    'kmp_rice_bundle_decode': (ctypes.c_int, [_i32, _vp, _i32, _i64, _vp, _i64, ctypes.c_uint64, _vp, _vp]),
     'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
                                                    _vp, _vp]),
     'kmp_encode_with_predictions_typed': (ctypes.c_int, [_i32, _i32, _i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp,

@@ -32,7 +32,7 @@ from . import _nd, packing
 from .predictors import LinearPredictor, MeanPredictor
 
 MAGIC = b'KMPF'
-VERSION = 1
+VERSION = 2  # 2: rice payloads are v2 bundles (packing.py)
 _HEAD = struct.Struct('<4sHHQ')
 _NP_NAME = {torch.uint8: 'uint8', torch.uint16: 'uint16', torch.int32: 'int32', torch.uint32: 'uint32',
             torch.float32: 'float32'}

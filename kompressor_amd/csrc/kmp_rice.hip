@@ -105,242 +105,319 @@ __device__ __forceinline__ int select32(uint32_t x, uint32_t t) {
   return pos;
 }
 
-// per block: k* and the payload words (params / bw), from the per-plane popcounts
-template <int W>
-__global__ void __launch_bounds__(256) rice_plan_kernel(const void* __restrict__ x, int64_t n,
-                                                      uint8_t* __restrict__ params, uint8_t* __restrict__ bw,
-                                                      int64_t nb) {
-  constexpr int NP = Sw<W>::NP;
-  const int lane = threadIdx.x & 63;
-  const int64_t nstep = (nb + 7) / 8;
-  for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
-       st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    uint32_t w[Sw<W>::NW];
-    load8s<W>(x, n, st * 512 + (int64_t)lane * 8, w);
-    uint32_t Z[NP][2];
-    zplanes<W>(w, Z);
-    uint32_t cnt[2 * NP];  // byte b of cnt[i]: the block's count of ones in z-plane 4i + b
+// ---- the Rice bundle (format v2): every array of a call in one single-pass encode launch and
+// one decode launch per sample width ----
+//
+// Work unit: a TILE of 32 blocks (2048 samples): one 256-thread workgroup, each wave 8 blocks in
+// the lane layout above.  Tiles of all arrays form one sequence (array after array); a tile's
+// payload words follow its predecessor's, so the bundle holds ONE payload region and per array a
+// table of tile offsets (u64 word offsets) that lets the decoder start every tile independently.
+//
+// Encode (rice_bundle_encode_kernel), reading the samples ONCE: per block k* and its word count
+// from the bit-plane popcounts (the plan above, in registers), the block's exclusive prefix inside
+// the wave (scan over the 8 groups) and the workgroup (LDS), the tile's start by a decoupled
+// look-back over the tiles before it (a tile publishes its aggregate, then its inclusive prefix;
+// tiles are numbered by an atomic ticket in start order, so every tile a tile waits on has
+// started -- no deadlock), then the payload written from the same registers.  Was: plan kernel
+// (reads the map), two scan launches, pack kernel (reads the map again) per array.
+//
+// Decode (rice_bundle_decode_kernel): the tile offset from the table, the blocks' offsets by the
+// same in-workgroup prefix over the stored bw, the unpack below.  Every read is bounded by the tile
+// / payload extents, and the side information is checked in the same pass (k < W, bw within
+// [2k + 2, 2W + 2], a zero block without payload, the tile's words meeting the next tile's offset);
+// a tile that fails decodes as zeros and is counted, so a corrupt bundle raises on the host after
+// the one synchronisation instead of steering a read outside the blob.
+constexpr int kTileBlocks = 32;
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+struct RArr {        // device copy of kmp_rice_array
+  const void* x;     // encode input / decode output
+  int64_t n, nb, ntile, tile0;
+  int64_t side_off, toff_off, rec_off;
+};
+constexpr int kMaxArr = 32;
+struct RArrs {
+  RArr a[kMaxArr];
+  int count;
+};
+
+// the array of global tile g (uniform)
+__device__ __forceinline__ int array_of(const RArrs& A, int64_t g) {
+  int a = 0;
+  while (a + 1 < A.count && g >= A.a[a + 1].tile0) ++a;
+  return a;
+}
+
+// exclusive prefix of v over the 8 block groups of a wave (v is the same on a group's 8 lanes);
+// *tot = the wave's total
+__device__ __forceinline__ uint32_t wave_groups_excl(uint32_t v, int lane, uint32_t* tot) {
+  uint32_t x = (lane & 7) == 0 ? v : 0u;
 #pragma unroll
-    for (int i = 0; i < 2 * NP; ++i) cnt[i] = group8_sum(bytes_popcount(Z[i >> 1][i & 1]), lane);
-    // S_k = sum_i (z_i >> k) = 2 S_{k+1} + count_k; words(k) = 2k + ceil((64 + S_k) / 32).  An S_k
-    // past kSumCap costs more than 2W + 2 words (the k = W - 1 cost bound), so capping it keeps the
-    // argmin exact (ties: the smallest k, as the descending loop keeps the last <=)
-    // (W <= 16: S_0 <= 64 (2^16 - 1) needs no cap.)  The argmin as one min per k over the key
-    // 32 words(k) + k = ((S_k + 95) & ~31) + 65 k: the fewest words, ties to the smallest k
-    uint32_t S = 0, key = 0xffffffffu;
-#pragma unroll
-    for (int k = W - 1; k >= 0; --k) {
-      const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      S = 2u * S + c;
-      if constexpr (W > 16) S = min(S, kSumCap);
-      key = min(key, ((S + 95u) & ~31u) + 65u * (uint32_t)k);
-    }
-    const uint32_t best = key >> 5;
-    const int kbest = (int)(key & 31u);
-    const bool zero = S == 0;  // S_0 == sum of z: an all-zero block
-    const int64_t blk = st * 8 + (lane >> 3);
-    if ((lane & 7) == 0 && blk < nb) {
-      params[blk] = zero ? 0 : (uint8_t)(kbest + 1);
-      bw[blk] = zero ? 0 : (uint8_t)best;
-    }
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += y;
   }
+  *tot = (uint32_t)__shfl((int)x, 63, 64);
+  const uint32_t incl = (uint32_t)__shfl((int)x, lane & ~7, 64);  // inclusive at the group's first lane
+  return incl - v;
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) rice_pack_kernel(const void* __restrict__ x, int64_t n,
-                                                      const uint8_t* __restrict__ params,
-                                                      const uint32_t* __restrict__ local,
-                                                      const uint64_t* __restrict__ cbase, int64_t nb,
-                                                      uint32_t* __restrict__ payload) {
+__global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_t tile_begin, int64_t tiles_total,
+                                                               uint8_t* __restrict__ blob, int64_t payload_off,
+                                                               uint64_t* __restrict__ state,
+                                                               unsigned* __restrict__ ticket) {
   constexpr int NP = Sw<W>::NP;
   constexpr int UMAX = 2 * W + 2;
   __shared__ uint32_t stream_lds[4][8][UMAX];
-  const int lane = threadIdx.x & 63, j = lane & 7, g = lane >> 3;
-  uint32_t* ustream = stream_lds[threadIdx.x >> 6][g];
-  const int64_t nstep = (nb + 7) / 8;
-  for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
-       st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int64_t blk = st * 8 + g;
-    uint32_t w[Sw<W>::NW];
-    load8s<W>(x, n, st * 512 + (int64_t)lane * 8, w);
-    int param = 0;
-    uint64_t off = 0;
-    if (blk < nb) {
-      param = params[blk];
-      off = cbase[blk / kChunk] + local[blk];
-    }
-    const int k = param > 0 ? min(param - 1, W - 1) : 0;
-    // low planes: lane j stores z-planes 8p + j < k
-    uint32_t Z[NP][2];
-    zplanes<W>(w, Z);
+  __shared__ uint32_t wsum[4];
+  __shared__ uint64_t s_excl;
+  __shared__ int64_t s_tile;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, j = lane & 7, g8 = lane >> 3;
+  if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t g = tile_begin + s_tile;
+  const int a = array_of(A, g);
+  const RArr& R = A.a[a];
+  const int64_t t = g - R.tile0;
+  const int64_t blk = t * kTileBlocks + wv * 8 + g8;
+  const bool has = blk < R.nb;
+  uint32_t w[Sw<W>::NW];
+  load8s<W>(R.x, R.n, blk * 64 + j * 8, w);
+  // ---- plan: k* and the word count (as rice_plan in round 2, now in the same pass) ----
+  uint32_t Z[NP][2];
+  zplanes<W>(w, Z);
+  uint32_t cnt[2 * NP];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      xtr8(Z[p][0], Z[p][1], j);
-      const int b = 8 * p + j;
-      if (param > 0 && b < k) {
-        KMP_DCHECK(off + 2 * b + 1 < off + 2 * W + 2, "plane %d past the block", b);
-        payload[off + 2 * b] = Z[p][0];
-        payload[off + 2 * b + 1] = Z[p][1];
+  for (int i = 0; i < 2 * NP; ++i) cnt[i] = group8_sum(bytes_popcount(Z[i >> 1][i & 1]), lane);
+  uint32_t S = 0, key = 0xffffffffu;
+#pragma unroll
+  for (int k = W - 1; k >= 0; --k) {
+    const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    S = 2u * S + c;
+    if constexpr (W > 16) S = min(S, kSumCap);
+    key = min(key, ((S + 95u) & ~31u) + 65u * (uint32_t)k);
+  }
+  const bool zero = S == 0 || !has;
+  const int param = zero ? 0 : (int)(key & 31u) + 1;
+  const uint32_t words = zero ? 0u : key >> 5;
+  uint8_t* params = blob + R.side_off;
+  uint8_t* bw = params + ((R.nb + 7) & ~(int64_t)7);
+  if (j == 0 && has) {
+    params[blk] = (uint8_t)param;
+    bw[blk] = (uint8_t)words;
+  }
+  // ---- offsets: in the wave, in the workgroup, then the tile's start (decoupled look-back) ----
+  uint32_t wtot;
+  const uint32_t bexcl = wave_groups_excl(words, lane, &wtot);
+  if (lane == 0) wsum[wv] = wtot;
+  __syncthreads();
+  const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  uint32_t wbase = 0;
+  for (int q = 0; q < wv; ++q) wbase += wsum[q];
+  if (tid == 0) {
+    uint64_t excl = 0;
+    if (g == 0) {
+      __hip_atomic_store(&state[0], kFlagPre | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&state[g], kFlagAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      for (int64_t i = g - 1; i >= 0;) {
+        const uint64_t v = __hip_atomic_load(&state[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 62) == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += v & kValMask;
+        if ((v >> 62) == 2) break;
+        --i;
       }
+      __hip_atomic_store(&state[g], kFlagPre | (excl + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // unary part: lane's quotients, their total, the prefix over the block's lanes
-    uint32_t q[8], len = 0;
+    s_excl = excl;
+    ((uint64_t*)(blob + R.toff_off))[t] = excl;
+    uint64_t* rec = (uint64_t*)(blob + R.rec_off);
+    if (t == 0) rec[0] = excl;
+    if (t == R.ntile - 1) rec[1] = excl + agg;
+    if (g == tiles_total - 1) {  // the bundle's payload words and byte size (header fields 56, 64)
+      ((uint64_t*)blob)[7] = excl + agg;
+      ((uint64_t*)blob)[8] = (uint64_t)payload_off + (((excl + agg) * 4 + 7) & ~7ull);
+    }
+  }
+  __syncthreads();
+  const uint64_t off = s_excl + wbase + bexcl;
+  uint32_t* payload = (uint32_t*)(blob + payload_off);
+  // ---- payload: the k low planes, then the unary part (as round 2's rice_pack) ----
+  const int k = param > 0 ? param - 1 : 0;
+  uint32_t* ustream = stream_lds[wv][g8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      q[e] = zigzag<W>(sample_of<W>(w, e)) >> k;
-      len += q[e] + 1u;
+  for (int p = 0; p < NP; ++p) {
+    xtr8(Z[p][0], Z[p][1], j);
+    const int b = 8 * p + j;
+    if (param > 0 && b < k) {
+      payload[off + 2 * b] = Z[p][0];
+      payload[off + 2 * b + 1] = Z[p][1];
     }
-    const uint32_t incl = group8_incl(len, j);
-    const uint32_t tot = (uint32_t)__shfl((int)incl, (g << 3) | 7, 64);  // the block's unary bits
-    const uint32_t uw = (tot + 31u) >> 5;
-    // zero the block's uw stream words (all a terminator can land in: pos < tot), OR in one
-    // terminator per sample, copy the words out
-    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    uint32_t pos = incl - len;
+  }
+  uint32_t q[8], len = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      pos += q[e];
-      if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
-      pos += 1u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (param > 0) {
-      const uint64_t ubase = off + 2u * (uint32_t)k;
-      for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) payload[ubase + i] = ustream[i];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();  // the next step's zeroing must not overtake these reads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int e = 0; e < 8; ++e) {
+    q[e] = zigzag<W>(sample_of<W>(w, e)) >> k;
+    len += q[e] + 1u;
+  }
+  const uint32_t incl = group8_incl(len, j);
+  const uint32_t tot = (uint32_t)__shfl((int)incl, (g8 << 3) | 7, 64);
+  const uint32_t uw = (tot + 31u) >> 5;
+  for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint32_t pos = incl - len;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    pos += q[e];
+    if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
+    pos += 1u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (param > 0) {
+    const uint64_t ubase = off + 2u * (uint32_t)k;
+    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) payload[ubase + i] = ustream[i];
   }
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) rice_unpack_kernel(const uint32_t* __restrict__ payload, int64_t n,
-                                                        const uint8_t* __restrict__ params,
-                                                        const uint8_t* __restrict__ bw,
-                                                        const uint32_t* __restrict__ local,
-                                                        const uint64_t* __restrict__ cbase, int64_t nb,
-                                                        void* __restrict__ out) {
+__global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_t tile_begin,
+                                                               const uint8_t* __restrict__ blob,
+                                                               int64_t payload_off, uint64_t payload_words,
+                                                               unsigned long long* __restrict__ bad_out) {
   constexpr int NP = Sw<W>::NP;
-  constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave step's 8 blocks, at most
+  constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave's 8 blocks, at most
   __shared__ uint32_t span_lds[4][SPAN];
-  const int lane = threadIdx.x & 63, j = lane & 7;
-  uint32_t* const wspan = span_lds[(threadIdx.x >> 6) & 3];
-  const int64_t nstep = (nb + 7) / 8;
-  for (int64_t st = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nstep;
-       st += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int64_t blk = st * 8 + (lane >> 3);
-    int param = 0, words = 0;
-    uint64_t off = 0;
-    if (blk < nb) {
-      param = params[blk];
-      words = min((int)bw[blk], 2 * W + 2);  // a corrupt bw never steers a read past the span
-      off = cbase[blk / kChunk] + local[blk];
-    }
-    // the step's 8 blocks are consecutive in the payload: stage their words [start, end) in LDS
-    // with coalesced loads, so the low planes and the unary walk below read LDS, not memory
-    const uint64_t start = __shfl(off, 0, 64);
-    uint64_t end = blk < nb ? off + (uint64_t)words : start;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      const uint64_t o = __shfl_xor(end, d, 64);
-      end = o > end ? o : end;
-    }
-    const int cnt = (int)min<uint64_t>(end - start, (uint64_t)SPAN);
-    for (int i = lane; i < cnt; i += 64) wspan[i] = payload[start + i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const uint32_t* const bp = wspan + (off - start);  // this lane's block in LDS
-    const int k = param > 0 ? min(param - 1, W - 1) : 0;
-    const int uw = param > 0 ? max(words - 2 * k, 0) : 0;  // a corrupt bw never steers a read past the block
-    // low bits: planes 8p + j < k, transposed back to the lane's 8 samples
-    uint32_t Z[NP][2];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int b = 8 * p + j;
-      const bool have = param > 0 && b < k && 2 * b + 1 < words;
-      Z[p][0] = have ? bp[2 * b] : 0u;
-      Z[p][1] = have ? bp[2 * b + 1] : 0u;
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      xtr8(Z[p][0], Z[p][1], j);
-      tr8x8(Z[p][0], Z[p][1]);
-    }
-    uint32_t lowv[Sw<W>::NW];
-    scatter_bytes<W>(Z, lowv);
-    // unary part: start after terminator 8j - 1, then 8 quotients by ctz
-    const uint32_t* us = bp + 2 * k;
-    uint32_t q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = 0u;
-    if (param > 0 && uw > 0) {
-      uint32_t pos = 0;  // stream position where sample 8j's code starts
-      if (j > 0) {
-        const uint32_t r = 8u * j - 1u;  // 0-based rank of the terminator ending sample 8j - 1
-        uint32_t acc = 0, word = 0;
-        int wi = 0;
-        for (; wi < uw; ++wi) {
-          word = us[wi];
-          const uint32_t c = __builtin_popcount(word);
-          if (acc + c > r) break;
-          acc += c;
-        }
-        pos = wi < uw ? 32u * wi + select32(word, r - acc) + 1u : 32u * uw;
-      }
-      int wi = (int)(pos >> 5);
-      // the 64 stream bits from ``pos`` (three words funnel-shifted); when they hold the lane's 8
-      // terminators -- a mean quotient below 7 at the block's k, nearly always -- the quotients are
-      // 8 branch-free ctz steps, otherwise the word-by-word walk below
-      const uint32_t sh = pos & 31u;
-      const uint32_t a = wi < uw ? us[wi] : 0u, b = wi + 1 < uw ? us[wi + 1] : 0u, c = wi + 2 < uw ? us[wi + 2] : 0u;
-      uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
-      if (__builtin_popcountll(win) >= 8) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t t = (uint32_t)__builtin_ctzll(win);
-          q[e] = t;
-          win = (win >> t) >> 1;
-        }
-      } else {
-        // ``cur``: the stream bits from position ``base`` up to the end of word ``wi``
-        uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
-        uint32_t base = pos;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          while (cur == 0u && wi + 1 < uw) {  // only zeros left in this word: continue in the next
-            ++wi;
-            cur = us[wi];
-            base = 32u * wi;
-          }
-          if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
-          const uint32_t t = __builtin_ctz(cur);
-          q[e] = base + t - pos;  // the zeros between the code's start and its terminator
-          pos = base + t + 1u;
-          cur = t == 31u ? 0u : cur >> (t + 1u);
-          base = pos;
-        }
-      }
-    }
-    uint32_t wout[Sw<W>::NW];
-#pragma unroll
-    for (int i = 0; i < Sw<W>::NW; ++i) wout[i] = 0u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t z = param > 0 ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
-      set_sample<W>(wout, e, unzigzag<W>(z));
-    }
-    store8s<W>(out, n, st * 512 + (int64_t)lane * 8, wout);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();  // the next step's staging must not overtake these reads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wbad[4];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, j = lane & 7, g8 = lane >> 3;
+  const int64_t g = tile_begin + blockIdx.x;
+  const int a = array_of(A, g);
+  const RArr& R = A.a[a];
+  const int64_t t = g - R.tile0;
+  const int64_t blk = t * kTileBlocks + wv * 8 + g8;
+  const bool has = blk < R.nb;
+  const uint8_t* params = blob + R.side_off;
+  const uint8_t* bwp = params + ((R.nb + 7) & ~(int64_t)7);
+  int param = has ? params[blk] : 0;
+  int words = has ? bwp[blk] : 0;
+  const int kk = param - 1;
+  bool bad = param == 0 ? words != 0 : (kk >= W || words < 2 * kk + 2 || words > 2 * W + 2);
+  if (bad) words = 0;  // keeps the offsets of the good blocks in bounds
+  uint32_t wtot;
+  const uint32_t bexcl = wave_groups_excl((uint32_t)words, lane, &wtot);
+  const bool wave_bad = __any(bad);
+  if (lane == 0) {
+    wsum[wv] = wtot;
+    wbad[wv] = wave_bad;
   }
+  __syncthreads();
+  const uint64_t* toff = (const uint64_t*)(blob + R.toff_off);
+  const uint64_t* rec = (const uint64_t*)(blob + R.rec_off);
+  const uint64_t start = toff[t];
+  const uint64_t end = t + 1 < R.ntile ? toff[t + 1] : rec[1];
+  const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const bool tile_bad = wbad[0] || wbad[1] || wbad[2] || wbad[3] || start > payload_words || end > payload_words ||
+                        start + agg != end || (t == 0 && start != rec[0]);
+  if (tile_bad) {
+    param = 0;
+    words = 0;
+    if (tid == 0) atomicAdd(bad_out, 1ull);
+  }
+  uint32_t wbase = 0;
+  for (int q = 0; q < wv; ++q) wbase += wsum[q];
+  const uint64_t off = tile_bad ? 0 : start + wbase + bexcl;
+  const uint32_t* payload = (const uint32_t*)(blob + payload_off);
+  // ---- the wave's 8 blocks are consecutive: stage their words in LDS, then unpack ----
+  const uint64_t wstart = tile_bad ? 0 : start + wbase;
+  const int cnt = tile_bad ? 0 : (int)min<uint64_t>((uint64_t)wsum[wv], (uint64_t)SPAN);
+  uint32_t* const wspan = span_lds[wv];
+  for (int i = lane; i < cnt; i += 64) wspan[i] = payload[wstart + i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const uint32_t* const bp = wspan + (off - wstart);
+  const int k = param > 0 ? param - 1 : 0;
+  const int uw = param > 0 ? words - 2 * k : 0;
+  uint32_t Z[NP][2];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int b = 8 * p + j;
+    const bool hv = param > 0 && b < k;
+    Z[p][0] = hv ? bp[2 * b] : 0u;
+    Z[p][1] = hv ? bp[2 * b + 1] : 0u;
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    xtr8(Z[p][0], Z[p][1], j);
+    tr8x8(Z[p][0], Z[p][1]);
+  }
+  uint32_t lowv[Sw<W>::NW];
+  scatter_bytes<W>(Z, lowv);
+  const uint32_t* us = bp + 2 * k;
+  uint32_t q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = 0u;
+  if (param > 0 && uw > 0) {
+    uint32_t pos = 0;
+    if (j > 0) {
+      const uint32_t r = 8u * j - 1u;
+      uint32_t acc = 0, word = 0;
+      int wi = 0;
+      for (; wi < uw; ++wi) {
+        word = us[wi];
+        const uint32_t c = __builtin_popcount(word);
+        if (acc + c > r) break;
+        acc += c;
+      }
+      pos = wi < uw ? 32u * wi + select32(word, r - acc) + 1u : 32u * uw;
+    }
+    int wi = (int)(pos >> 5);
+    const uint32_t sh = pos & 31u;
+    const uint32_t a0 = wi < uw ? us[wi] : 0u, b0 = wi + 1 < uw ? us[wi + 1] : 0u, c0 = wi + 2 < uw ? us[wi + 2] : 0u;
+    uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c0, b0, sh) << 32) | __builtin_amdgcn_alignbit(b0, a0, sh);
+    if (__builtin_popcountll(win) >= 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t tz = (uint32_t)__builtin_ctzll(win);
+        q[e] = tz;
+        win = (win >> tz) >> 1;
+      }
+    } else {
+      uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
+      uint32_t base = pos;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        while (cur == 0u && wi + 1 < uw) {
+          ++wi;
+          cur = us[wi];
+          base = 32u * wi;
+        }
+        if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
+        const uint32_t tz = __builtin_ctz(cur);
+        q[e] = base + tz - pos;
+        pos = base + tz + 1u;
+        cur = tz == 31u ? 0u : cur >> (tz + 1u);
+        base = pos;
+      }
+    }
+  }
+  uint32_t wout[Sw<W>::NW];
+#pragma unroll
+  for (int i = 0; i < Sw<W>::NW; ++i) wout[i] = 0u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t z = param > 0 ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
+    set_sample<W>(wout, e, unzigzag<W>(z));
+  }
+  if (has) store8s<W>((void*)R.x, R.n, blk * 64 + j * 8, wout);
 }
 
 // side information a blob may hold (one workgroup; written next to the scan's total): planes --
@@ -390,37 +467,6 @@ using namespace kmp;
 
 extern "C" {
 
-int kmp_rice_plan(int32_t dtype, const void* x, int64_t n, uint8_t* params, uint8_t* bw, void* workspace,
-                  kmp_stream_t stream) {
-  const int W = pk::sample_bits(dtype);
-  KMP_REQUIRE(W > 0, "rice: unsupported dtype");
-  KMP_REQUIRE(n >= 0 && workspace && (n == 0 || (x && params && bw)), "rice: bad argument");
-  const int64_t nb = kmp_pack_blocks(n);
-  hipStream_t s = (hipStream_t)stream;
-  if (nb > 0) {
-    if (W == 8) rc::rice_plan_kernel<8><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, bw, nb);
-    else if (W == 16) rc::rice_plan_kernel<16><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, bw, nb);
-    else rc::rice_plan_kernel<32><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, bw, nb);
-    if (int st = check_launch("rice_plan")) return st;
-  }
-  return pk::scan(bw, nb, pk::carve(workspace, nb), s);
-}
-
-int kmp_rice_pack(int32_t dtype, const void* x, int64_t n, const uint8_t* params, const void* workspace,
-                  uint32_t* payload, kmp_stream_t stream) {
-  const int W = pk::sample_bits(dtype);
-  KMP_REQUIRE(W > 0, "rice: unsupported dtype");
-  KMP_REQUIRE(n >= 0 && workspace && (n == 0 || (x && params && payload)), "rice: bad argument");
-  const int64_t nb = kmp_pack_blocks(n);
-  if (nb == 0) return KMP_OK;
-  const pk::Ws w = pk::carve((void*)workspace, nb);
-  hipStream_t s = (hipStream_t)stream;
-  if (W == 8) rc::rice_pack_kernel<8><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, w.local, w.cbase, nb, payload);
-  else if (W == 16) rc::rice_pack_kernel<16><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, w.local, w.cbase, nb, payload);
-  else rc::rice_pack_kernel<32><<<pk::waves_grid(nb), 256, 0, s>>>(x, n, params, w.local, w.cbase, nb, payload);
-  return check_launch("rice_pack");
-}
-
 int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const uint8_t* side_b, int64_t n,
                      void* workspace, kmp_stream_t stream) {
   const int W = pk::sample_bits(dtype);
@@ -440,19 +486,74 @@ int kmp_unpack_check(int32_t format, int32_t dtype, const uint8_t* side_a, const
   return check_launch("unpack_check");
 }
 
-int kmp_rice_unpack(int32_t dtype, const uint32_t* payload, int64_t n, const uint8_t* params, const uint8_t* bw,
-                    const void* workspace, void* out, kmp_stream_t stream) {
+int64_t kmp_rice_tiles(int64_t n) { return n > 0 ? ceil_div(kmp_pack_blocks(n), (int64_t)rc::kTileBlocks) : 0; }
+
+static int rice_arrays(const kmp_rice_array* arrays, int32_t count, int64_t tile_begin, rc::RArrs& A,
+                       int64_t& tiles) {
+  KMP_REQUIRE(arrays && count >= 1 && count <= rc::kMaxArr, "rice bundle: 1 .. 32 arrays per call");
+  A.count = count;
+  tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const kmp_rice_array& s = arrays[i];
+    KMP_REQUIRE(s.n >= 0 && (s.n == 0 || s.samples), "rice bundle: bad array");
+    KMP_REQUIRE(s.side_off >= 0 && s.toff_off % 8 == 0 && s.rec_off % 8 == 0, "rice bundle: bad layout");
+    rc::RArr& r = A.a[i];
+    r.x = s.samples;
+    r.n = s.n;
+    r.nb = kmp_pack_blocks(s.n);
+    r.ntile = kmp_rice_tiles(s.n);
+    r.tile0 = tile_begin + tiles;
+    r.side_off = s.side_off;
+    r.toff_off = s.toff_off;
+    r.rec_off = s.rec_off;
+    tiles += r.ntile;
+  }
+  return KMP_OK;
+}
+
+int kmp_rice_bundle_encode(int32_t dtype, const kmp_rice_array* arrays, int32_t count, int64_t tile_begin,
+                           int64_t tiles_total, uint8_t* bundle, int64_t payload_off, void* workspace,
+                           kmp_stream_t stream) {
   const int W = pk::sample_bits(dtype);
-  KMP_REQUIRE(W > 0, "rice: unsupported dtype");
-  KMP_REQUIRE(n >= 0 && workspace && (n == 0 || (payload && params && bw && out)), "rice: bad argument");
-  const int64_t nb = kmp_pack_blocks(n);
-  if (nb == 0) return KMP_OK;
-  const pk::Ws w = pk::carve((void*)workspace, nb);
+  KMP_REQUIRE(W > 0, "rice bundle: unsupported dtype");
+  KMP_REQUIRE(bundle && workspace && payload_off % 8 == 0 && tile_begin >= 0 && tiles_total >= 0,
+              "rice bundle: bad argument");
+  rc::RArrs A{};
+  int64_t tiles = 0;
+  if (int st = rice_arrays(arrays, count, tile_begin, A, tiles)) return st;
+  KMP_REQUIRE(tile_begin + tiles <= tiles_total, "rice bundle: tiles past the total");
+  uint64_t* state = (uint64_t*)workspace;
+  unsigned* ticket = (unsigned*)(state + tiles_total);
   hipStream_t s = (hipStream_t)stream;
-  if (W == 8) rc::rice_unpack_kernel<8><<<pk::waves_grid(nb), 256, 0, s>>>(payload, n, params, bw, w.local, w.cbase, nb, out);
-  else if (W == 16) rc::rice_unpack_kernel<16><<<pk::waves_grid(nb), 256, 0, s>>>(payload, n, params, bw, w.local, w.cbase, nb, out);
-  else rc::rice_unpack_kernel<32><<<pk::waves_grid(nb), 256, 0, s>>>(payload, n, params, bw, w.local, w.cbase, nb, out);
-  return check_launch("rice_unpack");
+  if (tile_begin == 0 && hipMemsetAsync(state, 0, (size_t)tiles_total * 8, s) != hipSuccess)
+    return fail(KMP_ERR_LAUNCH, "rice bundle: memset");
+  if (hipMemsetAsync(ticket, 0, sizeof(unsigned), s) != hipSuccess) return fail(KMP_ERR_LAUNCH, "rice bundle: memset");
+  if (tiles == 0) return KMP_OK;
+  KMP_REQUIRE(tiles < ((int64_t)1 << 31), "rice bundle: too many tiles in one call");
+  if (W == 8) rc::rice_bundle_encode_kernel<8><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  else if (W == 16) rc::rice_bundle_encode_kernel<16><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  else rc::rice_bundle_encode_kernel<32><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  return check_launch("rice_bundle_encode");
+}
+
+int64_t kmp_rice_bundle_workspace_bytes(int64_t tiles_total) { return 8 * tiles_total + 8; }
+
+int kmp_rice_bundle_decode(int32_t dtype, const kmp_rice_array* arrays, int32_t count, int64_t tile_begin,
+                           const uint8_t* bundle, int64_t payload_off, uint64_t payload_words,
+                           unsigned long long* bad, kmp_stream_t stream) {
+  const int W = pk::sample_bits(dtype);
+  KMP_REQUIRE(W > 0, "rice bundle: unsupported dtype");
+  KMP_REQUIRE(bundle && bad && payload_off % 8 == 0 && tile_begin >= 0, "rice bundle: bad argument");
+  rc::RArrs A{};
+  int64_t tiles = 0;
+  if (int st = rice_arrays(arrays, count, tile_begin, A, tiles)) return st;
+  if (tiles == 0) return KMP_OK;
+  KMP_REQUIRE(tiles < ((int64_t)1 << 31), "rice bundle: too many tiles in one call");
+  hipStream_t s = (hipStream_t)stream;
+  if (W == 8) rc::rice_bundle_decode_kernel<8><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, bundle, payload_off, payload_words, bad);
+  else if (W == 16) rc::rice_bundle_decode_kernel<16><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, bundle, payload_off, payload_words, bad);
+  else rc::rice_bundle_decode_kernel<32><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, bundle, payload_off, payload_words, bad);
+  return check_launch("rice_bundle_decode");
 }
 
 }  // extern "C"

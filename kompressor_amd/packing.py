@@ -8,7 +8,9 @@ about as many bits as they need, both lossless for every bit pattern:
 
 * ``'rice'`` (default, ``kmp_rice.hip``, spec ``oracle/rice.py``): block-adaptive Golomb-Rice --
   per 64-sample block the parameter k minimising the block's size; k low bit-planes plus the
-  unary quotients.  Within ~0.6 bit/sample of the empirical entropy of Laplacian residuals.
+  unary quotients.  About 0.5 bit/sample above the order-0 entropy of the residuals: 16 bits of
+  side information per 64-sample block plus the unary part padded to a 32-bit word
+  (tests/test_ratio.py).
 * ``'planes'`` (``kmp_pack.hip``, spec ``oracle/packing.py``): zigzag samples in blocks of 64 as
   ``width`` 64-bit bit-planes, width = the block's largest value's bit length.  Faster to unpack,
   ~0.8 bit/sample larger.
@@ -22,13 +24,21 @@ specifications ("parity unpinned" by the reference).
     lowres, (maps, dims) = unpack_encoded(blob)
 
 Blobs are device uint8 tensors for torch inputs and numpy uint8 arrays for numpy inputs.
-Array layout (little-endian, 8-byte aligned): ``magic u16 version u16 dtype u32 ndim u32 0 i64 n
-i64 nblocks i64 words`` (40 bytes), ``i64 shape[ndim]``, then
-  'KMPA' (planes): ``u8 widths[nblocks]`` padded to 8 bytes, ``u64 payload[words]``;
-  'KMPR' (rice):   ``u8 params[nblocks]`` padded to 8, ``u8 bw[nblocks]`` padded to 8,
-                   ``u32 payload[words]`` padded to 8.
-Bundle: ``'KMPB' u16 version u16 count u32 nsp``, ``i32 dims[nsp]`` padded to 8, ``i64
-lengths[count]``, then the array blobs (each padded to 8 bytes), lowres first.
+
+'rice' blobs are BUNDLES (format v2, spec ``oracle/rice.py`` pack_bundle): one header, the
+arrays' records, their side information and tile-offset tables, then ONE payload region holding
+every array's blocks in order.  ``pack`` of one array is a one-array bundle.  Encoding is one
+single-pass launch per run of same-dtype arrays (kmp_rice_bundle_encode: the samples are read once;
+per-block parameters, a decoupled look-back scan of the tiles' word counts and the payload in the
+same pass) and ONE synchronisation for the bundle's size; decoding is one launch per run
+(kmp_rice_bundle_decode: tile offsets from the table, no scan) and one synchronisation for the
+side-information check.
+
+'planes' blobs keep format v1: array layout (little-endian, 8-byte aligned) ``magic u16 version
+u16 dtype u32 ndim u32 0 i64 n i64 nblocks i64 words`` (40 bytes), ``i64 shape[ndim]``, then
+``u8 widths[nblocks]`` padded to 8 bytes, ``u64 payload[words]``; bundle v1: ``'KMPB' u16 version=1
+u16 count u32 nsp``, ``i32 dims[nsp]`` padded to 8, ``i64 lengths[count]``, then the array blobs
+(each padded to 8 bytes), lowres first.
 """
 
 import struct
@@ -36,12 +46,13 @@ import struct
 import torch
 
 from . import _device as dev
+from . import _lib
 from ._lib import check, lib
 
 ARRAY_MAGIC = b'KMPA'
-RICE_MAGIC = b'KMPR'
 BUNDLE_MAGIC = b'KMPB'
-VERSION = 1
+VERSION = 1         # planes arrays and bundles
+RICE_VERSION = 2    # rice bundles
 METHODS = ('rice', 'planes')
 _HEAD = struct.Struct('<4sHHIIqqq')  # magic, version, dtype, ndim, reserved, n, nblocks, words (40 bytes)
 _HEAD_MAX = _HEAD.size + 8 * 8       # header + the largest shape (ndim <= 8)
@@ -63,24 +74,16 @@ def _pad8(n):
 class _Plan:
     """Phase 1 of packing one array; ``write`` is phase 2 once the payload length is known."""
 
-    def __init__(self, t, method):
-        if method not in METHODS:
-            raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
-        self.t, self.method = t, method
+    def __init__(self, t):
+        self.t = t
         self.code, self.n = dev.dtype_code(t), t.numel()
         self.nb = nb = int(lib.kmp_pack_blocks(self.n))
         self.ws = dev.empty((int(lib.kmp_pack_workspace_bytes(self.n)),), torch.uint8)
         self.hlen = _HEAD.size + 8 * t.dim()
-        if method == 'rice':  # params | bw, each padded to 8 bytes
-            self.side = torch.zeros((2 * _pad8(nb),), dtype=torch.uint8, device='cuda')
-            check(lib.kmp_rice_plan(self.code, t.data_ptr(), self.n, self.side.data_ptr(),
-                                    self.side.data_ptr() + _pad8(nb), self.ws.data_ptr(), dev.stream()), 'rice')
-            self.magic, self.unit = RICE_MAGIC, 4
-        else:  # widths, padded to 8 bytes
-            self.side = torch.zeros((_pad8(nb),), dtype=torch.uint8, device='cuda')
-            check(lib.kmp_pack_plan(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
-                                    dev.stream()), 'pack')
-            self.magic, self.unit = ARRAY_MAGIC, 8
+        self.side = torch.zeros((_pad8(nb),), dtype=torch.uint8, device='cuda')  # widths, padded to 8 bytes
+        check(lib.kmp_pack_plan(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
+                                dev.stream()), 'pack')
+        self.magic, self.unit = ARRAY_MAGIC, 8
         self.poff = self.hlen + self.side.numel()
 
     def words_view(self):
@@ -98,17 +101,13 @@ class _Plan:
         base = dst.data_ptr()
         check(lib.kmp_pack_header(base, head, len(head), used, dst.numel(), None, 0, -1, dev.stream()), 'pack')
         dst[self.hlen:self.poff].copy_(self.side)
-        if self.method == 'rice':
-            check(lib.kmp_rice_pack(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
-                                    base + self.poff, dev.stream()), 'rice')
-        else:
-            check(lib.kmp_pack(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
-                               base + self.poff, dev.stream()), 'pack')
+        check(lib.kmp_pack(self.code, t.data_ptr(), self.n, self.side.data_ptr(), self.ws.data_ptr(),
+                           base + self.poff, dev.stream()), 'pack')
 
 
-def _plan_all(arrays, method):
+def _plan_all(arrays):
     """Phase 1 for every array, then the ONE synchronisation: (plans, payload words)."""
-    plans = [_Plan(dev.to_device(a)[0].contiguous(), method) for a in arrays]
+    plans = [_Plan(dev.to_device(a)[0].contiguous()) for a in arrays]
     words = torch.cat([p.words_view() for p in plans]).tolist() if plans else []
     return plans, words
 
@@ -133,7 +132,7 @@ def _parse_head(hb, avail):
     if len(hb) < _HEAD.size:
         raise ValueError('truncated array blob')
     magic, version, code, ndim, _, n, nb, words = _HEAD.unpack(hb[:_HEAD.size])
-    if magic not in (ARRAY_MAGIC, RICE_MAGIC) or version != VERSION or ndim > 8:
+    if magic != ARRAY_MAGIC or version != VERSION or ndim > 8:
         raise ValueError(f'not a kompressor_amd array blob (magic {magic!r}, version {version})')
     if code not in dev.CODE_TO_TORCH:
         raise ValueError(f'array blob has an unknown dtype code {code}')
@@ -145,15 +144,10 @@ def _parse_head(hb, avail):
     if nb != int(lib.kmp_pack_blocks(n)):
         raise ValueError(f'array blob has {nb} blocks, {n} samples need {int(lib.kmp_pack_blocks(n))}')
     bits = _SAMPLE_BITS[torch.empty(0, dtype=dev.CODE_TO_TORCH[code]).element_size()]
-    per_block = bits if magic == ARRAY_MAGIC else 2 * bits + 2
-    if words < 0 or words > nb * per_block:
-        raise ValueError(f'array blob payload of {words} words exceeds {nb} blocks of {per_block} words')
+    if words < 0 or words > nb * bits:
+        raise ValueError(f'array blob payload of {words} words exceeds {nb} blocks of {bits} words')
     woff = _HEAD.size + 8 * ndim
-    if magic == ARRAY_MAGIC:
-        poff, total = woff + _pad8(nb), woff + _pad8(nb) + 8 * words
-    else:
-        poff = woff + 2 * _pad8(nb)
-        total = poff + 4 * words
+    poff, total = woff + _pad8(nb), woff + _pad8(nb) + 8 * words
     if avail < total:
         raise ValueError(f'truncated array blob ({avail} < {total} bytes)')
     return dict(magic=magic, code=code, shape=shape, n=n, nb=nb, woff=woff, poff=poff, words=words, bits=bits)
@@ -167,19 +161,11 @@ def _prepare(b, h):
         return None
     n, nb, woff = h['n'], h['nb'], h['woff']
     ws = h['ws'] = dev.empty((int(lib.kmp_pack_workspace_bytes(n)),), torch.uint8)
-    if h['magic'] == ARRAY_MAGIC:
-        widths = h['widths'] = b[woff:woff + nb]
-        check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
-        check(lib.kmp_unpack_check(0, h['code'], widths.data_ptr(), None, n, ws.data_ptr(), dev.stream()), 'unpack')
-    else:
-        params = h['params'] = b[woff:woff + nb]
-        bw = h['bw'] = b[woff + _pad8(nb):woff + _pad8(nb) + nb]
-        check(lib.kmp_unpack_plan(bw.data_ptr(), n, ws.data_ptr(), dev.stream()), 'rice unpack')
-        check(lib.kmp_unpack_check(1, h['code'], params.data_ptr(), bw.data_ptr(), n, ws.data_ptr(), dev.stream()),
-              'rice unpack')
+    widths = h['widths'] = b[woff:woff + nb]
+    check(lib.kmp_unpack_plan(widths.data_ptr(), n, ws.data_ptr(), dev.stream()), 'unpack')
+    check(lib.kmp_unpack_check(0, h['code'], widths.data_ptr(), None, n, ws.data_ptr(), dev.stream()), 'unpack')
     # [payload words the stored block sizes add up to, blocks with impossible side information]
-    # (kmp_unpack_check: widths past W; Rice k >= W, a zero block with payload, a coded block
-    # smaller than its planes + 2 unary words or larger than 2W + 2 words)
+    # (kmp_unpack_check: widths past W)
     off = int(lib.kmp_pack_total_offset(n))
     return ws[off:off + 16].view(torch.int64)
 
@@ -188,12 +174,8 @@ def _run_unpack(b, h):
     if h['n'] == 0:
         return h['out']
     n, code, ws, out = h['n'], h['code'], h['ws'], h['out']
-    if h['magic'] == ARRAY_MAGIC:
-        check(lib.kmp_unpack(code, b.data_ptr() + h['poff'], n, h['widths'].data_ptr(), ws.data_ptr(),
-                             out.data_ptr(), dev.stream()), 'unpack')
-    else:
-        check(lib.kmp_rice_unpack(code, b.data_ptr() + h['poff'], n, h['params'].data_ptr(), h['bw'].data_ptr(),
-                                  ws.data_ptr(), out.data_ptr(), dev.stream()), 'rice unpack')
+    check(lib.kmp_unpack(code, b.data_ptr() + h['poff'], n, h['widths'].data_ptr(), ws.data_ptr(),
+                         out.data_ptr(), dev.stream()), 'unpack')
     return out
 
 
@@ -220,13 +202,189 @@ def _unpack_many(b, spans):
 
 
 # ---------------------------------------------------------------------------------------------
+# rice bundles (format v2): layout on the host, one single-pass launch per run of same-dtype
+# arrays, one synchronisation for the size; decode likewise
+# ---------------------------------------------------------------------------------------------
+
+_RHEAD = struct.Struct('<4sHHII8i4Q')       # 80 bytes: magic, version, count, nsp, 0, dims[8], payload_off,
+_RREC = struct.Struct('<II8q5q2Q')          # payload words, bytes, 0 / 128-byte array record
+_TILE_BLOCKS = 32
+_MAX_ARRAYS = 1 << 12
+
+
+def _bundle_layout(ns):
+    """``(header bytes, [(side_off, toff_off)], payload_off)`` of a v2 bundle of arrays of ``ns``
+    samples (oracle/rice.py bundle_layout)."""
+    head = _RHEAD.size + _RREC.size * len(ns)
+    off, sides, tofs = head, [], []
+    for n in ns:
+        sides.append(off)
+        off += 2 * _pad8(int(lib.kmp_pack_blocks(n)))
+    for n in ns:
+        tofs.append(off)
+        off += 8 * int(lib.kmp_rice_tiles(n))
+    return head, list(zip(sides, tofs)), _pad8(off)
+
+
+def _runs(ts):
+    """Maximal runs of same-dtype arrays, at most 32 per launch: [(first index, count)]."""
+    runs, i = [], 0
+    while i < len(ts):
+        k = i + 1
+        while k < len(ts) and k - i < 32 and ts[k].dtype == ts[i].dtype:
+            k += 1
+        runs.append((i, k - i))
+        i = k
+    return runs
+
+
+def _rice_arrays(ts, ptrs, offs, first, count):
+    arr = (_lib.RiceArray * count)()
+    for q in range(count):
+        i = first + q
+        arr[q].samples = ptrs[i]
+        arr[q].n = ts[i].numel()
+        arr[q].side_off, arr[q].toff_off = offs[i]
+        arr[q].rec_off = _RHEAD.size + _RREC.size * i + 112
+    return arr
+
+
+def _rice_pack_bundle(arrays, dims):
+    out, poff, launched, keep = _rice_encode_launch(arrays, dims)
+    if launched:
+        words, total = out[56:72].view(torch.int64).tolist()  # the one synchronisation
+        if poff + 4 * words < total:
+            out[poff + 4 * words:total].zero_()
+    else:
+        total = poff
+    del keep  # the header copy is complete (synchronised above, or nothing launched after it)
+    return out[:total]
+
+
+def _rice_encode_launch(arrays, dims):
+    """Everything of a rice pack up to the synchronisation: ``(worst-case sized output, payload
+    offset, whether a kernel ran, host objects the queued copy still reads)``."""
+    ts = [dev.to_device(a)[0].contiguous() for a in arrays]
+    if not ts or len(ts) > _MAX_ARRAYS or len(dims) > 8:
+        raise ValueError(f'a bundle holds 1 .. {_MAX_ARRAYS} arrays and <= 8 dims')
+    for t in ts:
+        dev.dtype_code(t)
+        if t.dim() > 8:
+            raise ValueError('arrays of at most 8 dimensions')
+    ns = [t.numel() for t in ts]
+    head, offs, poff = _bundle_layout(ns)
+    tiles = [int(lib.kmp_rice_tiles(n)) for n in ns]
+    T = sum(tiles)
+    worst = sum(int(lib.kmp_pack_blocks(n)) * (2 * 8 * t.element_size() + 2) * 4 for n, t in zip(ns, ts))
+    out = dev.empty((poff + worst + 8,), torch.uint8)
+    out[:poff].zero_()
+    hdr = bytearray(_RHEAD.pack(BUNDLE_MAGIC, RICE_VERSION, len(ts), len(dims), 0,
+                                *(list(int(d) for d in dims) + [0] * (8 - len(dims))), poff, 0, poff, 0))
+    for t, (side, toff), nt in zip(ts, offs, tiles):
+        hdr += _RREC.pack(dev.dtype_code(t), t.dim(), *(list(t.shape) + [0] * (8 - t.dim())), t.numel(),
+                          int(lib.kmp_pack_blocks(t.numel())), nt, side, toff, 0, 0)
+    pinned = torch.frombuffer(hdr, dtype=torch.uint8).pin_memory()
+    out[:head].copy_(pinned, non_blocking=True)
+    if T:
+        ws = dev.empty((int(lib.kmp_rice_bundle_workspace_bytes(T)),), torch.uint8)
+        ptrs = [t.data_ptr() for t in ts]
+        tile_begin = 0
+        for first, count in _runs(ts):
+            arr = _rice_arrays(ts, ptrs, offs, first, count)
+            check(lib.kmp_rice_bundle_encode(dev.dtype_code(ts[first]), arr, count, tile_begin, T, out.data_ptr(),
+                                             poff, ws.data_ptr(), dev.stream()), 'rice bundle')
+            tile_begin += sum(tiles[first:first + count])
+    return out, poff, T > 0, (pinned, ts)
+
+
+def _rice_unpack_bundle(b, hb):
+    """``(arrays, dims)`` of the v2 bundle ``b`` (device uint8) whose first bytes are ``hb``."""
+    outs, dims, bad = _rice_decode_launch(b, hb)
+    if bad is not None:
+        nbad = int(bad.item())  # the one synchronisation
+        if nbad:
+            raise ValueError(f'rice bundle side information is inconsistent in {nbad} tiles (corrupt bundle)')
+    return outs, dims
+
+
+def _rice_decode_launch(b, hb):
+    """Header checks and the decode launches, no synchronisation: ``(arrays, dims, bad-tile
+    counter or None)``."""
+    if len(hb) < _RHEAD.size:
+        raise ValueError('truncated bundle')
+    f = _RHEAD.unpack(hb[:_RHEAD.size])
+    _, _, count, nsp, flags = f[:5]
+    dims = f[5:13]
+    poff, words, total, _ = f[13:17]
+    if count < 1 or count > _MAX_ARRAYS or nsp > 8 or flags:
+        raise ValueError(f'bad rice bundle header (count {count}, nsp {nsp})')
+    head = _RHEAD.size + _RREC.size * count
+    if len(hb) < head:
+        hb = b[:head].cpu().numpy().tobytes()
+        if len(hb) < head:
+            raise ValueError('truncated bundle')
+    recs = [_RREC.unpack(hb[_RHEAD.size + _RREC.size * i:_RHEAD.size + _RREC.size * (i + 1)]) for i in range(count)]
+    shapes, codes, ns = [], [], []
+    for r in recs:
+        code, ndim = r[0], r[1]
+        if code not in dev.CODE_TO_TORCH or ndim > 8:
+            raise ValueError(f'bad array record (dtype code {code}, ndim {ndim})')
+        shape = tuple(r[2:2 + ndim])
+        n, nb, nt = r[10], r[11], r[12]
+        if any(x < 0 for x in shape) or n != dev.prod(shape) or nb != int(lib.kmp_pack_blocks(n)) or \
+                nt != int(lib.kmp_rice_tiles(n)):
+            raise ValueError(f'array record sample / block / tile counts do not match its shape {shape}')
+        shapes.append(shape)
+        codes.append(code)
+        ns.append(n)
+    ehead, offs, epoff = _bundle_layout(ns)
+    if poff != epoff or [(r[13], r[14]) for r in recs] != offs:
+        raise ValueError('bundle layout does not match its records')
+    if total != poff + _pad8(4 * words) or total > b.numel():
+        raise ValueError(f'truncated bundle ({b.numel()} < {total} bytes)')
+    prev_end = 0
+    for r, n, code in zip(recs, ns, codes):
+        first, end = r[15], r[16]
+        bits = 8 * torch.empty(0, dtype=dev.CODE_TO_TORCH[code]).element_size()
+        if n and (first != prev_end or end < first or end > words or end - first > r[11] * (2 * bits + 2)):
+            raise ValueError('array payload ranges are inconsistent')
+        if n:
+            prev_end = end
+    if prev_end != words:
+        raise ValueError('bundle payload words do not match its arrays')
+    outs = [dev.empty(shape, dev.CODE_TO_TORCH[code]) for shape, code in zip(shapes, codes)]
+    tiles = [int(lib.kmp_rice_tiles(n)) for n in ns]
+    if sum(tiles):
+        bad = torch.zeros((1,), dtype=torch.int64, device='cuda')
+        ptrs = [o.data_ptr() for o in outs]
+        tile_begin = 0
+        for first, count in _runs(outs):
+            arr = _rice_arrays(outs, ptrs, offs, first, count)
+            check(lib.kmp_rice_bundle_decode(codes[first], arr, count, tile_begin, b.data_ptr(), poff, words,
+                                             bad.data_ptr(), dev.stream()), 'rice bundle')
+            tile_begin += sum(tiles[first:first + count])
+    else:
+        bad = None
+    return outs, tuple(int(d) for d in dims[:nsp]), bad
+
+
+# ---------------------------------------------------------------------------------------------
 # public API
 # ---------------------------------------------------------------------------------------------
 
+def _check_method(method):
+    if method not in METHODS:
+        raise ValueError(f'unknown packing method {method!r} (expected one of {METHODS})')
+
+
 def pack(x, method='rice'):
-    """Pack one array (uint8 / uint16 / int32 / uint32 / float32 samples) into a blob."""
+    """Pack one array (uint8 / uint16 / int32 / uint32 / float32 samples) into a blob ('rice': a
+    one-array bundle)."""
+    _check_method(method)
     t, kind = dev.to_device(x)
-    (plan,), (words,) = _plan_all([t], method)
+    if method == 'rice':
+        return dev.from_device(_rice_pack_bundle([t], ()), kind)
+    (plan,), (words,) = _plan_all([t])
     out = dev.empty((plan.size(words),), torch.uint8)
     plan.write(out, words)
     return dev.from_device(out, kind)
@@ -235,16 +393,26 @@ def pack(x, method='rice'):
 def unpack(blob):
     """Inverse of :func:`pack`: the array, bit for bit."""
     b, kind = dev.to_device(blob)
+    hb = b[:min(b.numel(), 4096)].cpu().numpy().tobytes()
+    if hb[:4] == BUNDLE_MAGIC:
+        arrays, _ = _rice_unpack_bundle(b, hb)
+        if len(arrays) != 1:
+            raise ValueError(f'a bundle of {len(arrays)} arrays: use unpack_encoded')
+        return dev.from_device(arrays[0], kind)
     return dev.from_device(_unpack_many(b, [(0, b.numel())])[0], kind)
 
 
 def pack_encoded(lowres, encoded, method='rice'):
     """One blob for an ``encode`` result ``(lowres, (maps, dims))`` (any number of maps; ``dims``
-    may be empty): every array's plan kernels, ONE synchronisation, then every array written in
-    place."""
+    may be empty).  'rice': one v2 bundle -- a single-pass launch per run of same-dtype arrays and
+    ONE synchronisation; 'planes': every array's plan kernels, ONE synchronisation, then every
+    array written in place (v1)."""
+    _check_method(method)
     maps, dims = encoded
     kind = 'torch' if isinstance(lowres, torch.Tensor) else 'numpy'
-    plans, words = _plan_all((lowres, *maps), method)
+    if method == 'rice':
+        return dev.from_device(_rice_pack_bundle((lowres, *maps), dims), kind)
+    plans, words = _plan_all((lowres, *maps))
     sizes = [p.size(w) for p, w in zip(plans, words)]
     nsp = len(dims)
     head = struct.pack('<4sHHI', BUNDLE_MAGIC, VERSION, len(plans), nsp)
@@ -267,6 +435,10 @@ def unpack_encoded(blob):
     if len(hb) < 12:
         raise ValueError('truncated bundle')
     magic, version, count, nsp = struct.unpack('<4sHHI', hb[:12])
+    if magic == BUNDLE_MAGIC and version == RICE_VERSION:
+        arrays, dims = _rice_unpack_bundle(b, hb)
+        arrays = [dev.from_device(a, kind) for a in arrays]
+        return arrays[0], (tuple(arrays[1:]), dims)
     if magic != BUNDLE_MAGIC or version != VERSION or nsp > 8:
         raise ValueError(f'not a kompressor_amd bundle (magic {magic!r}, version {version})')
     off = _pad8(12 + 4 * nsp)

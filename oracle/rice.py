@@ -97,3 +97,104 @@ def unpack(params, bw, payload, n, dtype):
         q = np.diff(np.concatenate([[-1], pos])) - 1
         z[blk] = (q.astype(np.uint64) << np.uint64(k)) | low
     return unzigzag(z.reshape(-1)[:n], W).view(np.dtype(dtype))
+
+
+# ---------------------------------------------------------------------------------------------
+# Bundle format v2 (kompressor_amd.packing, kmp_rice.hip rice_bundle_*): the byte layout of a
+# Rice bundle of several arrays, restated here as the specification the GPU bundle is compared
+# against byte for byte (tests/test_packing.py).  Little-endian throughout.
+#
+#   0   'KMPB'  u16 version = 2  u16 count  u32 nsp  u32 0
+#   16  i32 dims[8] (nsp used, the rest 0)
+#   48  u64 payload_off  u64 payload_words  u64 bundle_bytes  u64 0
+#   80  count records of 128 bytes: u32 dtype code, u32 ndim, i64 shape[8] (zero-padded),
+#       i64 n, i64 nb, i64 ntile, i64 side_off, i64 toff_off, u64 first word, u64 end word
+#   then for each array params[nb] and bw[nb], each zero-padded to 8 bytes (at side_off);
+#   then for each array its tile offsets: u64 word offset of every tile of 32 blocks (at toff_off);
+#   then, 8-aligned at payload_off, the payload: every array's blocks in order (array after
+#   array), the Rice block payload of ``pack`` above; bundle_bytes = payload_off + the payload
+#   zero-padded to 8 bytes.  An empty array (n = 0) has first = end = 0.
+# ---------------------------------------------------------------------------------------------
+
+TILE_BLOCKS = 32
+DTYPE_CODE = {np.dtype(np.uint8): 0, np.dtype(np.uint16): 1, np.dtype(np.int32): 2, np.dtype(np.float32): 3,
+              np.dtype(np.uint32): 4}
+CODE_DTYPE = {v: k for k, v in DTYPE_CODE.items()}
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def bundle_layout(ns):
+    """``(header bytes, [(side_off, toff_off)], payload_off)`` for arrays of ``ns`` samples."""
+    head = 80 + 128 * len(ns)
+    off, sides, tofs = head, [], []
+    for n in ns:
+        nb = -(-n // BLOCK)
+        sides.append(off)
+        off += 2 * _pad8(nb)
+    for n in ns:
+        nb = -(-n // BLOCK)
+        tofs.append(off)
+        off += 8 * (-(-nb // TILE_BLOCKS))
+    return head, list(zip(sides, tofs)), _pad8(off)
+
+
+def pack_bundle(arrays, dims=()):
+    """The v2 bundle bytes (numpy uint8) of ``arrays`` (numpy, any shape) and the even-size dims."""
+    import struct
+    arrays = [np.ascontiguousarray(a) for a in arrays]
+    ns = [a.size for a in arrays]
+    head, offs, poff = bundle_layout(ns)
+    words, recs, parts = 0, [], []
+    for a in arrays:
+        params, bw, payload = pack(a.reshape(-1))
+        nb = len(params)
+        boff = np.zeros(nb + 1, np.int64)
+        np.cumsum(bw.astype(np.int64), out=boff[1:])
+        tiles = (words + boff[:-1][::TILE_BLOCKS]).astype(np.uint64) if nb else np.zeros(0, np.uint64)
+        first, end = (words, words + int(boff[-1])) if nb else (0, 0)
+        recs.append((params, bw, tiles, first, end))
+        parts.append(payload)
+        words += int(boff[-1]) if nb else 0
+    total = poff + _pad8(4 * words)
+    out = np.zeros(total, np.uint8)
+    hdr = struct.pack('<4sHHII', b'KMPB', 2, len(arrays), len(dims), 0)
+    hdr += struct.pack('<8i', *(list(int(d) for d in dims) + [0] * (8 - len(dims))))
+    hdr += struct.pack('<4Q', poff, words, total, 0)
+    for a, (side, toff), (params, bw, tiles, first, end) in zip(arrays, offs, recs):
+        nb = len(params)
+        shape = list(a.shape) + [0] * (8 - a.ndim)
+        hdr += struct.pack('<II8q', DTYPE_CODE[a.dtype], a.ndim, *shape)
+        hdr += struct.pack('<5q2Q', a.size, nb, len(tiles), side, toff, first, end)
+        out[side:side + nb] = params
+        out[side + _pad8(nb):side + _pad8(nb) + nb] = bw
+        out[toff:toff + 8 * len(tiles)] = tiles.view(np.uint8)
+    out[:head] = np.frombuffer(hdr, np.uint8)
+    if words:
+        out[poff:poff + 4 * words] = np.concatenate(parts).astype(np.uint32).view(np.uint8)
+    return out
+
+
+def unpack_bundle(blob):
+    """``(arrays, dims)`` of a v2 bundle (numpy)."""
+    import struct
+    b = np.asarray(blob, np.uint8).tobytes()
+    magic, version, count, nsp, _ = struct.unpack('<4sHHII', b[:16])
+    assert magic == b'KMPB' and version == 2
+    dims = struct.unpack('<8i', b[16:48])[:nsp]
+    poff, words, _, _ = struct.unpack('<4Q', b[48:80])
+    payload = np.frombuffer(b, np.uint32, count=words, offset=poff)
+    arrays = []
+    for i in range(count):
+        r = b[80 + 128 * i:80 + 128 * (i + 1)]
+        code, ndim = struct.unpack('<II', r[:8])
+        shape = struct.unpack('<8q', r[8:72])[:ndim]
+        n, nb, ntile, side, toff, first, end = struct.unpack('<5q2Q', r[72:128])
+        params = np.frombuffer(b, np.uint8, count=nb, offset=side)
+        bw = np.frombuffer(b, np.uint8, count=nb, offset=side + _pad8(nb))
+        dt = CODE_DTYPE[code]
+        x = unpack(params, bw, payload[first:end], n, np.dtype(dt.str.replace('f', 'u')) if dt.kind == 'f' else dt)
+        arrays.append(x.view(dt).reshape(shape))
+    return arrays, tuple(dims)

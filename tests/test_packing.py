@@ -106,21 +106,16 @@ def test_rice_matches_spec(kom, dtype, shape, spread):
         flat[: flat.size * 3 // 4] = _residuals(flat.size * 3 // 4, dtype, rng, spread=spread)
         flat[: min(flat.size, 200)] = 0  # all-zero blocks too
         bits = x
-    blob = kom.packing.pack(x)  # the default method is 'rice'
-    assert isinstance(blob, np.ndarray) and blob.dtype == np.uint8 and bytes(blob[:4]) == b'KMPR'
-    params, bw, payload = ORC.pack(bits)
-    head = 40 + 8 * x.ndim
-    nb = len(params)
-    p8 = (nb + 7) // 8 * 8
-    assert np.array_equal(blob[head:head + nb], params)
-    assert np.array_equal(blob[head + p8:head + p8 + nb], bw)
-    poff = head + 2 * p8
-    got = blob[poff:poff + 4 * payload.size].view(np.uint32)
-    assert np.array_equal(got, payload)
-    assert blob.size == poff + (4 * payload.size + 7) // 8 * 8
+    blob = kom.packing.pack(x)  # the default method is 'rice': a one-array v2 bundle
+    assert isinstance(blob, np.ndarray) and blob.dtype == np.uint8 and bytes(blob[:4]) == b'KMPB'
+    want = ORC.pack_bundle([x])
+    assert blob.size == want.size
+    bad = np.flatnonzero(blob != want)
+    assert bad.size == 0, f'{bad.size} bytes differ from the spec, first at {bad[:5].tolist()}'
     back = kom.packing.unpack(blob)
     assert back.dtype == x.dtype and back.shape == x.shape
     assert np.array_equal(back.view(np.uint8), x.view(np.uint8))
+    assert np.array_equal(ORC.unpack_bundle(blob)[0][0].view(np.uint8), x.view(np.uint8))
 
 
 @pytest.mark.gpu
@@ -145,15 +140,55 @@ def test_rice_long_unary_runs(kom, dtype):
     x = (np.concatenate(blocks) * np.where(rng.random(64 * len(blocks)) < 0.5, 1, -1)).astype(np.int64)
     x = (x % (1 << W)).astype(dtype)  # signed residuals in the coder's modular form
     blob = kom.packing.pack(x)
-    params, bw, payload = ORC.pack(x)
-    head = 40 + 8 * x.ndim
-    nb = len(params)
-    p8 = (nb + 7) // 8 * 8
-    assert np.array_equal(blob[head:head + nb], params)
-    assert np.array_equal(blob[head + p8:head + p8 + nb], bw)
-    got = blob[head + 2 * p8:head + 2 * p8 + 4 * payload.size].view(np.uint32)
-    assert np.array_equal(got, payload)
+    assert np.array_equal(blob, ORC.pack_bundle([x]))
     assert np.array_equal(kom.packing.unpack(blob), x)
+
+
+@pytest.mark.gpu
+def test_rice_bundle_matches_spec(kom):
+    """A bundle of many arrays in one call: mixed sample widths (one launch per run of a dtype),
+    an empty array, more than 32 arrays of one dtype (two launches continuing one tile chain), and
+    arrays whose tiles end ragged -- byte-exact to oracle/rice.py pack_bundle, lossless both ways."""
+    rng = np.random.default_rng(21)
+    arrays = [_residuals(70000, np.uint16, rng, spread=30).reshape(70, 1000),
+              _residuals(3000, np.int32, rng, spread=500),
+              _residuals(5, np.int32, rng),
+              np.zeros((0, 4), np.uint16),
+              rng.standard_normal((9, 9)).astype(np.float32)]
+    arrays += [_residuals(int(rng.integers(1, 9000)), np.uint8, rng, spread=6) for _ in range(40)]
+    arrays.append(_residuals(2048 * 3, np.uint16, rng, spread=2))  # exactly 3 tiles
+    dims = (1, 0, 1)
+    lo, maps = arrays[0], tuple(arrays[1:])
+    blob = kom.packing.pack_encoded(lo, (maps, dims))
+    want = ORC.pack_bundle(arrays, dims)
+    assert blob.size == want.size
+    bad = np.flatnonzero(blob != want)
+    assert bad.size == 0, f'{bad.size} bytes differ from the spec, first at {bad[:5].tolist()}'
+    lo2, (maps2, dims2) = kom.packing.unpack_encoded(blob)
+    assert tuple(dims2) == dims
+    for a, b in zip(arrays, (lo2, *maps2)):
+        assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_rice_bundle_rejects_corruption(kom):
+    """Flipped side information, tile offsets, records or a truncated bundle raise ValueError (the
+    decode kernel bounds every read by the tile / payload extents and counts inconsistent tiles)."""
+    rng = np.random.default_rng(3)
+    arrays = [_residuals(50000, np.uint16, rng, spread=40), _residuals(9000, np.uint16, rng, spread=3)]
+    blob = kom.packing.pack_encoded(arrays[0], ((arrays[1],), (1, 1)))
+    side0 = int(blob[80 + 96:80 + 104].view(np.int64)[0])
+    toff0 = int(blob[80 + 104:80 + 112].view(np.int64)[0])
+    for where, val in ((side0 + 5, 30), (side0 + 5, 0), (side0 + (-(-50000 // 64) + 7) // 8 * 8 + 9, 200),
+                       (toff0 + 8, 0x7f), (toff0 + 9, 0x10), (80 + 72, 1), (80 + 112, 3), (56, 0)):
+        bad = blob.copy()
+        bad[where] = val if bad[where] != val else val ^ 1
+        with pytest.raises(ValueError):
+            kom.packing.unpack_encoded(bad)
+    with pytest.raises(ValueError):
+        kom.packing.unpack_encoded(blob[:-16])
+    a, (m, _) = kom.packing.unpack_encoded(blob)  # the intact bundle still decodes
+    assert np.array_equal(a, arrays[0]) and np.array_equal(m[0], arrays[1])
 
 
 @pytest.mark.gpu
@@ -226,7 +261,10 @@ def test_pack_encoded_round_trip_and_ratio(kom):
 def test_pack_empty(kom, shape, method):
     x = np.zeros(shape, np.uint16)
     blob = kom.packing.pack(x, method)
-    assert blob.size == 40 + 8 * x.ndim  # header + shape, no widths, no payload
+    # header (+ shape), no side information, no payload
+    assert blob.size == (80 + 128 if method == 'rice' else 40 + 8 * x.ndim)
+    if method == 'rice':
+        assert np.array_equal(blob, ORC.pack_bundle([x]))
     back = kom.packing.unpack(blob)
     assert back.shape == x.shape and back.dtype == x.dtype
 
@@ -261,20 +299,47 @@ def test_unpack_rejects_inconsistent_headers(kom, method):
     width past the sample size, a payload word count that the widths do not add up to."""
     x = (np.arange(1000) % 7).astype(np.uint16)
     blob = kom.packing.pack(x, method)
-    head = 40 + 8 * x.ndim
-    cases = [
-        _poke(blob, 16, '<q', 1 << 20),   # n past prod(shape): the kernel would write past `out`
-        _poke(blob, 40, '<q', 1 << 20),   # shape past n
-        _poke(blob, 24, '<q', 3),         # nblocks too small for n
-        _poke(blob, 6, '<H', 99),         # unknown dtype code (ValueError, not KeyError)
-        _poke(blob, 32, '<q', 1),         # words smaller than the widths add up to
-        _poke(blob, head, '<B', 200),     # a block width / Rice k past 16 bits
-        _poke(blob, head, '<B', 16),      # planes: a legal width whose sum no longer matches words;
-    ]                                     # rice: k = 15 with too few payload words for its planes
-    if method == 'rice':
-        cases.append(_poke(blob, head + 16, '<B', 0))     # a coded block claiming no payload
-        cases.append(_poke(blob, head + 16, '<B', 90))    # more words than a 16-bit block can take
+    if method == 'planes':
+        head = 40 + 8 * x.ndim
+        cases = [
+            _poke(blob, 16, '<q', 1 << 20),   # n past prod(shape): the kernel would write past `out`
+            _poke(blob, 40, '<q', 1 << 20),   # shape past n
+            _poke(blob, 24, '<q', 3),         # nblocks too small for n
+            _poke(blob, 6, '<H', 99),         # unknown dtype code (ValueError, not KeyError)
+            _poke(blob, 32, '<q', 1),         # words smaller than the widths add up to
+            _poke(blob, head, '<B', 200),     # a block width past 16 bits
+            _poke(blob, head, '<B', 16),      # a legal width whose sum no longer matches words
+        ]
+    else:  # v2 bundle: header 80 bytes, the array record at 80, params at 208, bw at 224
+        cases = [
+            _poke(blob, 152, '<q', 1 << 20),  # n past prod(shape)
+            _poke(blob, 88, '<q', 1 << 20),   # shape past n
+            _poke(blob, 160, '<q', 3),        # nblocks too small for n
+            _poke(blob, 168, '<q', 9),        # a tile count that does not match n
+            _poke(blob, 80, '<I', 99),        # unknown dtype code
+            _poke(blob, 176, '<q', 4096),     # side information moved off the layout
+            _poke(blob, 56, '<Q', 1),         # payload words that do not match the bundle size
+            _poke(blob, 200, '<Q', 3),        # the array's payload end before its start's blocks
+            _poke(blob, 208, '<B', 200),      # a Rice k past 16 bits
+            _poke(blob, 208, '<B', 16),       # k = 15 with too few payload words for its planes
+            _poke(blob, 224, '<B', 0),        # a coded block claiming no payload
+            _poke(blob, 224, '<B', 90),       # more words than a 16-bit block can take
+        ]
     for bad in cases:
         with pytest.raises(ValueError):
             kom.packing.unpack(bad)
     assert np.array_equal(kom.packing.unpack(blob), x)
+
+
+def test_rice_bundle_spec_round_trip():
+    """oracle/rice.py's v2 bundle: mixed widths, an empty array, float32 bit patterns, dims."""
+    rng = np.random.default_rng(9)
+    arrays = [_residuals(3000, np.uint16, rng, spread=20).reshape(3, 1000), _residuals(70, np.int32, rng),
+              np.zeros(0, np.uint8), rng.standard_normal((2, 33)).astype(np.float32),
+              _residuals(2048 * 2, np.uint8, rng)]
+    blob = ORC.pack_bundle(arrays, (1, 0))
+    assert bytes(blob[:4]) == b'KMPB' and blob.size % 8 == 0
+    back, dims = ORC.unpack_bundle(blob)
+    assert dims == (1, 0)
+    for a, b in zip(arrays, back):
+        assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))

@@ -255,11 +255,16 @@ def main():
              gpu_time(unpack_dev, args.reps))
         del tiles, lo, maps
 
-    # Rice entropy coder (kmp_rice.hip) vs the bit-plane format on structured C3-shaped volumes:
-    # a smooth 512^3 field + Gaussian noise of std 1 / 4 / 16, tiled 64^3, MeanPredictor(0) maps
+    # Rice entropy coder (kmp_rice.hip, bundle v2) vs the bit-plane format on structured C3-shaped
+    # volumes: a smooth 512^3 field + Gaussian noise of std 1 / 4 / 16, tiled 64^3, MeanPredictor(0)
+    # maps.  Ratio bar (tests/test_ratio.py): the order-0 entropy of the residual maps, and zlib-6 /
+    # lzma-6 against Rice on the same bytes of a 16-tile sample; the container's file ratio with one
+    # pyramid level and with levels='auto'
     if not want or 'rice' in want:
-        from kompressor_amd import _device as kdev
-        from kompressor_amd._lib import lib as klib
+        import lzma
+        import tempfile
+        import zlib
+        from kompressor_amd import packing as kpk
         zz, yy, xx = torch.meshgrid(*[torch.arange(512, device='cuda', dtype=torch.float32)] * 3, indexing='ij')
         field = (torch.sin(xx / 41.0) * torch.cos(yy / 29.0) + torch.sin(zz / 53.0 + xx / 97.0)
                  + 1.5 * torch.exp(-((xx - 200) ** 2 + (yy - 300) ** 2 + (zz - 250) ** 2) / (2 * 90.0 ** 2)))
@@ -269,9 +274,9 @@ def main():
         gen = torch.Generator(device='cuda').manual_seed(0)
         for noise in (1.0, 4.0, 16.0):
             nvol = (field + noise * torch.randn(field.shape, device='cuda', generator=gen)).round().clamp(0, 65535)
-            tiles = nvol.to(torch.int32).to(torch.uint16).view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5) \
-                .reshape(512, 64, 64, 64, 1).contiguous()
+            vol512 = nvol.to(torch.int32).to(torch.uint16)
             del nvol
+            tiles = vol512.view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5).reshape(512, 64, 64, 64, 1).contiguous()
             lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, tiles)
             raw = tiles.numel() * 2
             b_r = kom.packing.pack_encoded(lo, (maps, dims), 'rice')
@@ -280,46 +285,50 @@ def main():
             assert torch.equal(lo2, lo) and all(torch.equal(a, b) for a, b in zip(maps2, maps))
             t_enc = gpu_time(lambda: kom.packing.pack_encoded(lo, (maps, dims), 'rice'), args.reps)
             t_dec = gpu_time(lambda: kom.packing.unpack_encoded(b_r), args.reps)
-            m = maps[3]
-            n, code = m.numel(), kdev.dtype_code(m)
-            nb = int(klib.kmp_pack_blocks(n))
-            ws = torch.empty(int(klib.kmp_pack_workspace_bytes(n)), dtype=torch.uint8, device='cuda')
-            prm = torch.empty(nb, dtype=torch.uint8, device='cuda')
-            bwv = torch.empty(nb, dtype=torch.uint8, device='cuda')
-            pay = torch.empty(nb * 34 * 4, dtype=torch.uint8, device='cuda')
-            out = torch.empty_like(m)
-
-            def rice_pack_dev():
-                klib.kmp_rice_plan(code, m.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(), kdev.stream())
-                klib.kmp_rice_pack(code, m.data_ptr(), n, prm.data_ptr(), ws.data_ptr(), pay.data_ptr(), kdev.stream())
-
-            def rice_unpack_dev():
-                klib.kmp_unpack_plan(bwv.data_ptr(), n, ws.data_ptr(), kdev.stream())
-                klib.kmp_rice_unpack(code, pay.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(),
-                                     out.data_ptr(), kdev.stream())
-
-            rice_pack_dev()
-            rice_unpack_dev()
-            torch.cuda.synchronize()
-            assert torch.equal(out, m)
-            words = int(ws[int(klib.kmp_pack_total_offset(n)):int(klib.kmp_pack_total_offset(n)) + 8]
-                        .view(torch.int64).item())
-            cmap = 4 * words + 2 * nb
-            tag = f'noise{int(noise)}'
-            line = {'row': f'rice:{tag}', 'what': f'structured 512^3 u16 (smooth field + N(0, {noise}^2)), 512 x 64^3, '
-                                                 f'MeanPredictor(0)',
+            hb = b_r[:4096].cpu().numpy().tobytes()
+            t_enc_dev = gpu_time(lambda: kpk._rice_encode_launch((lo, *maps), dims), args.reps)
+            t_dec_dev = gpu_time(lambda: kpk._rice_decode_launch(b_r, hb), args.reps)
+            # order-0 entropy of the maps' residual samples (all 7 maps)
+            res = torch.cat([m.reshape(-1) for m in maps]).view(torch.int16).to(torch.int32) & 0xffff
+            cnt = torch.bincount(res, minlength=65536).double()
+            pr = cnt[cnt > 0] / res.numel()
+            h0 = float(-(pr * torch.log2(pr)).sum())
+            # zlib / lzma vs Rice on the same bytes: the maps of the first 16 tiles (3.7 MB)
+            sample = [m[:16].contiguous() for m in maps]
+            sb = torch.cat([m.reshape(-1) for m in sample]).cpu().numpy().tobytes()
+            ns = sum(m.numel() for m in sample)
+            rice_s = kom.packing.pack_encoded(sample[0], (tuple(sample[1:]), dims), 'rice').numel()
+            # container files: one level vs levels='auto' (the whole volume as 512 tiles)
+            with tempfile.TemporaryDirectory() as td:
+                f1 = kom.container.compress(td + '/l1.kmp', tiles, pred, levels=1)
+                fa = kom.container.compress(td + '/la.kmp', tiles, pred, levels='auto')
+            mapb = sum(m.numel() for m in maps) * 2
+            line = {'row': f'rice:noise{int(noise)}', 'what': f'structured 512^3 u16 (smooth field + N(0, {noise}^2)), '
+                                                             f'512 x 64^3, MeanPredictor(0)',
                     'ratio_rice': round(raw / b_r.numel(), 3), 'ratio_planes': round(raw / b_p.numel(), 3),
                     'bits_per_voxel_rice': round(8 * b_r.numel() / tiles.numel(), 3),
                     'bits_per_voxel_planes': round(8 * b_p.numel() / tiles.numel(), 3),
+                    'residual_bits': {'H0': round(h0, 3), 'rice_all_maps': None,
+                                      'sample_16_tiles': {'rice': round(8 * rice_s / ns, 3),
+                                                          'zlib6': round(8 * len(zlib.compress(sb, 6)) / ns, 3),
+                                                          'lzma6': round(8 * len(lzma.compress(sb, preset=6)) / ns, 3)}},
+                    'file_ratio': {'levels_1': round(f1['ratio'], 3), 'levels_auto': round(fa['ratio'], 3),
+                                   'auto_levels': fa['levels']},
                     'pack_encoded_ms': round(t_enc * 1e3, 3), 'unpack_encoded_ms': round(t_dec * 1e3, 3),
+                    'pack_device_us': round(t_enc_dev * 1e6, 1), 'unpack_device_us': round(t_dec_dev * 1e6, 1),
                     'pack_encoded_GBps_raw': round(raw / t_enc / 1e9, 1),
                     'unpack_encoded_GBps_raw': round(raw / t_dec / 1e9, 1)}
+            # the residual maps' share of the bundle (lowres excluded): bits per residual sample
+            lo_only = kom.packing.pack(lo, 'rice').numel()
+            line['residual_bits']['rice_all_maps'] = round(8 * (b_r.numel() - lo_only) / (mapb // 2), 3)
             print(json.dumps(line), flush=True)
-            emit(f'rice:{tag}:pack_device', 'rice plan + scan + pack kernels of the 32 MiB C map (no header / sync)',
-                 m.numel() * 2 * 2 + cmap, gpu_time(rice_pack_dev, args.reps))
-            emit(f'rice:{tag}:unpack_device', 'scan + rice unpack kernels of the same map', m.numel() * 2 + cmap,
-                 gpu_time(rice_unpack_dev, args.reps))
-            del tiles, lo, maps, maps2, lo2, b_r, b_p
+            # device chains against HBM: the encode reads the 8 arrays once and writes the bundle,
+            # the decode reads the bundle and writes the 8 arrays
+            emit(f'rice:noise{int(noise)}:pack_device', 'rice bundle encode: one single-pass launch for lowres + 7 maps',
+                 raw + b_r.numel(), t_enc_dev)
+            emit(f'rice:noise{int(noise)}:unpack_device', 'rice bundle decode: one launch for lowres + 7 maps',
+                 raw + b_r.numel(), t_dec_dev)
+            del tiles, lo, maps, maps2, lo2, b_r, b_p, vol512, res, cnt
         del field
 
     # geometry primitives (volume/utils.py) on the C3 tile batch

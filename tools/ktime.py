@@ -1,6 +1,6 @@
 """Launch the fused volume/image codec N times per direction (for rocprofv3 --kernel-trace --stats).
     python tools/ktime.py [volume|image] [padding] [reps] [mean|linear]
-    python tools/ktime.py rice SIGMA [reps]"""
+    python tools/ktime.py rice SIGMA [reps]   (the Rice bundle kernels on a C3 encode result)"""
 import os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -23,29 +23,19 @@ if wl == 'categorical':  # rank coder, 1M elements x 256 logits (tools/bench_row
     assert torch.equal(dec, gt)
     print('ok', os.environ.get('KMP_TAG', ''))
     sys.exit(0)
-if wl == 'rice':  # Rice plan + pack + unpack of one 32 MiB u16 map of N(0, sigma^2) residuals (sigma = argv[2])
-    from kompressor_amd import _device as kdev
-    from kompressor_amd._lib import lib as klib
+if wl == 'rice':  # Rice bundle encode + decode of 8 C3-sized u16 maps of N(0, sigma^2) residuals (sigma = argv[2])
+    from kompressor_amd import packing as kpk
     gen = torch.Generator(device='cuda').manual_seed(0)
-    m = (max(p, 1) * torch.randn(1 << 24, device='cuda', generator=gen)).round().to(torch.int32).to(torch.int16) \
-        .view(torch.uint16)
-    n, code = m.numel(), kdev.dtype_code(m)
-    nb = int(klib.kmp_pack_blocks(n))
-    ws = torch.empty(int(klib.kmp_pack_workspace_bytes(n)), dtype=torch.uint8, device='cuda')
-    prm = torch.empty(nb, dtype=torch.uint8, device='cuda')
-    bwv = torch.empty(nb, dtype=torch.uint8, device='cuda')
-    pay = torch.empty(nb * 34 * 4, dtype=torch.uint8, device='cuda')
-    out = torch.empty_like(m)
-    s = kdev.stream()
+    arrays = [(max(p, 1) * torch.randn((512, 32, 32, 32, 1), device='cuda', generator=gen)).round().to(torch.int32)
+              .to(torch.int16).view(torch.uint16) for _ in range(8)]
+    blob = kpk.pack_encoded(arrays[0], (tuple(arrays[1:]), (1, 1, 1)))
+    hb = blob[:4096].cpu().numpy().tobytes()
     for _ in range(reps):
-        assert klib.kmp_rice_plan(code, m.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(), s) == 0
-        assert klib.kmp_rice_pack(code, m.data_ptr(), n, prm.data_ptr(), ws.data_ptr(), pay.data_ptr(), s) == 0
-        assert klib.kmp_unpack_plan(bwv.data_ptr(), n, ws.data_ptr(), s) == 0
-        assert klib.kmp_rice_unpack(code, pay.data_ptr(), n, prm.data_ptr(), bwv.data_ptr(), ws.data_ptr(),
-                                    out.data_ptr(), s) == 0
+        kpk._rice_encode_launch(arrays, (1, 1, 1))
+        outs, _, bad = kpk._rice_decode_launch(blob, hb)
     torch.cuda.synchronize()
-    assert torch.equal(out, m)
-    print('ok', os.environ.get('KMP_TAG', ''), 'payload words', int(bwv.to(torch.int64).sum()))
+    assert int(bad.item()) == 0 and all(torch.equal(a, b) for a, b in zip(outs, arrays))
+    print('ok', os.environ.get('KMP_TAG', ''), 'bundle bytes', blob.numel())
     sys.exit(0)
 ndim = 3 if wl == 'volume' else 2
 shape, dt = ((512, 64, 64, 64, 1), np.uint16) if ndim == 3 else ((1024, 256, 256, 1), np.uint8)
