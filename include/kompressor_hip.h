@@ -269,7 +269,7 @@ int kmp_unpack(int32_t dtype, const uint64_t* payload, int64_t n, const uint8_t*
 /* §8f f-3 -- no reference counterpart, volume/encode_decode.py:56 returns the residuals         */
 /* unreduced; byte layout spec: oracle/rice.py pack_bundle).  n samples of ``dtype`` (8/16/32-bit), */
 /* zigzag-mapped, blocks of 64: params[b] = Rice k + 1 (0 = all-zero block), bw[b] = the block's  */
-/* 32-bit payload words; tiles of 32 blocks.  All arrays of a bundle share ONE payload region in  */
+/* 32-bit payload words; tiles of 256 blocks.  All arrays of a bundle share ONE payload region in  */
 /* tile order; each array keeps a u64 table of its tiles' word offsets into it.                  */
 /* ---------------------------------------------------------------------------------------- */
 typedef struct kmp_rice_array {
@@ -279,7 +279,7 @@ typedef struct kmp_rice_array {
   int64_t toff_off;    /* byte offset of the u64 tile offsets [kmp_rice_tiles(n)] (8-aligned)    */
   int64_t rec_off;     /* byte offset of the array's {u64 first word, u64 end word} (8-aligned)  */
 } kmp_rice_array;
-/* tiles of 32 blocks of 64 samples: ceil(ceil(n / 64) / 32) */
+/* tiles of 256 blocks of 64 samples: ceil(ceil(n / 64) / 256) */
 int64_t kmp_rice_tiles(int64_t n);
 /* workspace of the single-pass encode: the look-back states of tiles_total tiles + a ticket */
 int64_t kmp_rice_bundle_workspace_bytes(int64_t tiles_total);

@@ -77,20 +77,27 @@ __global__ void __launch_bounds__(256) linear_reorder_kernel(const float* __rest
 
 // One sweep: channels KS[0..NK) of the lane's VX = 4 cells (row Y, cols X..X+3) of cell plane
 // c-1+PLANE, from the staged planes.  Results cast to T in out[kk][1..4].
+// All-zero weights and bias: the channels of a cell plane outside the tile (plane c-1 at c = 0,
+// plane c at c >= Lcz) evaluated with these are 0.0 -> 0, what the aggregation's mask gives them
+// (FULL kernel: the plane masks disappear from the aggregation)
+__constant__ float kZeroW[kNC * 64 + 19];
+
 template <typename T, int P, int PLANE, int NK>
 __device__ __forceinline__ void sweep(const float* st, const L3P& a, int Yc, int X, const int (&KS)[NK], int woff,
-                                      uint32_t (&out)[NK][5]) {
+                                      bool zero, uint32_t (&out)[NK][5]) {
   constexpr int NB = 2 * P + 2;
   constexpr int NF = 4 + 2 * P + 1;  // nodes X-P .. X+3+P+1
   constexpr int NV = (NF + 3) / 4;   // 16-byte LDS reads per node row
   // the sweep's weights in consumption order [node row][kk][dx] (a.Wr, written by
   // linear_reorder_kernel), read through the constant address space: per node row NK x NB
   // contiguous words = a few wide uniform scalar loads into SGPRs
-  const __attribute__((address_space(4))) float* Wc = (const __attribute__((address_space(4))) float*)(a.Wr + woff);
+  typedef const __attribute__((address_space(4))) float* CF;
+  const CF Wc = zero ? (CF)kZeroW : (CF)(a.Wr + woff);
+  const CF Bc = zero ? (CF)kZeroW : (CF)a.b;
   f32x2 acc[NK][2];
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
-    const float bk = a.b[KS[kk]];
+    const float bk = Bc[KS[kk]];
     acc[kk][0] = (f32x2){bk, bk};
     acc[kk][1] = (f32x2){bk, bk};
   }
@@ -131,7 +138,12 @@ __device__ __forceinline__ void sweep(const float* st, const L3P& a, int Yc, int
   }
 }
 
-template <typename T, bool DEC, int P>
+// FULL: the tile's cells fill the stored lowres rows and columns (Lcy == Ey, Lcx == Ex: every
+// even-sized tile, C3's 64^3 included).  Then the y+1 validity and every x validity but the row's
+// first cell are compile-time true and a missing cell plane is zeroed at the source (kZeroW), so
+// the aggregation masks only the row-above channels on row 0 and the left cell on lane 0 (the p = 0
+// kernel's FULL body, kmp_codec_linear3d.hip)
+template <typename T, bool DEC, int P, bool FULL>
 __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   constexpr int VX = 4;  // u16: 4 outputs per lane
   static_assert(sizeof(T) == 2, "u16");
@@ -163,7 +175,7 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   const bool live = wave_live && Y < a.Ey;
   const int Yc = live ? Y : a.Ey - 1;
   const bool first = r == 0;
-  const bool vy1 = Y < a.Lcy;
+  const bool vy1 = FULL || Y < a.Lcy;  // FULL: Lcy == Ey, and lanes past Ey are not live
   const bool vy0 = Y >= 1;
   const bool vz1 = c < a.Lcz, vz0 = c >= 1;
 
@@ -262,8 +274,8 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   constexpr int KC[kNC] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16};  // plane c
   constexpr int KQ[kNQ] = {5, 13, 14, 17, 18};                               // plane c-1
   uint32_t PC[14][5], PQ[5][5];
-  sweep<T, P, 0, 5>(st, a, Yc, X, KQ, 0, PQ);
-  sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), PC);
+  sweep<T, P, 0, 5>(st, a, Yc, X, KQ, 0, FULL && !vz0, PQ);
+  sweep<T, P, 1, 14>(st, a, Yc, X, KC, kNQ * (2 * P + 2) * (2 * P + 2) * (2 * P + 2), FULL && !vz1, PC);
   auto& P0 = PC[0]; auto& P1 = PC[1]; auto& P2 = PC[2]; auto& P3 = PC[3]; auto& P4 = PC[4];
   auto& P6 = PC[5]; auto& P7 = PC[6]; auto& P8 = PC[7]; auto& P9 = PC[8]; auto& P10 = PC[9];
   auto& P11 = PC[10]; auto& P12 = PC[11]; auto& P15 = PC[12]; auto& P16 = PC[13];
@@ -312,10 +324,12 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
 
   bool vx[VX + 1];
 #pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  for (int q = 0; q <= VX; ++q) vx[q] = (FULL && q >= 1) || ((X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
   const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
-  auto m = [&](const uint32_t (&v)[VX + 1], int q, bool zok, bool yok) { return (zok && yok && vx[q]) ? v[q] : 0u; };
+  auto m = [&](const uint32_t (&v)[VX + 1], int q, bool zok, bool yok) {
+    return ((FULL || zok) && yok && vx[q]) ? v[q] : 0u;  // FULL: a missing z plane's channels are 0 already
+  };
   auto put8 = [&](int k, const uint32_t (&res)[VX]) {
     int par[3];
     map_parity(3, k, par);
@@ -482,7 +496,8 @@ int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    l3p::linear3dp_kernel<T, false, 1><<<grid, block, lds, stream>>>(a);
+    if (a.Lcy == a.Ey && a.Lcx == a.Ex) l3p::linear3dp_kernel<T, false, 1, true><<<grid, block, lds, stream>>>(a);
+    else l3p::linear3dp_kernel<T, false, 1, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3dp_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -509,7 +524,8 @@ int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     if (!ws || ws_bytes < kL3pWsBytes) return KMP_ERR_UNSUPPORTED;
     a.Wr = (const float*)ws;
     l3p::linear_reorder_kernel<<<1, 256, 0, stream>>>(pred->weights, (float*)ws, 4);
-    l3p::linear3dp_kernel<T, true, 1><<<grid, block, lds, stream>>>(a);
+    if (a.Lcy == a.Ey && a.Lcx == a.Ex) l3p::linear3dp_kernel<T, true, 1, true><<<grid, block, lds, stream>>>(a);
+    else l3p::linear3dp_kernel<T, true, 1, false><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3dp_decode");
   }
   return KMP_ERR_UNSUPPORTED;

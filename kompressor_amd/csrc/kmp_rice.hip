@@ -108,8 +108,8 @@ __device__ __forceinline__ int select32(uint32_t x, uint32_t t) {
 // ---- the Rice bundle (format v2): every array of a call in one single-pass encode launch and
 // one decode launch per sample width ----
 //
-// Work unit: a TILE of 32 blocks (2048 samples): one 256-thread workgroup, each wave 8 blocks in
-// the lane layout above.  Tiles of all arrays form one sequence (array after array); a tile's
+// Work unit: a TILE of 256 blocks (16384 samples): one 256-thread workgroup, each wave 8 steps of
+// 8 blocks in the lane layout above (fewer, larger tiles: the look-back chain is per tile).  Tiles of all arrays form one sequence (array after array); a tile's
 // payload words follow its predecessor's, so the bundle holds ONE payload region and per array a
 // table of tile offsets (u64 word offsets) that lets the decoder start every tile independently.
 //
@@ -117,8 +117,8 @@ __device__ __forceinline__ int select32(uint32_t x, uint32_t t) {
 // from the bit-plane popcounts (the plan above, in registers), the block's exclusive prefix inside
 // the wave (scan over the 8 groups) and the workgroup (LDS), the tile's start by a decoupled
 // look-back over the tiles before it (a tile publishes its aggregate, then its inclusive prefix;
-// tiles are numbered by an atomic ticket in start order, so every tile a tile waits on has
-// started -- no deadlock), then the payload written from the same registers.  Was: plan kernel
+// the first wave reads 64 predecessors per round trip; tiles are numbered by an atomic ticket in
+// start order, so every tile a tile waits on has started -- no deadlock), then the payload written from the same registers.  Was: plan kernel
 // (reads the map), two scan launches, pack kernel (reads the map again) per array.
 //
 // Decode (rice_bundle_decode_kernel): the tile offset from the table, the blocks' offsets by the
@@ -127,7 +127,8 @@ __device__ __forceinline__ int select32(uint32_t x, uint32_t t) {
 // [2k + 2, 2W + 2], a zero block without payload, the tile's words meeting the next tile's offset);
 // a tile that fails decodes as zeros and is counted, so a corrupt bundle raises on the host after
 // the one synchronisation instead of steering a read outside the blob.
-constexpr int kTileBlocks = 32;
+constexpr int kTileSteps = 8;                     // wave steps (of 8 blocks) per wave and tile
+constexpr int kTileBlocks = 4 * 8 * kTileSteps;    // 256 blocks = 16384 samples per tile
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kValMask = (1ull << 62) - 1;
 
 struct RArr {        // device copy of kmp_rice_array
@@ -167,8 +168,9 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
                                                                uint8_t* __restrict__ blob, int64_t payload_off,
                                                                uint64_t* __restrict__ state,
                                                                unsigned* __restrict__ ticket) {
-  constexpr int NP = Sw<W>::NP;
+  constexpr int NP = Sw<W>::NP, NW = Sw<W>::NW;
   constexpr int UMAX = 2 * W + 2;
+  constexpr int S = kTileSteps;
   __shared__ uint32_t stream_lds[4][8][UMAX];
   __shared__ uint32_t wsum[4];
   __shared__ uint64_t s_excl;
@@ -180,110 +182,144 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
   const int a = array_of(A, g);
   const RArr& R = A.a[a];
   const int64_t t = g - R.tile0;
-  const int64_t blk = t * kTileBlocks + wv * 8 + g8;
-  const bool has = blk < R.nb;
-  uint32_t w[Sw<W>::NW];
-  load8s<W>(R.x, R.n, blk * 64 + j * 8, w);
-  // ---- plan: k* and the word count (as rice_plan in round 2, now in the same pass) ----
-  uint32_t Z[NP][2];
-  zplanes<W>(w, Z);
-  uint32_t cnt[2 * NP];
-#pragma unroll
-  for (int i = 0; i < 2 * NP; ++i) cnt[i] = group8_sum(bytes_popcount(Z[i >> 1][i & 1]), lane);
-  uint32_t S = 0, key = 0xffffffffu;
-#pragma unroll
-  for (int k = W - 1; k >= 0; --k) {
-    const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    S = 2u * S + c;
-    if constexpr (W > 16) S = min(S, kSumCap);
-    key = min(key, ((S + 95u) & ~31u) + 65u * (uint32_t)k);
-  }
-  const bool zero = S == 0 || !has;
-  const int param = zero ? 0 : (int)(key & 31u) + 1;
-  const uint32_t words = zero ? 0u : key >> 5;
+  const int64_t blk0 = t * kTileBlocks + wv * 8 * S;  // the wave's first block; step s: blk0 + 8 s + g8
   uint8_t* params = blob + R.side_off;
   uint8_t* bw = params + ((R.nb + 7) & ~(int64_t)7);
-  if (j == 0 && has) {
-    params[blk] = (uint8_t)param;
-    bw[blk] = (uint8_t)words;
+  // ---- pass 1: per step, the block's k* and word count (the plan in registers); the samples stay
+  // in registers for pass 2 ----
+  uint32_t w[S][NW];
+  int prm[S];
+  uint32_t bex[S];  // the block's exclusive word offset inside the wave
+  uint32_t wtot = 0;
+#pragma unroll
+  for (int st = 0; st < S; ++st) load8s<W>(R.x, R.n, (blk0 + 8 * st + g8) * 64 + j * 8, w[st]);
+#pragma unroll
+  for (int st = 0; st < S; ++st) {
+    const int64_t blk = blk0 + 8 * st + g8;
+    const bool has = blk < R.nb;
+    uint32_t Z[NP][2];
+    zplanes<W>(w[st], Z);
+    uint32_t cnt[2 * NP];
+#pragma unroll
+    for (int i = 0; i < 2 * NP; ++i) cnt[i] = group8_sum(bytes_popcount(Z[i >> 1][i & 1]), lane);
+    uint32_t Ssum = 0, key = 0xffffffffu;
+#pragma unroll
+    for (int k = W - 1; k >= 0; --k) {
+      const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
+      Ssum = 2u * Ssum + c;
+      if constexpr (W > 16) Ssum = min(Ssum, kSumCap);
+      key = min(key, ((Ssum + 95u) & ~31u) + 65u * (uint32_t)k);
+    }
+    const bool zero = Ssum == 0 || !has;
+    prm[st] = zero ? 0 : (int)(key & 31u) + 1;
+    const uint32_t words = zero ? 0u : key >> 5;
+    if (j == 0 && has) {
+      params[blk] = (uint8_t)prm[st];
+      bw[blk] = (uint8_t)words;
+    }
+    uint32_t stot;
+    bex[st] = wtot + wave_groups_excl(words, lane, &stot);
+    wtot += stot;
   }
-  // ---- offsets: in the wave, in the workgroup, then the tile's start (decoupled look-back) ----
-  uint32_t wtot;
-  const uint32_t bexcl = wave_groups_excl(words, lane, &wtot);
+  // ---- the tile's start: workgroup sum, then the decoupled look-back ----
   if (lane == 0) wsum[wv] = wtot;
   __syncthreads();
   const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   uint32_t wbase = 0;
   for (int q = 0; q < wv; ++q) wbase += wsum[q];
-  if (tid == 0) {
+  if (wv == 0) {
+    // decoupled look-back by the whole first wave: lane l reads the state of tile base - l, so each
+    // memory round trip covers 64 predecessors (a thread walking them one by one serialised the
+    // chain at ~0.5 us per tile).  The states are the only data exchanged, so relaxed agent-scope
+    // atomics suffice: a release store at agent scope writes back the XCD's dirty L2 lines (every
+    // tile's payload) and an acquire load invalidates caches
     uint64_t excl = 0;
     if (g == 0) {
-      __hip_atomic_store(&state[0], kFlagPre | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&state[0], kFlagPre | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_store(&state[g], kFlagAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      for (int64_t i = g - 1; i >= 0;) {
-        const uint64_t v = __hip_atomic_load(&state[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v >> 62) == 0) {
+      if (lane == 0) __hip_atomic_store(&state[g], kFlagAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t base = g - 1;
+      while (true) {
+        const int64_t i = base - lane;
+        uint64_t v = i >= 0 ? __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
+        while (__any((v >> 62) == 0)) {  // a predecessor has not published yet: re-read those
           __builtin_amdgcn_s_sleep(1);
-          continue;
+          if ((v >> 62) == 0) v = __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        excl += v & kValMask;
-        if ((v >> 62) == 2) break;
-        --i;
+        const uint64_t pre = __ballot((v >> 62) == 2);  // tiles whose inclusive prefix is known
+        const int lp = pre ? __builtin_ctzll(pre) : 64;  // the nearest one
+        uint64_t c = lane <= lp ? (v & kValMask) : 0;  // aggregates after it, and its prefix
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+        excl += c;
+        if (pre) break;
+        base -= 64;
       }
-      __hip_atomic_store(&state[g], kFlagPre | (excl + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&state[g], kFlagPre | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_excl = excl;
-    ((uint64_t*)(blob + R.toff_off))[t] = excl;
-    uint64_t* rec = (uint64_t*)(blob + R.rec_off);
-    if (t == 0) rec[0] = excl;
-    if (t == R.ntile - 1) rec[1] = excl + agg;
-    if (g == tiles_total - 1) {  // the bundle's payload words and byte size (header fields 56, 64)
-      ((uint64_t*)blob)[7] = excl + agg;
-      ((uint64_t*)blob)[8] = (uint64_t)payload_off + (((excl + agg) * 4 + 7) & ~7ull);
+    if (lane == 0) {
+      s_excl = excl;
+      ((uint64_t*)(blob + R.toff_off))[t] = excl;
+      uint64_t* rec = (uint64_t*)(blob + R.rec_off);
+      if (t == 0) rec[0] = excl;
+      if (t == R.ntile - 1) rec[1] = excl + agg;
+      if (g == tiles_total - 1) {  // the bundle's payload words and byte size (header fields 56, 64)
+        ((uint64_t*)blob)[7] = excl + agg;
+        ((uint64_t*)blob)[8] = (uint64_t)payload_off + (((excl + agg) * 4 + 7) & ~7ull);
+      }
     }
   }
   __syncthreads();
-  const uint64_t off = s_excl + wbase + bexcl;
+  const uint64_t wstart = s_excl + wbase;
   uint32_t* payload = (uint32_t*)(blob + payload_off);
-  // ---- payload: the k low planes, then the unary part (as round 2's rice_pack) ----
-  const int k = param > 0 ? param - 1 : 0;
   uint32_t* ustream = stream_lds[wv][g8];
+  // ---- pass 2: the payload of each step's blocks: the k low planes, then the unary part ----
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    xtr8(Z[p][0], Z[p][1], j);
-    const int b = 8 * p + j;
-    if (param > 0 && b < k) {
-      payload[off + 2 * b] = Z[p][0];
-      payload[off + 2 * b + 1] = Z[p][1];
+  for (int st = 0; st < S; ++st) {
+    const int param = prm[st];
+    const uint64_t off = wstart + bex[st];
+    const int k = param > 0 ? param - 1 : 0;
+    uint32_t Z[NP][2];
+    zplanes<W>(w[st], Z);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      xtr8(Z[p][0], Z[p][1], j);
+      const int b = 8 * p + j;
+      if (param > 0 && b < k) {
+        payload[off + 2 * b] = Z[p][0];
+        payload[off + 2 * b + 1] = Z[p][1];
+      }
     }
-  }
-  uint32_t q[8], len = 0;
+    uint32_t q[8], len = 0;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    q[e] = zigzag<W>(sample_of<W>(w, e)) >> k;
-    len += q[e] + 1u;
-  }
-  const uint32_t incl = group8_incl(len, j);
-  const uint32_t tot = (uint32_t)__shfl((int)incl, (g8 << 3) | 7, 64);
-  const uint32_t uw = (tot + 31u) >> 5;
-  for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  uint32_t pos = incl - len;
+    for (int e = 0; e < 8; ++e) {
+      q[e] = zigzag<W>(sample_of<W>(w[st], e)) >> k;
+      len += q[e] + 1u;
+    }
+    const uint32_t incl = group8_incl(len, j);
+    const uint32_t tot = (uint32_t)__shfl((int)incl, (g8 << 3) | 7, 64);
+    const uint32_t uw = (tot + 31u) >> 5;
+    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint32_t pos = incl - len;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    pos += q[e];
-    if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
-    pos += 1u;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (param > 0) {
-    const uint64_t ubase = off + 2u * (uint32_t)k;
-    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) payload[ubase + i] = ustream[i];
+    for (int e = 0; e < 8; ++e) {
+      pos += q[e];
+      if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
+      pos += 1u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (param > 0) {
+      const uint64_t ubase = off + 2u * (uint32_t)k;
+      for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) payload[ubase + i] = ustream[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();  // the next step's zeroing must not overtake these reads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
 }
 
@@ -292,8 +328,9 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
                                                                const uint8_t* __restrict__ blob,
                                                                int64_t payload_off, uint64_t payload_words,
                                                                unsigned long long* __restrict__ bad_out) {
-  constexpr int NP = Sw<W>::NP;
-  constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave's 8 blocks, at most
+  constexpr int NP = Sw<W>::NP, NW = Sw<W>::NW;
+  constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave step's 8 blocks, at most
+  constexpr int S = kTileSteps;
   __shared__ uint32_t span_lds[4][SPAN];
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t wbad[4];
@@ -302,17 +339,32 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
   const int a = array_of(A, g);
   const RArr& R = A.a[a];
   const int64_t t = g - R.tile0;
-  const int64_t blk = t * kTileBlocks + wv * 8 + g8;
-  const bool has = blk < R.nb;
+  const int64_t blk0 = t * kTileBlocks + wv * 8 * S;
   const uint8_t* params = blob + R.side_off;
   const uint8_t* bwp = params + ((R.nb + 7) & ~(int64_t)7);
-  int param = has ? params[blk] : 0;
-  int words = has ? bwp[blk] : 0;
-  const int kk = param - 1;
-  bool bad = param == 0 ? words != 0 : (kk >= W || words < 2 * kk + 2 || words > 2 * W + 2);
-  if (bad) words = 0;  // keeps the offsets of the good blocks in bounds
-  uint32_t wtot;
-  const uint32_t bexcl = wave_groups_excl((uint32_t)words, lane, &wtot);
+  // ---- the side information of the wave's S steps, checked; per-block offsets in the wave ----
+  int prm[S], wds[S];
+  uint32_t bex[S], stp[S];
+  uint32_t wtot = 0;
+  bool bad = false;
+#pragma unroll
+  for (int st = 0; st < S; ++st) {
+    const int64_t blk = blk0 + 8 * st + g8;
+    const bool has = blk < R.nb;
+    prm[st] = has ? params[blk] : 0;
+    wds[st] = has ? bwp[blk] : 0;
+  }
+#pragma unroll
+  for (int st = 0; st < S; ++st) {
+    const int kk = prm[st] - 1;
+    const bool b = prm[st] == 0 ? wds[st] != 0 : (kk >= W || wds[st] < 2 * kk + 2 || wds[st] > 2 * W + 2);
+    bad |= b;
+    if (b) wds[st] = 0;  // keeps the offsets of the good blocks in bounds
+    uint32_t stot;
+    bex[st] = wave_groups_excl((uint32_t)wds[st], lane, &stot);
+    stp[st] = wtot;
+    wtot += stot;
+  }
   const bool wave_bad = __any(bad);
   if (lane == 0) {
     wsum[wv] = wtot;
@@ -326,98 +378,103 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
   const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   const bool tile_bad = wbad[0] || wbad[1] || wbad[2] || wbad[3] || start > payload_words || end > payload_words ||
                         start + agg != end || (t == 0 && start != rec[0]);
-  if (tile_bad) {
-    param = 0;
-    words = 0;
-    if (tid == 0) atomicAdd(bad_out, 1ull);
-  }
+  if (tile_bad && tid == 0) atomicAdd(bad_out, 1ull);
   uint32_t wbase = 0;
   for (int q = 0; q < wv; ++q) wbase += wsum[q];
-  const uint64_t off = tile_bad ? 0 : start + wbase + bexcl;
   const uint32_t* payload = (const uint32_t*)(blob + payload_off);
-  // ---- the wave's 8 blocks are consecutive: stage their words in LDS, then unpack ----
-  const uint64_t wstart = tile_bad ? 0 : start + wbase;
-  const int cnt = tile_bad ? 0 : (int)min<uint64_t>((uint64_t)wsum[wv], (uint64_t)SPAN);
   uint32_t* const wspan = span_lds[wv];
-  for (int i = lane; i < cnt; i += 64) wspan[i] = payload[wstart + i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const uint32_t* const bp = wspan + (off - wstart);
-  const int k = param > 0 ? param - 1 : 0;
-  const int uw = param > 0 ? words - 2 * k : 0;
-  uint32_t Z[NP][2];
+  // ---- per step: stage the 8 blocks' words in LDS, unpack ----
+#pragma unroll 1
+  for (int st = 0; st < S; ++st) {
+    int param = tile_bad ? 0 : prm[st];
+    const int words = tile_bad ? 0 : wds[st];
+    const uint32_t sw = (st + 1 < S ? stp[st + 1] : wtot) - stp[st];  // this step's words
+    const uint64_t sstart = start + wbase + stp[st];
+    const int cnt = tile_bad ? 0 : (int)min<uint64_t>((uint64_t)sw, (uint64_t)SPAN);
+    for (int i = lane; i < cnt; i += 64) wspan[i] = payload[sstart + i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t* const bp = wspan + (tile_bad ? 0 : bex[st]);
+    const int k = param > 0 ? param - 1 : 0;
+    const int uw = param > 0 ? words - 2 * k : 0;
+    uint32_t Z[NP][2];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int b = 8 * p + j;
-    const bool hv = param > 0 && b < k;
-    Z[p][0] = hv ? bp[2 * b] : 0u;
-    Z[p][1] = hv ? bp[2 * b + 1] : 0u;
-  }
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    xtr8(Z[p][0], Z[p][1], j);
-    tr8x8(Z[p][0], Z[p][1]);
-  }
-  uint32_t lowv[Sw<W>::NW];
-  scatter_bytes<W>(Z, lowv);
-  const uint32_t* us = bp + 2 * k;
-  uint32_t q[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = 0u;
-  if (param > 0 && uw > 0) {
-    uint32_t pos = 0;
-    if (j > 0) {
-      const uint32_t r = 8u * j - 1u;
-      uint32_t acc = 0, word = 0;
-      int wi = 0;
-      for (; wi < uw; ++wi) {
-        word = us[wi];
-        const uint32_t c = __builtin_popcount(word);
-        if (acc + c > r) break;
-        acc += c;
-      }
-      pos = wi < uw ? 32u * wi + select32(word, r - acc) + 1u : 32u * uw;
+    for (int p = 0; p < NP; ++p) {
+      const int b = 8 * p + j;
+      const bool hv = param > 0 && b < k;
+      Z[p][0] = hv ? bp[2 * b] : 0u;
+      Z[p][1] = hv ? bp[2 * b + 1] : 0u;
     }
-    int wi = (int)(pos >> 5);
-    const uint32_t sh = pos & 31u;
-    const uint32_t a0 = wi < uw ? us[wi] : 0u, b0 = wi + 1 < uw ? us[wi + 1] : 0u, c0 = wi + 2 < uw ? us[wi + 2] : 0u;
-    uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c0, b0, sh) << 32) | __builtin_amdgcn_alignbit(b0, a0, sh);
-    if (__builtin_popcountll(win) >= 8) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t tz = (uint32_t)__builtin_ctzll(win);
-        q[e] = tz;
-        win = (win >> tz) >> 1;
-      }
-    } else {
-      uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
-      uint32_t base = pos;
+    for (int p = 0; p < NP; ++p) {
+      xtr8(Z[p][0], Z[p][1], j);
+      tr8x8(Z[p][0], Z[p][1]);
+    }
+    uint32_t lowv[NW];
+    scatter_bytes<W>(Z, lowv);
+    const uint32_t* us = bp + 2 * k;
+    uint32_t q[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        while (cur == 0u && wi + 1 < uw) {
-          ++wi;
-          cur = us[wi];
-          base = 32u * wi;
+    for (int e = 0; e < 8; ++e) q[e] = 0u;
+    if (param > 0 && uw > 0) {
+      uint32_t pos = 0;
+      if (j > 0) {
+        const uint32_t r = 8u * j - 1u;
+        uint32_t acc = 0, word = 0;
+        int wi = 0;
+        for (; wi < uw; ++wi) {
+          word = us[wi];
+          const uint32_t c = __builtin_popcount(word);
+          if (acc + c > r) break;
+          acc += c;
         }
-        if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
-        const uint32_t tz = __builtin_ctz(cur);
-        q[e] = base + tz - pos;
-        pos = base + tz + 1u;
-        cur = tz == 31u ? 0u : cur >> (tz + 1u);
-        base = pos;
+        pos = wi < uw ? 32u * wi + select32(word, r - acc) + 1u : 32u * uw;
+      }
+      int wi = (int)(pos >> 5);
+      const uint32_t sh = pos & 31u;
+      const uint32_t a0 = wi < uw ? us[wi] : 0u, b0 = wi + 1 < uw ? us[wi + 1] : 0u, c0 = wi + 2 < uw ? us[wi + 2] : 0u;
+      uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c0, b0, sh) << 32) | __builtin_amdgcn_alignbit(b0, a0, sh);
+      if (__builtin_popcountll(win) >= 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t tz = (uint32_t)__builtin_ctzll(win);
+          q[e] = tz;
+          win = (win >> tz) >> 1;
+        }
+      } else {
+        uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
+        uint32_t base = pos;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          while (cur == 0u && wi + 1 < uw) {
+            ++wi;
+            cur = us[wi];
+            base = 32u * wi;
+          }
+          if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
+          const uint32_t tz = __builtin_ctz(cur);
+          q[e] = base + tz - pos;
+          pos = base + tz + 1u;
+          cur = tz == 31u ? 0u : cur >> (tz + 1u);
+          base = pos;
+        }
       }
     }
-  }
-  uint32_t wout[Sw<W>::NW];
+    uint32_t wout[NW];
 #pragma unroll
-  for (int i = 0; i < Sw<W>::NW; ++i) wout[i] = 0u;
+    for (int i = 0; i < NW; ++i) wout[i] = 0u;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t z = param > 0 ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
-    set_sample<W>(wout, e, unzigzag<W>(z));
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t z = param > 0 ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
+      set_sample<W>(wout, e, unzigzag<W>(z));
+    }
+    const int64_t blk = blk0 + 8 * st + g8;
+    if (blk < R.nb) store8s<W>((void*)R.x, R.n, blk * 64 + j * 8, wout);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();  // the next step's staging must not overtake these reads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  if (has) store8s<W>((void*)R.x, R.n, blk * 64 + j * 8, wout);
 }
 
 // side information a blob may hold (one workgroup; written next to the scan's total): planes --

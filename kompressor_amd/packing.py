@@ -208,7 +208,7 @@ def _unpack_many(b, spans):
 
 _RHEAD = struct.Struct('<4sHHII8i4Q')       # 80 bytes: magic, version, count, nsp, 0, dims[8], payload_off,
 _RREC = struct.Struct('<II8q5q2Q')          # payload words, bytes, 0 / 128-byte array record
-_TILE_BLOCKS = 32
+_TILE_BLOCKS = 256
 _MAX_ARRAYS = 1 << 12
 
 

@@ -110,13 +110,13 @@ def unpack(params, bw, payload, n, dtype):
 #   80  count records of 128 bytes: u32 dtype code, u32 ndim, i64 shape[8] (zero-padded),
 #       i64 n, i64 nb, i64 ntile, i64 side_off, i64 toff_off, u64 first word, u64 end word
 #   then for each array params[nb] and bw[nb], each zero-padded to 8 bytes (at side_off);
-#   then for each array its tile offsets: u64 word offset of every tile of 32 blocks (at toff_off);
+#   then for each array its tile offsets: u64 word offset of every tile of 256 blocks (at toff_off);
 #   then, 8-aligned at payload_off, the payload: every array's blocks in order (array after
 #   array), the Rice block payload of ``pack`` above; bundle_bytes = payload_off + the payload
 #   zero-padded to 8 bytes.  An empty array (n = 0) has first = end = 0.
 # ---------------------------------------------------------------------------------------------
 
-TILE_BLOCKS = 32
+TILE_BLOCKS = 256
 DTYPE_CODE = {np.dtype(np.uint8): 0, np.dtype(np.uint16): 1, np.dtype(np.int32): 2, np.dtype(np.float32): 3,
               np.dtype(np.uint32): 4}
 CODE_DTYPE = {v: k for k, v in DTYPE_CODE.items()}

@@ -156,7 +156,7 @@ def test_rice_bundle_matches_spec(kom):
               np.zeros((0, 4), np.uint16),
               rng.standard_normal((9, 9)).astype(np.float32)]
     arrays += [_residuals(int(rng.integers(1, 9000)), np.uint8, rng, spread=6) for _ in range(40)]
-    arrays.append(_residuals(2048 * 3, np.uint16, rng, spread=2))  # exactly 3 tiles
+    arrays.append(_residuals(16384 * 3, np.uint16, rng, spread=2))  # exactly 3 tiles
     dims = (1, 0, 1)
     lo, maps = arrays[0], tuple(arrays[1:])
     blob = kom.packing.pack_encoded(lo, (maps, dims))
