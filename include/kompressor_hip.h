@@ -165,6 +165,13 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
                           const int64_t shape[3], int64_t C, int32_t padding, void* const out[7],
                           kmp_stream_t stream);
 
+/* The same maps written as ``out_dtype``: the sample dtype, or KMP_F32 -- the values a
+   float32-emitting predictions_fn (a network, volume/encode_decode.py:48) hands the coder; 3D,
+   C == 1 windows only (else KMP_ERR_UNSUPPORTED). */
+int kmp_mean_predict_maps_typed(int32_t nsp, int32_t dtype, int32_t out_dtype, const void* padded_lowres,
+                                int64_t B, const int64_t shape[3], int64_t C, int32_t padding,
+                                void* const out[7], kmp_stream_t stream);
+
 /* Linear predictor on a padded lowres window: per-cell [B, cells..., K, C] predictions in the
    dtype (MFMA f32), optionally also the f32 pre-cast values (``preds_f32`` may be NULL). */
 int kmp_linear_predict(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],

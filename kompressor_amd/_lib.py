@@ -82,6 +82,7 @@ _PROTOS = {
     'kmp_features_from_lowres': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp]),
     'kmp_maps_from_predictions': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp]),
     'kmp_mean_predict_maps': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vpp, _vp]),
+    'kmp_mean_predict_maps_typed': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vpp, _vp]),
     'kmp_linear_predict': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     'kmp_pad': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i64p, _i64p, _i32, _vp, _vp]),
     'kmp_copy_box': (ctypes.c_int, [_i32, _i32, _vp, _i64p, _i64p, _i32, _vp, _i64p, _i64p, _i64, _i64, _i64p,

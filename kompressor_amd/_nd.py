@@ -231,17 +231,25 @@ def d_maps_from_predictions(preds, nsp):
     return tuple(outs)
 
 
-def d_mean_predict_maps(window, padding, nsp):
+def d_mean_predict_maps(window, padding, nsp, out_dtype=None):
+    """The mean predictor's 7 (3) maps of a padded lowres window, in the sample dtype or (out_dtype
+    torch.float32) as float32 maps written by the kernel itself -- the shape of a network's output.
+    Windows the float32 kernels do not take (2D, C > 1) convert the sample-dtype maps on the device."""
     S = _sp(window.shape, nsp)
     cells = [s - 2 * padding - 1 for s in S]
     _require(all(c >= 1 for c in cells), 'window has no cells')
     ch = _ch(window.shape, nsp)
-    outs = [dev.empty((window.shape[0], *[(c if p else c + 1) for c, p in zip(cells, par)], *ch), window.dtype)
+    od = window.dtype if out_dtype is None else out_dtype
+    _require(od in (window.dtype, torch.float32), 'maps dtype must be the sample dtype or float32')
+    outs = [dev.empty((window.shape[0], *[(c if p else c + 1) for c, p in zip(cells, par)], *ch), od)
             for par in PARITY[nsp]]
     if _empty_ok(window, *outs):
-        check(lib.kmp_mean_predict_maps(nsp, dev.dtype_code(window), window.data_ptr(), window.shape[0],
-                                        _lib.i64x3(S), _C(window.shape, nsp), padding, _lib.ptrs(outs),
-                                        dev.stream()), 'mean_predict_maps')
+        st = lib.kmp_mean_predict_maps_typed(nsp, dev.dtype_code(window), dev.dtype_code(outs[0]), window.data_ptr(),
+                                             window.shape[0], _lib.i64x3(S), _C(window.shape, nsp), padding,
+                                             _lib.ptrs(outs), dev.stream())
+        if st == _lib.KMP_ERR_UNSUPPORTED and od != window.dtype:
+            return tuple(m.to(od) for m in d_mean_predict_maps(window, padding, nsp))
+        check(st, 'mean_predict_maps')
     return tuple(outs)
 
 

@@ -598,18 +598,18 @@ __device__ __forceinline__ RowMap row_map(int32_t W) {
 // ox < Lcx go through the row mapping in x chunks of <= 64; the last column (ox == Lcx, where
 // only the three maps with an even x parity exist and only the cells at ox - 1 contribute) is a
 // separate pass with one lane per row.
-template <typename T>
+template <typename T, typename O>
 __device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t oz, int64_t b, int32_t Lcz,
                                                 int32_t Lcy, int32_t Lcx, const MapPtrs& outs, int s_cur, int s_prev) {
   const int32_t nplanes = Lcz + 1, oyn = Lcy + 1, oxn = Lcx + 1, cplane = Lcy * Lcx;
   const bool z0 = oz < Lcz, z1 = oz >= 1;  // cell planes oz and oz - 1 exist
-  T* const o0 = (T*)outs.p[0] + ((b * Lcz + oz) * Lcy) * oxn;       // LR (1,1,0)
-  T* const o1 = (T*)outs.p[1] + ((b * Lcz + oz) * oyn) * Lcx;       // UD (1,0,1)
-  T* const o2 = (T*)outs.p[2] + ((b * nplanes + oz) * Lcy) * Lcx;   // FB (0,1,1)
-  T* const o3 = (T*)outs.p[3] + ((b * Lcz + oz) * Lcy) * Lcx;       // C  (1,1,1)
-  T* const o4 = (T*)outs.p[4] + ((b * Lcz + oz) * oyn) * oxn;       // Z  (1,0,0)
-  T* const o5 = (T*)outs.p[5] + ((b * nplanes + oz) * Lcy) * oxn;   // Y  (0,1,0)
-  T* const o6 = (T*)outs.p[6] + ((b * nplanes + oz) * oyn) * Lcx;   // X  (0,0,1)
+  O* const o0 = (O*)outs.p[0] + ((b * Lcz + oz) * Lcy) * oxn;       // LR (1,1,0)
+  O* const o1 = (O*)outs.p[1] + ((b * Lcz + oz) * oyn) * Lcx;       // UD (1,0,1)
+  O* const o2 = (O*)outs.p[2] + ((b * nplanes + oz) * Lcy) * Lcx;   // FB (0,1,1)
+  O* const o3 = (O*)outs.p[3] + ((b * Lcz + oz) * Lcy) * Lcx;       // C  (1,1,1)
+  O* const o4 = (O*)outs.p[4] + ((b * Lcz + oz) * oyn) * oxn;       // Z  (1,0,0)
+  O* const o5 = (O*)outs.p[5] + ((b * nplanes + oz) * Lcy) * oxn;   // Y  (0,1,0)
+  O* const o6 = (O*)outs.p[6] + ((b * nplanes + oz) * oyn) * Lcx;   // X  (0,0,1)
   const uint32_t* cur = cells + s_cur * cplane;
   const uint32_t* prev = cells + s_prev * cplane;
   const uint32_t nz = (uint32_t)z0 + z1;
@@ -635,17 +635,17 @@ __device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t o
       const uint32_t c110 = prev[q - Lcx] & (mz1 & my1);
       const uint32_t nx = 1u + x1, ny = (uint32_t)y0 + y1;
       const int32_t px = oy * oxn + ox, pc = oy * Lcx + ox;
-      o6[pc] = (T)((c000 + c010 + c110 + c100) >> ((nz * ny) >> 1));
+      o6[pc] = (O)((c000 + c010 + c110 + c100) >> ((nz * ny) >> 1));
       if (z0) {
-        o1[pc] = (T)((c000 + c010) >> (ny >> 1));
-        o4[px] = (T)((c000 + c001 + c011 + c010) >> ((ny * nx) >> 1));
+        o1[pc] = (O)((c000 + c010) >> (ny >> 1));
+        o4[px] = (O)((c000 + c001 + c011 + c010) >> ((ny * nx) >> 1));
       }
       if (y0) {
-        o2[pc] = (T)((c000 + c100) >> (nz >> 1));
-        o5[px] = (T)((c000 + c001 + c101 + c100) >> ((nz * nx) >> 1));
+        o2[pc] = (O)((c000 + c100) >> (nz >> 1));
+        o5[px] = (O)((c000 + c001 + c101 + c100) >> ((nz * nx) >> 1));
         if (z0) {
-          o0[px] = (T)((c000 + c001) >> (nx >> 1));
-          o3[pc] = (T)c000;
+          o0[px] = (O)((c000 + c001) >> (nx >> 1));
+          o3[pc] = (O)c000;
         }
       }
     }
@@ -658,10 +658,10 @@ __device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t o
     const uint32_t c101 = prev[q] & (z1 && y0 ? ~0u : 0u);
     const uint32_t ny = (uint32_t)y0 + y1;
     const int32_t px = oy * oxn + Lcx;
-    if (z0) o4[px] = (T)((c001 + c011) >> (ny >> 1));
+    if (z0) o4[px] = (O)((c001 + c011) >> (ny >> 1));
     if (y0) {
-      o5[px] = (T)((c001 + c101) >> (nz >> 1));
-      if (z0) o0[px] = (T)c001;
+      o5[px] = (O)((c001 + c101) >> (nz >> 1));
+      if (z0) o0[px] = (O)c001;
     }
   }
 }
@@ -679,7 +679,7 @@ __device__ __forceinline__ void mean_maps_plane(const uint32_t* cells, int32_t o
 // PPB output planes per workgroup (1 or 2): with 2, the cell plane between them is summed once
 // for both (3 cell planes for 2 outputs instead of 4) -- the kernel is VALU-bound
 // (profiles/round2/sq_callback_kernels.txt)
-template <typename T, int P, int PPB>
+template <typename T, int P, int PPB, typename O = T>
 __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
     const T* __restrict__ win, E3<int32_t> S, int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs, int32_t xcd_per,
     int32_t nodes_bytes, int32_t xs_bytes) {
@@ -762,8 +762,180 @@ __global__ void __launch_bounds__(kThreads) mean_predict_plane_kernel(
   }
   __syncthreads();
 
-  mean_maps_plane<T>(cells, oz, b, Lcz, Lcy, Lcx, outs, 1, 0);
-  if (PPB == 2 && oz + 1 < nplanes) mean_maps_plane<T>(cells, oz + 1, b, Lcz, Lcy, Lcx, outs, 2, 1);
+  mean_maps_plane<T, O>(cells, oz, b, Lcz, Lcy, Lcx, outs, 1, 0);
+  if (PPB == 2 && oz + 1 < nplanes) mean_maps_plane<T, O>(cells, oz + 1, b, Lcz, Lcy, Lcx, outs, 2, 1);
+}
+
+// ---- p = 0, eight x positions per lane (3D, C == 1, Lcx % 8 == 0) ----
+// The same maps as mean_predict_plane_kernel<T, 0, *> with the per-position work cut to adds and
+// shifts: the LDS cell planes carry a zero border (row -1 / Lcy, column -1, whole planes -1 /
+// Lcz), so a cell that does not exist reads 0 and no read is masked, and each map is a sum of the
+// existing cells shifted by log2 of their count (the per-axis flags sz, sy, sx below).  A lane
+// owns 8 consecutive x of one row: 2 x 16-byte node-row loads per cell row, 2 ds_read_b128 + 1
+// ds_read_b32 per cell row read, one 8-element store per map.  A workgroup computes ZP output
+// planes from ZP + 1 cell planes (cell plane oz - 1 is summed by two workgroups).
+
+typedef uint32_t u32x2u __attribute__((ext_vector_type(2), aligned(1)));
+
+// nodes p[0 .. 8] of a window row (unaligned: rows of odd length)
+template <typename T>
+__device__ __forceinline__ void load_row9(const T* p, uint32_t (&n)[9]) {
+  if constexpr (sizeof(T) == 2) {
+    const u32x4u v = *(const u32x4u*)p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      n[2 * k] = v[k] & 0xFFFFu;
+      n[2 * k + 1] = v[k] >> 16;
+    }
+  } else {
+    const u32x2u v = *(const u32x2u*)p;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) n[4 * k + i] = (v[k] >> (8 * i)) & 0xFFu;
+  }
+  n[8] = p[8];
+}
+
+// 8 map values (each < 2^(8 sizeof(T))) as O at p (element-aligned)
+template <typename O>
+__device__ __forceinline__ void store_row8(O* p, const uint32_t (&v)[8]) {
+  if constexpr (std::is_same<O, float>::value) {
+    u32x4u a, b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = __float_as_uint((float)v[k]);
+      b[k] = __float_as_uint((float)v[4 + k]);
+    }
+    *(u32x4u*)p = a;
+    *(u32x4u*)(p + 4) = b;
+  } else if constexpr (sizeof(O) == 2) {
+    u32x4u a;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = v[2 * k] | (v[2 * k + 1] << 16);
+    *(u32x4u*)p = a;
+  } else {
+    u32x2u a;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) a[k] = v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24);
+    *(u32x2u*)p = a;
+  }
+}
+
+// words of one LDS cell plane: rows -1 .. Lcy, pitch Lcx + 8 (cell x at word x + 4: 16-byte aligned)
+__host__ __device__ __forceinline__ int32_t mp8_plane_words(int32_t Lcy, int32_t Lcx) { return (Lcy + 2) * (Lcx + 8); }
+
+template <typename T, typename O>
+__global__ void __launch_bounds__(kThreads) mean_predict_p0x8_kernel(const T* __restrict__ win, E3<int32_t> S,
+                                                                    int32_t Lcz, int32_t Lcy, int32_t Lcx, MapPtrs outs,
+                                                                    int32_t xcd_per, int32_t ZP, int32_t ngrp) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cl[];  // [ZP + 1][Lcy + 2][Lcx + 8]
+  int32_t blk = (int32_t)blockIdx.x;
+  if (xcd_per > 0) {  // the groups of one window on one XCD (their shared node planes hit its L2)
+    const int32_t x = blk % 8, k = blk / 8;
+    blk = ((k / xcd_per) * 8 + x) * xcd_per + (k % xcd_per);
+  }
+  const int32_t b = blk / ngrp, z0 = (blk - b * ngrp) * ZP;  // output planes z0 .. z0 + ZP - 1
+  const int32_t RP = Lcx + 8, PW = mp8_plane_words(Lcy, Lcx), NJ = Lcx >> 3;
+  const int32_t S1 = S.e[1], S2 = S.e[2];
+
+  // zero border (and the planes outside the window's cells)
+  for (int32_t i = threadIdx.x; i < (ZP + 1) * PW / 4; i += kThreads) ((uint4*)cl)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  // cell planes zc = z0 - 1 + s: 8 cells per lane = (8 nodes) >> 3, summed over 4 node rows
+  const float rnj = 1.0f / (float)NJ, rlcy = 1.0f / (float)Lcy;
+  for (int32_t t = threadIdx.x; t < (ZP + 1) * Lcy * NJ; t += kThreads) {
+    int32_t sy, j, s, cy;
+    divmod_small(t, NJ, rnj, sy, j);
+    divmod_small(sy, Lcy, rlcy, s, cy);
+    const int32_t zc = z0 - 1 + s;
+    if (zc < 0 || zc >= Lcz) continue;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        uint32_t n[9];
+        load_row9<T>(win + (((int64_t)b * S.e[0] + zc + dz) * S1 + cy + dy) * S2 + 8 * j, n);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += n[i] + n[i + 1];
+      }
+    uint32_t* dst = cl + s * PW + (cy + 1) * RP + 4 + 8 * j;
+    *(uint4*)dst = make_uint4(acc[0] >> 3, acc[1] >> 3, acc[2] >> 3, acc[3] >> 3);
+    *(uint4*)(dst + 4) = make_uint4(acc[4] >> 3, acc[5] >> 3, acc[6] >> 3, acc[7] >> 3);
+  }
+  __syncthreads();
+
+  const int32_t nz = Lcz + 1 - z0 < ZP ? Lcz + 1 - z0 : ZP;  // output planes of this group
+  const int32_t oyn = Lcy + 1, oxn = Lcx + 1;
+  const float roy = 1.0f / (float)oyn;
+  // cells x = 8j - 1 .. 8j + 7 of one LDS row
+  auto row9 = [&](const uint32_t* r, int32_t j, uint32_t (&v)[9]) {
+    v[0] = r[3 + 8 * j];
+    const uint4 a = *(const uint4*)(r + 4 + 8 * j), c = *(const uint4*)(r + 8 + 8 * j);
+    v[1] = a.x; v[2] = a.y; v[3] = a.z; v[4] = a.w;
+    v[5] = c.x; v[6] = c.y; v[7] = c.z; v[8] = c.w;
+  };
+  for (int32_t t = threadIdx.x; t < nz * oyn * NJ; t += kThreads) {
+    int32_t py, j, pz, oy;
+    divmod_small(t, NJ, rnj, py, j);
+    divmod_small(py, oyn, roy, pz, oy);
+    const int32_t oz = z0 + pz, ox = 8 * j;
+    const bool z0f = oz < Lcz, y0f = oy < Lcy;
+    const uint32_t sz = (uint32_t)(z0f && oz >= 1), sy = (uint32_t)(y0f && oy >= 1);
+    const uint32_t* cur = cl + (pz + 1) * PW;  // cell plane oz
+    const uint32_t* prv = cl + pz * PW;        // cell plane oz - 1
+    uint32_t a[9], bb[9], c[9], d[9];          // cur row oy, cur row oy - 1, prev row oy, prev row oy - 1
+    row9(cur + (oy + 1) * RP, j, a);
+    row9(cur + oy * RP, j, bb);
+    row9(prv + (oy + 1) * RP, j, c);
+    row9(prv + oy * RP, j, d);
+    uint32_t m0[8], m1[8], m2[8], m3[8], m4[8], m5[8], m6[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t sx = i > 0 ? 1u : (uint32_t)(ox >= 1);
+      const uint32_t lr = a[i + 1] + a[i];
+      m0[i] = lr >> sx;                                          // LR (1,1,0)
+      m1[i] = (a[i + 1] + bb[i + 1]) >> sy;                      // UD (1,0,1)
+      m2[i] = (a[i + 1] + c[i + 1]) >> sz;                       // FB (0,1,1)
+      m3[i] = a[i + 1];                                          // C  (1,1,1)
+      m4[i] = (lr + bb[i] + bb[i + 1]) >> (sy + sx);             // Z  (1,0,0)
+      m5[i] = (lr + c[i] + c[i + 1]) >> (sz + sx);               // Y  (0,1,0)
+      m6[i] = (a[i + 1] + bb[i + 1] + c[i + 1] + d[i + 1]) >> (sz + sy);  // X (0,0,1)
+    }
+    const int32_t zL = b * Lcz + oz, zN = b * (Lcz + 1) + oz;  // plane index in a map of Lcz / Lcz + 1 planes
+    store_row8<O>((O*)outs.p[6] + (zN * oyn + oy) * Lcx + ox, m6);
+    if (z0f) {
+      store_row8<O>((O*)outs.p[1] + (zL * oyn + oy) * Lcx + ox, m1);
+      store_row8<O>((O*)outs.p[4] + (zL * oyn + oy) * oxn + ox, m4);
+    }
+    if (y0f) {
+      store_row8<O>((O*)outs.p[2] + (zN * Lcy + oy) * Lcx + ox, m2);
+      store_row8<O>((O*)outs.p[5] + (zN * Lcy + oy) * oxn + ox, m5);
+      if (z0f) {
+        store_row8<O>((O*)outs.p[0] + (zL * Lcy + oy) * oxn + ox, m0);
+        store_row8<O>((O*)outs.p[3] + (zL * Lcy + oy) * Lcx + ox, m3);
+      }
+    }
+  }
+  // the last column, ox = Lcx: LR, Z, Y from the cells at x = Lcx - 1
+  for (int32_t t = threadIdx.x; t < nz * oyn; t += kThreads) {
+    int32_t pz, oy;
+    divmod_small(t, oyn, roy, pz, oy);
+    const int32_t oz = z0 + pz;
+    const bool z0f = oz < Lcz, y0f = oy < Lcy;
+    const uint32_t sz = (uint32_t)(z0f && oz >= 1), sy = (uint32_t)(y0f && oy >= 1);
+    const uint32_t* cur = cl + (pz + 1) * PW + 3 + Lcx;  // x = Lcx - 1
+    const uint32_t* prv = cl + pz * PW + 3 + Lcx;
+    const uint32_t c001 = cur[(oy + 1) * RP], c011 = cur[oy * RP], c101 = prv[(oy + 1) * RP];
+    const int32_t zL = b * Lcz + oz, zN = b * (Lcz + 1) + oz;
+    if (z0f) ((O*)outs.p[4])[(zL * oyn + oy) * oxn + Lcx] = (O)((c001 + c011) >> sy);
+    if (y0f) {
+      ((O*)outs.p[5])[(zN * Lcy + oy) * oxn + Lcx] = (O)((c001 + c101) >> sz);
+      if (z0f) ((O*)outs.p[0])[(zL * Lcy + oy) * oxn + Lcx] = (O)c001;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1377,9 +1549,13 @@ int kmp_maps_from_predictions(int32_t nsp, int32_t dtype, const void* preds, int
   });
 }
 
-int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],
-                          int64_t C, int32_t padding, void* const out[7], kmp_stream_t stream) {
+// out_dtype: the maps' dtype -- the sample dtype, or KMP_F32 (a network-shaped predictor's
+// float32 output; the values are the same integers) on the 3D C == 1 LDS kernels.
+static int mean_predict_maps_impl(int32_t nsp, int32_t dtype, int32_t out_dtype, const void* padded_lowres, int64_t B,
+                                  const int64_t shape[3], int64_t C, int32_t padding, void* const out[7],
+                                  kmp_stream_t stream) {
   if (int s = check_common(nsp, B, shape, C)) return s;
+  KMP_REQUIRE(out_dtype == dtype || out_dtype == KMP_F32, "map dtype must be the sample dtype or float32");
   KMP_REQUIRE(padded_lowres && out && padding >= 0, "null pointer or negative padding");
   Ext3 S = ext_from(nsp, shape);
   MapPtrs outs{};
@@ -1422,8 +1598,39 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
       }
       const int64_t ngrp = ceil_div(cells.e[0] + 1, (int64_t)ppb);
       const int64_t nblk_plane = B * ngrp;
+      const bool f32 = out_dtype == KMP_F32 && !std::is_same<T, float>::value;
+      // p = 0, Lcx % 8 == 0: eight x positions per lane (mean_predict_p0x8_kernel), ZP = 3 output
+      // planes per workgroup (4 cell planes); 32-bit map offsets
+      const int64_t zp8 = std::min<int64_t>(3, cells.e[0] + 1), ngrp8 = ceil_div(cells.e[0] + 1, zp8);
+      const int64_t lds8 = 4 * (zp8 + 1) * mp8_plane_words((int32_t)std::min<int64_t>(cells.e[1], 1 << 20),
+                                                           (int32_t)std::min<int64_t>(cells.e[2], 1 << 20));
+      if (nsp == 3 && C == 1 && padding == 0 && cells.e[2] % 8 == 0 && lds8 <= 64 * 1024 &&
+          B * (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31) &&
+          B * ngrp8 < ((int64_t)1 << 31) && (zp8 + 1) * cells.e[1] * (cells.e[2] / 8) < ((int64_t)1 << 21)) {
+        auto kern = f32 ? mean_predict_p0x8_kernel<T, float> : mean_predict_p0x8_kernel<T, T>;
+        kern<<<(unsigned)(B * ngrp8), kThreads, (size_t)lds8, (hipStream_t)stream>>>(
+            (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2], outs,
+            B % 8 == 0 ? (int32_t)ngrp8 : 0, (int32_t)zp8, (int32_t)ngrp8);
+        return check_launch("mean_predict_p0x8");
+      }
       if (nsp == 3 && C == 1 && padding <= 2 && lds_plane <= 64 * 1024 && nblk_plane < ((int64_t)1 << 31) &&
           (cells.e[0] + 1) * (cells.e[1] + 1) * (cells.e[2] + 1) < ((int64_t)1 << 31)) {
+        if (f32) {
+          auto launch = [&](auto kern) {
+            kern<<<(unsigned)nblk_plane, kThreads, (size_t)lds_plane, (hipStream_t)stream>>>(
+                (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2],
+                outs, B % 8 == 0 ? (int32_t)ngrp : 0, (int32_t)nodes_bytes, (int32_t)xs_bytes);
+            return check_launch(ppb == 2 ? "mean_predict_plane2" : "mean_predict_plane");
+          };
+          if (ppb == 2) {
+            if (padding == 0) return launch(mean_predict_plane_kernel<T, 0, 2, float>);
+            if (padding == 1) return launch(mean_predict_plane_kernel<T, 1, 2, float>);
+            return launch(mean_predict_plane_kernel<T, 2, 2, float>);
+          }
+          if (padding == 0) return launch(mean_predict_plane_kernel<T, 0, 1, float>);
+          if (padding == 1) return launch(mean_predict_plane_kernel<T, 1, 1, float>);
+          return launch(mean_predict_plane_kernel<T, 2, 1, float>);
+        }
         auto launch = [&](auto kern) {
           kern<<<(unsigned)nblk_plane, kThreads, (size_t)lds_plane, (hipStream_t)stream>>>(
               (const T*)padded_lowres, e32(S), (int32_t)cells.e[0], (int32_t)cells.e[1], (int32_t)cells.e[2], outs,
@@ -1439,6 +1646,7 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
         if (padding == 1) return launch(mean_predict_plane_kernel<T, 1, 1>);
         return launch(mean_predict_plane_kernel<T, 2, 1>);
       }
+      if (f32) return fail(KMP_ERR_UNSUPPORTED, "mean_predict_maps: float32 maps need the 3D C == 1 LDS kernels");
       if (rows_ok(C, {vol(B, S, C), total}) && padding <= 1) {
         const int32_t XO = (int32_t)std::min<int64_t>(cells.e[2] + 1, 64);
         const int32_t YB = std::max(1, std::min(8, kThreads / XO));
@@ -1458,6 +1666,7 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
         return check_launch("mean_predict_maps");
       }
     }
+    if (out_dtype != dtype) return fail(KMP_ERR_UNSUPPORTED, "mean_predict_maps: float32 maps of this window");
     int st = with_index(small, [&](auto itag) {
       using I = decltype(itag);
       cell_mean_map_kernel<T, I><<<grid_for(ncell), kThreads, 0, (hipStream_t)stream>>>(
@@ -1479,6 +1688,17 @@ int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres,
     }
     return check_launch("mean_predict_maps");
   });
+}
+
+int kmp_mean_predict_maps(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],
+                          int64_t C, int32_t padding, void* const out[7], kmp_stream_t stream) {
+  return mean_predict_maps_impl(nsp, dtype, dtype, padded_lowres, B, shape, C, padding, out, stream);
+}
+
+int kmp_mean_predict_maps_typed(int32_t nsp, int32_t dtype, int32_t out_dtype, const void* padded_lowres, int64_t B,
+                                const int64_t shape[3], int64_t C, int32_t padding, void* const out[7],
+                                kmp_stream_t stream) {
+  return mean_predict_maps_impl(nsp, dtype, out_dtype, padded_lowres, B, shape, C, padding, out, stream);
 }
 
 int kmp_pad(int32_t nsp, int32_t dtype, const void* in, int64_t B, const int64_t shape[3], int64_t C,

@@ -22,24 +22,34 @@ from ._lib import check, lib
 
 
 class MeanPredictor:
-    """``maps_from_predictions(repeat(astype(mean(features_from_lowres(x, p)), dtype)))``."""
+    """``maps_from_predictions(repeat(astype(mean(features_from_lowres(x, p)), dtype)))``.
 
-    def __init__(self, padding=0, ndim=3):
+    ``maps_dtype=None`` returns the maps in the sample dtype (the reference test predictor);
+    ``maps_dtype=float32`` returns the same values as float32 maps, written by the kernel -- the
+    shape of a trained network's output, which the coders read as int32 (utils.py:38-55)."""
+
+    def __init__(self, padding=0, ndim=3, maps_dtype=None):
         if ndim not in (2, 3):
             raise ValueError('ndim must be 2 (image) or 3 (volume)')
         if not isinstance(padding, int) or padding < 0:
             raise ValueError('padding must be an int >= 0')
+        if maps_dtype is not None and maps_dtype is not torch.float32 and (
+                isinstance(maps_dtype, torch.dtype) or np.dtype(maps_dtype) != np.float32):
+            raise ValueError('maps_dtype must be None (the sample dtype) or float32')
         self.padding, self.ndim = padding, ndim
+        self.maps_dtype = None if maps_dtype is None else torch.float32
 
     def _kmp_predictor(self):
         return _lib.Predictor(_lib.PRED_MEAN, self.padding, None, None)
 
     def __call__(self, lowres):
         t, kind = dev.to_device(lowres)
-        return tuple(dev.from_device(m, kind) for m in d_mean_predict_maps(t, self.padding, self.ndim))
+        return tuple(dev.from_device(m, kind) for m in d_mean_predict_maps(t, self.padding, self.ndim,
+                                                                          self.maps_dtype))
 
     def __repr__(self):
-        return f'MeanPredictor(padding={self.padding}, ndim={self.ndim})'
+        md = '' if self.maps_dtype is None else ', maps_dtype=float32'
+        return f'MeanPredictor(padding={self.padding}, ndim={self.ndim}{md})'
 
 
 class LinearPredictor:

@@ -147,9 +147,11 @@ def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
     window = oracle.volume.pad_neighborhood(lo, padding)
     want = oracle.predictors.mean_predictions_fn(padding, 3)(window)
     two = _mp_lds_bytes(window.shape, window.itemsize, padding, 2) <= 64 * 1024
+    x8 = padding == 0 and (window.shape[3] - 1) % 8 == 0  # p = 0, cell rows of 8k: mean_predict_p0x8
     runs = {}
-    for env, val, name in ((None, None, 'mean_predict_plane2' if two else 'mean_predict_plane'),
-                           ('KMP_MP_PPB', '1', 'mean_predict_plane')):
+    for env, val, name in ((None, None, 'mean_predict_p0x8' if x8 else 'mean_predict_plane2' if two
+                            else 'mean_predict_plane'),
+                           ('KMP_MP_PPB', '1', 'mean_predict_p0x8' if x8 else 'mean_predict_plane')):
         if env:
             os.environ[env] = val
         try:
@@ -161,6 +163,43 @@ def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
     for key, got in runs.items():
         for a, b in zip(got, want):
             _eq(a, b)
+
+
+@pytest.mark.parametrize('wshape,dtype', [((2, 33, 33, 33, 1), np.uint16),  # the C3 callback window
+                                          ((3, 9, 17, 9, 1), np.uint8),
+                                          ((8, 5, 3, 17, 1), np.uint16),    # B % 8 == 0, last group of 2 planes
+                                          ((1, 2, 2, 9, 1), np.uint16),     # one cell
+                                          ((16, 4, 9, 25, 1), np.uint8)])
+@pytest.mark.parametrize('fill', ['rand', 'max'])
+def test_mean_predictor_p0x8_kernel(kom, wshape, dtype, fill):
+    """p = 0 windows whose cell rows are a multiple of 8 long take the eight-positions-per-lane kernel
+    ('mean_predict_p0x8'); its maps, in the sample dtype and as float32, equal the oracle's."""
+    window = _rand(wshape, dtype, 3) if fill == 'rand' else np.full(wshape, np.iinfo(dtype).max, dtype)
+    want = oracle.predictors.mean_predictions_fn(0, 3)(window)
+    got = kom.MeanPredictor(0, 3)(torch.from_numpy(window).cuda())
+    assert kom._lib.lib.kmp_last_launch().decode() == 'mean_predict_p0x8'
+    for a, b in zip(got, want):
+        _eq(a, b)
+    got = kom.MeanPredictor(0, 3, maps_dtype=torch.float32)(torch.from_numpy(window).cuda())
+    assert kom._lib.lib.kmp_last_launch().decode() == 'mean_predict_p0x8'
+    for a, b in zip(got, want):
+        _eq(a, b.astype(np.float32))
+
+
+@pytest.mark.parametrize('ndim,padding', [(3, 1), (3, 2), (2, 0), (2, 1)])
+def test_mean_predictor_float32_maps(kom, ndim, padding):
+    """maps_dtype=float32 on the per-plane kernel (3D, p >= 1: the kernel writes float32) and on
+    image windows (converted on the device): the sample-dtype maps' values as float32."""
+    ns, ons = _pair(kom, ndim)
+    hi = _rand((2, 20, 18, 22, 1) if ndim == 3 else (2, 20, 18, 1), np.uint16, 9)
+    window = ons.pad_neighborhood(ons.lowres_from_highres(ons.pad_highres(hi)[0]), padding)
+    want = oracle.predictors.mean_predictions_fn(padding, ndim)(window)
+    got = kom.MeanPredictor(padding, ndim, maps_dtype=np.float32)(torch.from_numpy(window).cuda())
+    if ndim == 3:
+        assert kom._lib.lib.kmp_last_launch().decode().startswith('mean_predict_plane')
+    for a, b in zip(got, want):
+        assert a.dtype == torch.float32
+        _eq(a, b.astype(np.float32))
 
 
 @pytest.mark.parametrize('ndim', [3, 2])

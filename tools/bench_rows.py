@@ -170,19 +170,27 @@ def main():
             del lo, maps
 
     # the callback path with float32 prediction maps (a network's output; the coder reads int32(pred)):
-    # the fused coder reads them directly (kmp_*_with_predictions_typed); '_steps' is the same call with
-    # an opaque coder, i.e. the reference's step sequence (what float32 maps ran as before)
+    # the stand-in writes float32 maps itself (MeanPredictor(maps_dtype=float32), one launch, as a
+    # network's last layer would) and the fused coder reads them directly
+    # (kmp_*_with_predictions_typed); '_cast' is the round-2 stand-in (sample-dtype maps + 7 torch
+    # .float() conversions, 47 us each); '_steps' the same call with an opaque coder, i.e. the
+    # reference's step sequence
     if not want or 'volume_callback_f32' in want:
+        pred32 = kom.MeanPredictor(0, 3, maps_dtype=torch.float32)
         pred = kom.MeanPredictor(0, 3)
-        cbf = lambda lowres: [m.float() for m in pred(lowres)]  # noqa: E731
+        cbf = lambda lowres: pred32(lowres)  # noqa: E731
+        cbc = lambda lowres: [m.float() for m in pred(lowres)]  # noqa: E731
         encs, decs = V.encode_values_uint16, V.decode_values_uint16
-        for tag, enc, dec in (('volume_callback_f32', encs, decs),
-                              ('volume_callback_f32_steps', lambda a, b: encs(a, b), lambda a, b: decs(a, b))):
-            lo, (maps, dims) = V.encode(cbf, enc, vol)
-            assert torch.equal(V.decode(cbf, dec, lo, (maps, dims)), vol), tag
-            te = gpu_time(lambda: V.encode(cbf, enc, vol), args.reps)
-            td = gpu_time(lambda: V.decode(cbf, dec, lo, (maps, dims)), args.reps)
-            what = 'fused coder' if tag == 'volume_callback_f32' else "the reference's step sequence"
+        for tag, fn, enc, dec in (('volume_callback_f32', cbf, encs, decs),
+                                  ('volume_callback_f32_cast', cbc, encs, decs),
+                                  ('volume_callback_f32_steps', cbf, lambda a, b: encs(a, b), lambda a, b: decs(a, b))):
+            lo, (maps, dims) = V.encode(fn, enc, vol)
+            assert torch.equal(V.decode(fn, dec, lo, (maps, dims)), vol), tag
+            te = gpu_time(lambda: V.encode(fn, enc, vol), args.reps)
+            td = gpu_time(lambda: V.decode(fn, dec, lo, (maps, dims)), args.reps)
+            what = {'volume_callback_f32': 'predictor writes float32, fused coder',
+                    'volume_callback_f32_cast': 'sample-dtype maps + torch .float(), fused coder',
+                    'volume_callback_f32_steps': "the reference's step sequence"}[tag]
             emit(tag + ':encode', f'callback encode, 512 tiles, float32 prediction maps, {what}', vol.numel() * 4, te)
             emit(tag + ':decode', f'callback decode, 512 tiles, float32 prediction maps, {what}', vol.numel() * 4, td)
             del lo, maps

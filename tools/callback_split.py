@@ -1,6 +1,6 @@
 """The trained-network callback path at C3 (512 x 64^3 uint16), for a per-kernel rocprofv3 split
 (VERDICT r2 item 5): encode + decode with an opaque predictions_fn returning uint16 maps (the mean
-predictor's primitive) and returning float32 maps (a network's output).
+predictor's primitive) and returning float32 maps (a network's output: the stand-in writes them itself).
     rocprofv3 --kernel-trace --stats -d OUT -- python3 tools/callback_split.py [reps] [u16|f32|both]"""
 import os
 import sys
@@ -16,7 +16,8 @@ which = sys.argv[2] if len(sys.argv) > 2 else 'both'
 V = kom.volume
 vol = torch.from_numpy(np.random.default_rng(0).integers(0, 65536, size=(512, 64, 64, 64, 1)).astype(np.uint16)).cuda()
 pred = kom.MeanPredictor(0, 3)
-fns = {'u16': lambda lowres: pred(lowres), 'f32': lambda lowres: [m.float() for m in pred(lowres)]}
+pred32 = kom.MeanPredictor(0, 3, maps_dtype=torch.float32)
+fns = {'u16': lambda lowres: pred(lowres), 'f32': lambda lowres: pred32(lowres)}
 for name, fn in fns.items():
     if which not in (name, 'both'):
         continue
