@@ -208,7 +208,7 @@ struct CatRow {
   int64_t x;
 };
 
-template <typename T, int E4>
+template <typename T, int E4, bool FULL>
 __device__ __forceinline__ void cat_load(const float* __restrict__ logits, int64_t L, const T* __restrict__ x,
                                          int64_t el, int lane, CatRow<E4>& r) {
   const cat_f32x4* row = (const cat_f32x4*)(logits + el * L);
@@ -216,7 +216,7 @@ __device__ __forceinline__ void cat_load(const float* __restrict__ logits, int64
 #pragma unroll
   for (int s = 0; s < E4; ++s) {
     const int c4 = s * 64 + lane;
-    r.v[s] = 4 * c4 < L ? __builtin_nontemporal_load(row + c4) : (cat_f32x4){qnan, qnan, qnan, qnan};
+    r.v[s] = FULL || 4 * c4 < L ? __builtin_nontemporal_load(row + c4) : (cat_f32x4){qnan, qnan, qnan, qnan};
   }
   r.x = std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el];
 }
@@ -252,7 +252,7 @@ __device__ __forceinline__ uint64_t lanes_below(int nl) {  // mask of lanes 0 ..
   return nl <= 0 ? 0ull : nl >= 64 ? ~0ull : ((1ull << nl) - 1);
 }
 
-template <typename T, int DIR, int E4>
+template <typename T, int DIR, int E4, bool FULL>
 __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins, int peel,
                                          T* __restrict__ out, int64_t el) {
   if constexpr (DIR == KMP_ENCODE) {
@@ -301,13 +301,28 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
   } else {
     uint32_t key[E4][4];
     bool ok[E4][4];
+    // every logit in [+0, +inf] (softmax output, the reference's categorical predictor): the float
+    // bits are already order-preserving, and + 1 keeps key 0 for padding -- one add per key instead
+    // of order_key's six operations.  -0, negatives and NaN (bits above +inf) take order_key.
+    uint32_t mx = 0;
 #pragma unroll
     for (int s = 0; s < E4; ++s)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        ok[s][q] = s * 256 + 4 * lane + q < L;
-        key[s][q] = ok[s][q] ? order_key_fast(cur.v[s][q]) : 0u;  // padding keys 0: below every key
+        ok[s][q] = FULL || s * 256 + 4 * lane + q < L;
+        mx = max(mx, ok[s][q] ? __float_as_uint(cur.v[s][q]) : 0u);
       }
+    if (__ballot(mx > 0x7f800000u) == 0) {  // wave-uniform
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) key[s][q] = ok[s][q] ? __float_as_uint(cur.v[s][q]) + 1u : 0u;
+    } else {
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) key[s][q] = ok[s][q] ? order_key_fast(cur.v[s][q]) : 0u;  // padding keys 0
+    }
     auto count = [&](auto pred) {  // wave-uniform #{classes j with pred(key_j)}; pred(0) is false
       uint32_t c = 0;
 #pragma unroll
@@ -323,7 +338,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
     if ((int)k < peel) {
       uint32_t taken = 0;
       while (true) {
-        uint32_t best = 0;  // valid keys are > 0 (order_key of -inf is 0x007fffff)
+        uint32_t best = 0;  // valid keys are > 0 (order_key of -inf is 0x007fffff; the bits + 1 >= 1)
 #pragma unroll
         for (int s = 0; s < E4; ++s)
 #pragma unroll
@@ -397,7 +412,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
       m = k - c_hi;
     }
     // the m-th highest class index among the classes with key in [t, hi); padding keys (0) are
-    // below every valid key (>= 0x007fffff), so the range starts at 1 at the least
+    // below every valid key (>= 1), so the range starts at 1 at the least
     const uint32_t tlo = t > 0 ? t : 1u;
     int64_t cls = 0;
     for (int s = E4 - 1; s >= 0; --s) {
@@ -433,7 +448,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
   }
 }
 
-template <typename T, int DIR, int E4, int PF>
+template <typename T, int DIR, int E4, int PF, bool FULL>
 __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const float* __restrict__ logits, int64_t n,
                                                                           int64_t L, const T* __restrict__ x,
                                                                           T* __restrict__ out, int peel) {
@@ -447,7 +462,7 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
   CatRow<E4> ring[PF];
 #pragma unroll
   for (int u = 0; u < PF; ++u)
-    if (el0 + u * ws < n) cat_load<T, E4>(logits, L, x, el0 + u * ws, lane, ring[u]);
+    if (el0 + u * ws < n) cat_load<T, E4, FULL>(logits, L, x, el0 + u * ws, lane, ring[u]);
   for (int64_t base = el0; base < n; base += PF * ws) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -455,8 +470,8 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
       if (e >= n) break;
       const CatRow<E4> cur = ring[u];
       const int64_t ep = e + PF * ws;
-      if (ep < n) cat_load<T, E4>(logits, L, x, ep, lane, ring[u]);
-      cat_rank<T, DIR, E4>(cur, L, lane, bins, peel, out, e);
+      if (ep < n) cat_load<T, E4, FULL>(logits, L, x, ep, lane, ring[u]);
+      cat_rank<T, DIR, E4, FULL>(cur, L, lane, bins, peel, out, e);
     }
   }
 }
@@ -483,14 +498,16 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
     if (vec) {
       constexpr int PF = kCatPF;
       hipStream_t st = (hipStream_t)stream;
+      // FULL: L == 256 E4, no padding classes (no per-class masks)
+      auto go = [&](auto kern) { kern<<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel); };
       if (direction == KMP_ENCODE && L <= 256)
-        categorical_vec_kernel<T, KMP_ENCODE, 1, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+        L == 256 ? go(categorical_vec_kernel<T, KMP_ENCODE, 1, PF, true>) : go(categorical_vec_kernel<T, KMP_ENCODE, 1, PF, false>);
       else if (direction == KMP_ENCODE)
-        categorical_vec_kernel<T, KMP_ENCODE, 2, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+        L == 512 ? go(categorical_vec_kernel<T, KMP_ENCODE, 2, PF, true>) : go(categorical_vec_kernel<T, KMP_ENCODE, 2, PF, false>);
       else if (L <= 256)
-        categorical_vec_kernel<T, KMP_DECODE, 1, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+        L == 256 ? go(categorical_vec_kernel<T, KMP_DECODE, 1, PF, true>) : go(categorical_vec_kernel<T, KMP_DECODE, 1, PF, false>);
       else
-        categorical_vec_kernel<T, KMP_DECODE, 2, PF><<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel);
+        L == 512 ? go(categorical_vec_kernel<T, KMP_DECODE, 2, PF, true>) : go(categorical_vec_kernel<T, KMP_DECODE, 2, PF, false>);
       return check_launch("categorical_vec");
     }
     if (direction == KMP_ENCODE)

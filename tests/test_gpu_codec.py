@@ -396,6 +396,29 @@ def test_categorical_coder_vs_oracle(kom, vec):
         got = kom.utils.decode_categorical(lg, xg).cpu().numpy()
         want = oracle.common.decode_categorical(logits, x)
         assert np.array_equal(got, want), L
+    # non-negative logits (softmax output: the decode's raw-bits key path), with +0, +inf, ties, and
+    # rows that fall back to the order key (-0, a negative, NaN)
+    for L, dt in ((256, np.uint8), (512, np.uint16), (64, np.uint8), (300, np.uint16), (4, np.uint8),
+                  (260, np.uint8), (252, np.uint8)):
+        logits = rng.random((513, L)).astype(np.float32)
+        logits[::5] = np.exp(logits[::5] * 8) / np.exp(logits[::5] * 8).sum(axis=1, keepdims=True)
+        logits[1, :2] = [0.0, np.inf]
+        logits[2, :] = 0.0
+        logits[3, :3] = [-0.0, 0.0, 0.25]
+        logits[4, 1] = -1.0
+        logits[8, 2] = np.nan
+        logits[::9, L // 2] = logits[::9, 0]  # ties
+        x = rng.integers(0, min(L + 3, np.iinfo(dt).max), size=513).astype(dt)
+        x[::3] = rng.integers(0, min(L, 10), size=x[::3].size)
+        lg, xg = torch.from_numpy(logits).cuda(), torch.from_numpy(x).cuda()
+        if vec == '0':
+            buf = torch.empty(logits.size + 4, dtype=torch.float32, device='cuda')
+            lg = buf[1:1 + logits.size].view(logits.shape)
+            lg.copy_(torch.from_numpy(logits))
+        assert np.array_equal(kom.utils.encode_categorical(lg, xg).cpu().numpy(),
+                              oracle.common.encode_categorical(logits, x)), L
+        assert np.array_equal(kom.utils.decode_categorical(lg, xg).cpu().numpy(),
+                              oracle.common.decode_categorical(logits, x)), L
 
 
 @pytest.mark.parametrize('shape,dtype,p', [
