@@ -80,6 +80,28 @@ def _median_rate(fn, nbytes, reps=5):
     return nbytes / t / 1e9, t
 
 
+def host_cores():
+    """The host cores this process may run on: the affinity mask, capped by a cgroup CPU quota
+    when one is set (cgroup v2 ``cpu.max``, else v1 ``cpu.cfs_quota_us``).  Returns (cores, how)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = -(-int(q) // int(per))
+    except (OSError, ValueError):
+        try:
+            q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+            per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            if q > 0:
+                quota = -(-q // per)
+        except (OSError, ValueError):
+            pass
+    if quota is not None and quota < aff:
+        return quota, f'cgroup CPU quota {quota} of {aff} cores in the affinity mask'
+    return aff, f'the affinity mask ({aff} cores, no smaller cgroup CPU quota)'
+
+
 def cpu_baseline(spec, host, padding, ntiles_numpy=0, ntiles_torch=0):
     """The reference path on the host cores, on a bounded sample of the same workload
     (BASELINE.md §2): 1 warm-up + the median of 5 encode+decode rounds of
@@ -107,8 +129,13 @@ def cpu_baseline(spec, host, padding, ntiles_numpy=0, ntiles_torch=0):
         lo, e = TC.encode(host[:nt], padding, ndim)
         out['torch'] = TC.decode(lo, e, padding, ndim)
 
-    threads = torch.get_num_threads()
-    r_t, t_t = _median_rate(torch_round, host[:nt].nbytes)
+    threads, how = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        r_t, t_t = _median_rate(torch_round, host[:nt].nbytes)
+    finally:
+        torch.set_num_threads(prev)
     assert np.array_equal(out['torch'], host[:nt]), 'torch-CPU round trip failed'
     r_n, t_n = _median_rate(numpy_round, host[:nn].nbytes)
     assert np.array_equal(out['np'], host[:nn]), 'oracle round trip failed'
@@ -116,9 +143,7 @@ def cpu_baseline(spec, host, padding, ntiles_numpy=0, ntiles_torch=0):
     return {'value': round(r_t, 4), 'unit': 'GB/s', 'cores': threads, 'kind': 'port',
             'sample': f'{nt} of {n} {unit}: torch-CPU restatement of the reference path (oracle/torch_cpu.py, '
                       f'materialised features / predictions like the JAX path) on {threads} threads '
-                      f'(torch.get_num_threads() = the OMP_NUM_THREADS CPU share this GPU is allotted on the box; '
-                      f'the host exposes {len(os.sched_getaffinity(0))} cores shared by its 8 GPUs, and the '
-                      f'memory-bound op sequence gains 1.4x from 1 to 16 threads), '
+                      f'(every host core this process may use: {how}), '
                       f'1 warm-up + median of 5 encode+decode rounds, {t_t:.3f} s/round',
             'single_thread_numpy': {'value': round(r_n, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
                                     'sample': f'{nn} of {n} {unit}: numpy op-for-op restatement (oracle/), '
@@ -513,14 +538,19 @@ def main_stream(args):
             lo_t, enc_t = TC.encode(host32[:nt], args.padding, 3)
             out['torch'] = TC.decode(lo_t, enc_t, args.padding, 3)
 
-        r_t, t_t = _median_rate(torch_round, host32[:nt].nbytes)
+        threads, how = host_cores()
+        prev = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            r_t, t_t = _median_rate(torch_round, host32[:nt].nbytes)
+        finally:
+            torch.set_num_threads(prev)
         assert np.array_equal(out['torch'], host32[:nt])
         r_n, t_n = _median_rate(numpy_round, host32[:nn].nbytes)
         assert np.array_equal(out['np'], host32[:nn])
-        threads = torch.get_num_threads()
         base = {'value': round(r_t, 4), 'unit': 'GB/s', 'cores': threads, 'kind': 'port',
                 'sample': f'{nt} of {n} chunks of 128^3: torch-CPU restatement (oracle/torch_cpu.py, uint32 '
-                          f'bit-cast) on {threads} threads, 1 warm-up + median of 5, {t_t:.3f} s/round',
+                          f'bit-cast) on {threads} threads ({how}), 1 warm-up + median of 5, {t_t:.3f} s/round',
                 'single_thread_numpy': {'value': round(r_n, 4), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
                                         'sample': f'{nn} of {n} chunks, numpy restatement (oracle/), 1 thread, '
                                                   f'1 warm-up + median of 5, {t_n:.3f} s/round'}}

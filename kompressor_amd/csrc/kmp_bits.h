@@ -156,7 +156,9 @@ __device__ __forceinline__ void scatter_bytes(const uint32_t (&X)[Sw<W>::NP][2],
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false);
+  // bound_ctrl: a read past the row gives 0 (no copy of the old value; the move can fold into its
+  // consumer).  Every caller discards the lanes whose source lies past the row
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
 }
 
 // 8x8 BYTE transpose across lanes j = lane & 7 (row j = the lane's (lo, hi)): afterwards lane j

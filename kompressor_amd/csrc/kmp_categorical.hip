@@ -356,7 +356,12 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
         hi = wmax;
       }
     } else {
-      // the bits below the keys' common prefix: P of them; histogram digit = bits [sh, sh + 8)
+      // radix select on digits of up to 8 bits from the top of the bits in which the keys differ
+      // (P of them below the common prefix): per round a 256-bin LDS histogram of the digit over
+      // the keys in the current range [t, hi), a DPP scan over the bins (descending digit order:
+      // bin 255 - digit), the bin that holds rank k; the range narrows to that bin.  Stops when
+      // the bin holds one key or the digits run out (ties).  Two rounds isolate the key for
+      // softmax rows, whose first digit is mostly exponent bits (up to half the keys in one bin)
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[0][0]);  // class 0 exists
       uint32_t dif = 0;
 #pragma unroll
@@ -365,50 +370,49 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
         for (int q = 0; q < 4; ++q) dif |= ok[s][q] ? key[s][q] ^ k0 : 0u;
       dif = wave_or_dpp(dif);
       const int P = dif == 0 ? 0 : 32 - __clz((int)dif);
-      const int sh = P > 8 ? P - 8 : 0;
-      // bins in descending digit order: bin 255 - digit
-      *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
-      __builtin_amdgcn_wave_barrier();
+      int sh = P > 8 ? P - 8 : 0, wd = P - sh;  // digit = bits [sh, sh + wd)
+      t = P >= 32 ? 0u : (k0 >> P) << P;
+      uint32_t c_hi = 0;  // keys above the range
+      for (int round = 0;; ++round) {
+        *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t dm = (1u << wd) - 1u;
+        const uint32_t hm = sh + wd >= 32 ? 0u : ~0u << (sh + wd);  // the range: key & hm == t & hm
 #pragma unroll
-      for (int s = 0; s < E4; ++s)
+        for (int s = 0; s < E4; ++s)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (ok[s][q]) atomicAdd(bins + (255 - ((key[s][q] >> sh) & 255u)), 1u);
-      __builtin_amdgcn_wave_barrier();
-      const uint4 b = *(const uint4*)(bins + 4 * lane);
-      const uint32_t tot = b.x + b.y + b.z + b.w;
-      const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
-      const uint32_t base = incl - tot;
-      const uint64_t hit = __ballot(base <= k && k < incl);
-      const int ls = (int)__builtin_ctzll(hit);
-      // inside the lane: the bin whose cumulative range holds k
-      uint32_t c_hi = base, cnt = b.x, q = 0;
-      if (k >= c_hi + b.x) {
-        c_hi += b.x; cnt = b.y; q = 1;
-        if (k >= c_hi + b.y) {
-          c_hi += b.y; cnt = b.z; q = 2;
-          if (k >= c_hi + b.z) { c_hi += b.z; cnt = b.w; q = 3; }
+          for (int q = 0; q < 4; ++q)
+            if (ok[s][q] && (round == 0 || ((key[s][q] ^ t) & hm) == 0))
+              atomicAdd(bins + (255 - ((key[s][q] >> sh) & dm)), 1u);
+        __builtin_amdgcn_wave_barrier();
+        const uint4 b = *(const uint4*)(bins + 4 * lane);
+        const uint32_t tot = b.x + b.y + b.z + b.w;
+        const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
+        const uint32_t base = incl - tot;
+        const uint32_t r = k - c_hi;
+        const uint64_t hit = __ballot(base <= r && r < incl);
+        const int ls = (int)__builtin_ctzll(hit);
+        // inside the lane: the bin whose cumulative range holds r
+        uint32_t cb = base, cnt = b.x, q = 0;
+        if (r >= cb + b.x) {
+          cb += b.x; cnt = b.y; q = 1;
+          if (r >= cb + b.y) {
+            cb += b.y; cnt = b.z; q = 2;
+            if (r >= cb + b.z) { cb += b.z; cnt = b.w; q = 3; }
+          }
         }
+        c_hi += (uint32_t)__builtin_amdgcn_readlane((int)cb, ls);
+        cnt = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ls);
+        q = (uint32_t)__builtin_amdgcn_readlane((int)q, ls);
+        const uint32_t digit = (255u - (uint32_t)(4 * ls + (int)q)) & dm;
+        t |= digit << sh;
+        if (cnt <= 1 || sh == 0) break;
+        const int nsh = sh > 8 ? sh - 8 : 0;
+        wd = sh - nsh;
+        sh = nsh;
+        __builtin_amdgcn_wave_barrier();  // the next round's zeroing must not overtake these reads
       }
-      c_hi = (uint32_t)__builtin_amdgcn_readlane((int)c_hi, ls);
-      cnt = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ls);
-      q = (uint32_t)__builtin_amdgcn_readlane((int)q, ls);
-      const uint32_t digit = 255u - (uint32_t)(4 * ls + (int)q);
-      const uint32_t top = sh + 8 >= 32 ? 0u : (k0 >> (sh + 8)) << (sh + 8);
-      t = top | (digit << sh);
       hi = (uint64_t)t + (1ull << sh);
-      uint32_t c_t = c_hi + cnt;
-      for (int bit = sh - 1; bit >= 0 && c_t - c_hi > 1; --bit) {
-        const uint32_t cand = t | (1u << bit);
-        const uint32_t c = count([&](uint32_t v) { return v >= cand; });
-        if (c >= k + 1) {
-          t = cand;
-          c_t = c;
-        } else {
-          hi = cand;
-          c_hi = c;
-        }
-      }
       m = k - c_hi;
     }
     // the m-th highest class index among the classes with key in [t, hi); padding keys (0) are

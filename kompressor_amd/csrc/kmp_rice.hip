@@ -64,18 +64,36 @@ __device__ __forceinline__ void zplanes(const uint32_t (&w)[Sw<W>::NW], uint32_t
   }
 }
 
-__device__ __forceinline__ uint32_t bytes_popcount(uint32_t v) {  // 4 byte-wise popcounts (each <= 8)
-  v = v - ((v >> 1) & 0x55555555u);
-  v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
-  return (v + (v >> 4)) & 0x0f0f0f0fu;
+// lane j of a block's 8-lane group ends with sum_{m=j..7} x_m 2^(m-j) (row_shl:d reads lane l+d;
+// a lane whose partner lies past the group adds nothing)
+__device__ __forceinline__ uint32_t group8_suffix2(uint32_t x, int j) {
+  uint32_t t = dpp<0x101>(x);
+  if (j < 7) x += t << 1;
+  t = dpp<0x102>(x);
+  if (j < 6) x += t << 2;
+  t = dpp<0x104>(x);
+  if (j < 4) x += t << 4;
+  return x;
 }
 
-// sum over the block's 8 lanes (every lane of the group ends with the total)
-__device__ __forceinline__ uint32_t group8_sum(uint32_t v, int lane) {
-  v += dpp<0xB1>(v);
-  v += dpp<0x4E>(v);
-  const uint32_t up = dpp<0x104>(v), dn = dpp<0x114>(v);  // full exec (see kmp_pack.hip widths_kernel)
-  return v + ((lane & 4) ? dn : up);
+// the value of the group's lane 0 / lane 7 on all its 8 lanes
+__device__ __forceinline__ uint32_t group8_first(uint32_t x, int j) {
+  const uint32_t t = dpp<0x00>(x);   // quad_perm [0,0,0,0]
+  const uint32_t u = dpp<0x114>(t);  // row_shr:4: lanes 4-7 take lane 0's
+  return (j & 4) ? u : t;
+}
+__device__ __forceinline__ uint32_t group8_last(uint32_t x, int j) {
+  const uint32_t t = dpp<0xFF>(x);   // quad_perm [3,3,3,3]
+  const uint32_t u = dpp<0x104>(t);  // row_shl:4: lanes 0-3 take lane 7's
+  return (j & 4) ? t : u;
+}
+
+// minimum over the group (every lane of the group ends with it)
+__device__ __forceinline__ uint32_t group8_min(uint32_t v, int j) {
+  v = min(v, dpp<0xB1>(v));
+  v = min(v, dpp<0x4E>(v));
+  const uint32_t up = dpp<0x104>(v), dn = dpp<0x114>(v);
+  return min(v, (j & 4) ? dn : up);
 }
 
 // inclusive prefix over the block's 8 lanes (j = lane & 7)
@@ -127,8 +145,10 @@ __device__ __forceinline__ int select32(uint32_t x, uint32_t t) {
 // [2k + 2, 2W + 2], a zero block without payload, the tile's words meeting the next tile's offset);
 // a tile that fails decodes as zeros and is counted, so a corrupt bundle raises on the host after
 // the one synchronisation instead of steering a read outside the blob.
-constexpr int kTileSteps = 8;                     // wave steps (of 8 blocks) per wave and tile
+constexpr int kTileSteps = 8;                     // decode: wave steps (of 8 blocks) per wave and tile
 constexpr int kTileBlocks = 4 * 8 * kTileSteps;    // 256 blocks = 16384 samples per tile
+constexpr int kEncWaves = 4, kEncSteps = 8;        // encode: as the decode (8 waves of 4 steps: 5 % slower)
+static_assert(kEncWaves * 8 * kEncSteps == kTileBlocks, "encode tile shape");
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kValMask = (1ull << 62) - 1;
 
 struct RArr {        // device copy of kmp_rice_array
@@ -149,30 +169,54 @@ __device__ __forceinline__ int array_of(const RArrs& A, int64_t g) {
   return a;
 }
 
-// exclusive prefix of v over the 8 block groups of a wave (v is the same on a group's 8 lanes);
-// *tot = the wave's total
+// exclusive prefix of v over the 8 block groups of a wave (v is the same on a group's 8 lanes, so
+// shifts by whole groups keep every lane of a group equal); *tot = the wave's total
 __device__ __forceinline__ uint32_t wave_groups_excl(uint32_t v, int lane, uint32_t* tot) {
-  uint32_t x = (lane & 7) == 0 ? v : 0u;
+  uint32_t x = v;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int d = 8; d < 64; d <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
     if (lane >= d) x += y;
   }
-  *tot = (uint32_t)__shfl((int)x, 63, 64);
-  const uint32_t incl = (uint32_t)__shfl((int)x, lane & ~7, 64);  // inclusive at the group's first lane
-  return incl - v;
+  *tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  return x - v;
+}
+
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// q[e] = zigzag(sample e) >> k for the lane's 8 samples; 16-bit samples two at a time (packed
+// 16-bit shifts: zigzag = (s << 1) ^ (s >> 15) per half)
+template <int W>
+__device__ __forceinline__ void quotients(const uint32_t (&w)[Sw<W>::NW], int k, uint32_t (&q)[8]) {
+  if constexpr (W == 16) {
+    const u16x2 kk = {(unsigned short)k, (unsigned short)k};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const s16x2 sv = __builtin_bit_cast(s16x2, w[i]);
+      const u16x2 z = __builtin_bit_cast(u16x2, (s16x2)(sv << (s16x2){1, 1})) ^
+                      __builtin_bit_cast(u16x2, (s16x2)(sv >> (s16x2){15, 15}));
+      const uint32_t qw = __builtin_bit_cast(uint32_t, (u16x2)(z >> kk));
+      q[2 * i] = qw & 0xffffu;
+      q[2 * i + 1] = qw >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = zigzag<W>(sample_of<W>(w, e)) >> k;
+  }
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_t tile_begin, int64_t tiles_total,
+__global__ void __launch_bounds__(64 * kEncWaves) rice_bundle_encode_kernel(RArrs A, int64_t tile_begin, int64_t tiles_total,
                                                                uint8_t* __restrict__ blob, int64_t payload_off,
                                                                uint64_t* __restrict__ state,
                                                                unsigned* __restrict__ ticket) {
   constexpr int NP = Sw<W>::NP, NW = Sw<W>::NW;
   constexpr int UMAX = 2 * W + 2;
-  constexpr int S = kTileSteps;
-  __shared__ uint32_t stream_lds[4][8][UMAX];
-  __shared__ uint32_t wsum[4];
+  constexpr int S = kEncSteps;
+  __shared__ uint32_t stage[kEncWaves][8 * S * UMAX];  // each wave's payload words, in payload order
+  __shared__ uint32_t wsum[kEncWaves];
   __shared__ uint64_t s_excl;
   __shared__ int64_t s_tile;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, j = lane & 7, g8 = lane >> 3;
@@ -185,11 +229,11 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
   const int64_t blk0 = t * kTileBlocks + wv * 8 * S;  // the wave's first block; step s: blk0 + 8 s + g8
   uint8_t* params = blob + R.side_off;
   uint8_t* bw = params + ((R.nb + 7) & ~(int64_t)7);
-  // ---- pass 1: per step, the block's k* and word count (the plan in registers); the samples stay
-  // in registers for pass 2 ----
+  // ---- pass 1: per step, the block's z-planes (lane j: planes 8p + j after the byte transpose,
+  // kept for pass 2), k* and its word count; the samples stay in registers for pass 2 ----
   uint32_t w[S][NW];
-  int prm[S];
-  uint32_t bex[S];  // the block's exclusive word offset inside the wave
+  uint32_t Zt[S][NP][2];
+  uint32_t pb[S];  // the block's k + 1 (6 bits) | its exclusive word offset inside the wave << 6
   uint32_t wtot = 0;
 #pragma unroll
   for (int st = 0; st < S; ++st) load8s<W>(R.x, R.n, (blk0 + 8 * st + g8) * 64 + j * 8, w[st]);
@@ -197,54 +241,120 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
   for (int st = 0; st < S; ++st) {
     const int64_t blk = blk0 + 8 * st + g8;
     const bool has = blk < R.nb;
-    uint32_t Z[NP][2];
-    zplanes<W>(w[st], Z);
-    uint32_t cnt[2 * NP];
+    zplanes<W>(w[st], Zt[st]);
 #pragma unroll
-    for (int i = 0; i < 2 * NP; ++i) cnt[i] = group8_sum(bytes_popcount(Z[i >> 1][i & 1]), lane);
-    uint32_t Ssum = 0, key = 0xffffffffu;
+    for (int p = 0; p < NP; ++p) xtr8(Zt[st][p][0], Zt[st][p][1], j);
+    // S_k = sum_i (z_i >> k) = sum_{b >= k} count_b 2^(b - k) for this lane's k = 8p + j: a doubling
+    // suffix sum of the plane counts over the group, plus S_{8(p+1)} (group lane 0) << (8 - j).
+    // Equal to the Horner recurrence S_k = 2 S_{k+1} + count_k of the oracle (capped at kSumCap
+    // for 32-bit samples: min(S_k, cap), which is what the capped recurrence yields)
+    uint32_t key = 0xffffffffu, above = 0;
 #pragma unroll
-    for (int k = W - 1; k >= 0; --k) {
-      const uint32_t c = (cnt[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      Ssum = 2u * Ssum + c;
-      if constexpr (W > 16) Ssum = min(Ssum, kSumCap);
-      key = min(key, ((Ssum + 95u) & ~31u) + 65u * (uint32_t)k);
+    for (int p = NP - 1; p >= 0; --p) {
+      const uint32_t c = __builtin_popcount(Zt[st][p][0]) + __builtin_popcount(Zt[st][p][1]);
+      uint32_t sk = group8_suffix2(c, j);
+      if (p < NP - 1) sk += above << (8 - j);
+      if constexpr (W > 16) sk = min(sk, kSumCap);
+      key = min(key, ((sk + 95u) & ~31u) + 65u * (uint32_t)(8 * p + j));
+      if (p > 0) above = group8_first(sk, j);
     }
-    const bool zero = Ssum == 0 || !has;
-    prm[st] = zero ? 0 : (int)(key & 31u) + 1;
+    key = group8_min(key, j);
+    // key == 64 <=> k = 0 with 2 words <=> S_0 == 0: an all-zero block
+    const bool zero = key == 64u || !has;
+    const uint32_t prm = zero ? 0u : (key & 31u) + 1u;
     const uint32_t words = zero ? 0u : key >> 5;
     if (j == 0 && has) {
-      params[blk] = (uint8_t)prm[st];
+      params[blk] = (uint8_t)prm;
       bw[blk] = (uint8_t)words;
     }
     uint32_t stot;
-    bex[st] = wtot + wave_groups_excl(words, lane, &stot);
+    pb[st] = prm | ((wtot + wave_groups_excl(words, lane, &stot)) << 6);
     wtot += stot;
   }
-  // ---- the tile's start: workgroup sum, then the decoupled look-back ----
+  // ---- the tile's start: workgroup sum; wave 0 publishes the aggregate and issues the first
+  // look-back reads, which are in flight while every wave stages its payload in LDS ----
   if (lane == 0) wsum[wv] = wtot;
   __syncthreads();
-  const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  uint32_t wbase = 0;
-  for (int q = 0; q < wv; ++q) wbase += wsum[q];
+  uint32_t agg = 0, wbase = 0;
+#pragma unroll
+  for (int q = 0; q < kEncWaves; ++q) {
+    wbase += q < wv ? wsum[q] : 0u;
+    agg += wsum[q];
+  }
+  // decoupled look-back by the whole first wave: lane l reads the state of tile base - l, so each
+  // memory round trip covers 64 predecessors (a thread walking them one by one serialised the chain
+  // at ~0.5 us per tile; 256 per round trip measured slower: more registers).  The states are the
+  // only data exchanged, so relaxed agent-scope atomics suffice
+  int64_t base = g - 1;
+  uint64_t v = 0;
   if (wv == 0) {
-    // decoupled look-back by the whole first wave: lane l reads the state of tile base - l, so each
-    // memory round trip covers 64 predecessors (a thread walking them one by one serialised the
-    // chain at ~0.5 us per tile).  The states are the only data exchanged, so relaxed agent-scope
-    // atomics suffice: a release store at agent scope writes back the XCD's dirty L2 lines (every
-    // tile's payload) and an acquire load invalidates caches
+    if (lane == 0) __hip_atomic_store(&state[g], (g == 0 ? kFlagPre : kFlagAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t i = base - lane;
+    if (g > 0) v = i >= 0 ? __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
+  }
+  // ---- pass 2: each step's block payloads staged in LDS at their wave-local word offsets: the k
+  // low planes, then the unary part (zeroed, then one LDS or per 32 bits of a lane's codes) ----
+  uint32_t* const wl = stage[wv];
+#pragma unroll
+  for (int st = 0; st < S; ++st) {
+    const int param = (int)(pb[st] & 63u);
+    const uint32_t off = pb[st] >> 6;
+    const int k = param > 0 ? param - 1 : 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int b = 8 * p + j;
+      if (param > 0 && b < k) {
+        wl[off + 2 * b] = Zt[st][p][0];
+        wl[off + 2 * b + 1] = Zt[st][p][1];
+      }
+    }
+    uint32_t q[8];
+    quotients<W>(w[st], k, q);
+    // r[e]: bit of sample e's terminator relative to the lane's first code
+    uint32_t r[8];
+    r[0] = q[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) r[e] = r[e - 1] + q[e] + 1u;
+    const uint32_t len = r[7] + 1u;
+    const uint32_t incl = group8_incl(len, j);
+    const uint32_t uw = (group8_last(incl, j) + 31u) >> 5;
+    uint32_t* const us = wl + off + 2 * k;
+    if (param > 0)
+      for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) us[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t pos0 = incl - len;
+    if (param > 0) {
+      if (len <= 32u) {  // the lane's 8 codes in one 32-bit mask: at most 2 LDS ors
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m |= 1u << r[e];
+        const uint32_t wd = pos0 >> 5;
+        const uint64_t mm = (uint64_t)m << (pos0 & 31u);
+        atomicOr(&us[wd], (uint32_t)mm);
+        if ((uint32_t)(mm >> 32)) atomicOr(&us[wd + 1], (uint32_t)(mm >> 32));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t pos = pos0 + r[e];
+          if (pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&us[pos >> 5], 1u << (pos & 31));
+        }
+      }
+    }
+  }
+  // ---- wave 0 completes the look-back ----
+  if (wv == 0) {
     uint64_t excl = 0;
-    if (g == 0) {
-      if (lane == 0) __hip_atomic_store(&state[0], kFlagPre | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&state[g], kFlagAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t base = g - 1;
+    if (g > 0) {
+#ifdef KMP_RICE_EXP_NOLOOKBACK
+      excl = (uint64_t)g * 8192u;
+      if (true) {} else
+#endif
       while (true) {
-        const int64_t i = base - lane;
-        uint64_t v = i >= 0 ? __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
         while (__any((v >> 62) == 0)) {  // a predecessor has not published yet: re-read those
           __builtin_amdgcn_s_sleep(1);
-          if ((v >> 62) == 0) v = __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((v >> 62) == 0) v = __hip_atomic_load(&state[base - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const uint64_t pre = __ballot((v >> 62) == 2);  // tiles whose inclusive prefix is known
         const int lp = pre ? __builtin_ctzll(pre) : 64;  // the nearest one
@@ -254,6 +364,8 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
         excl += c;
         if (pre) break;
         base -= 64;
+        const int64_t i = base - lane;
+        v = i >= 0 ? __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
       }
       if (lane == 0) __hip_atomic_store(&state[g], kFlagPre | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -270,56 +382,33 @@ __global__ void __launch_bounds__(256) rice_bundle_encode_kernel(RArrs A, int64_
     }
   }
   __syncthreads();
-  const uint64_t wstart = s_excl + wbase;
-  uint32_t* payload = (uint32_t*)(blob + payload_off);
-  uint32_t* ustream = stream_lds[wv][g8];
-  // ---- pass 2: the payload of each step's blocks: the k low planes, then the unary part ----
+  // ---- the wave's payload words are contiguous: one coalesced copy out of LDS ----
+  uint32_t* const dst = (uint32_t*)(blob + payload_off) + (s_excl + wbase);
+  for (uint32_t i = lane; i < wtot; i += 64) dst[i] = wl[i];
+}
+
+// the lane's 8 samples from their quotients and low bits: unzigzag((q << k) | low); 16-bit samples
+// two at a time (for a valid stream q << k < 2^16, so the packed shift loses nothing)
+template <int W>
+__device__ __forceinline__ void samples_from_codes(const uint32_t (&q)[8], int k, const uint32_t (&lowv)[Sw<W>::NW],
+                                                   bool coded, uint32_t (&wout)[Sw<W>::NW]) {
+  if constexpr (W == 16) {
+    const u16x2 kk = {(unsigned short)k, (unsigned short)k};
 #pragma unroll
-  for (int st = 0; st < S; ++st) {
-    const int param = prm[st];
-    const uint64_t off = wstart + bex[st];
-    const int k = param > 0 ? param - 1 : 0;
-    uint32_t Z[NP][2];
-    zplanes<W>(w[st], Z);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      xtr8(Z[p][0], Z[p][1], j);
-      const int b = 8 * p + j;
-      if (param > 0 && b < k) {
-        payload[off + 2 * b] = Z[p][0];
-        payload[off + 2 * b + 1] = Z[p][1];
-      }
+    for (int i = 0; i < 4; ++i) {
+      const u16x2 qv = __builtin_bit_cast(u16x2, (q[2 * i] & 0xffffu) | (q[2 * i + 1] << 16));
+      const u16x2 z = (u16x2)(qv << kk) | __builtin_bit_cast(u16x2, lowv[i]);
+      const u16x2 v = (u16x2)(z >> (u16x2){1, 1}) ^ (u16x2)((u16x2){0, 0} - (z & (u16x2){1, 1}));
+      wout[i] = coded ? __builtin_bit_cast(uint32_t, v) : 0u;
     }
-    uint32_t q[8], len = 0;
+  } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      q[e] = zigzag<W>(sample_of<W>(w[st], e)) >> k;
-      len += q[e] + 1u;
-    }
-    const uint32_t incl = group8_incl(len, j);
-    const uint32_t tot = (uint32_t)__shfl((int)incl, (g8 << 3) | 7, 64);
-    const uint32_t uw = (tot + 31u) >> 5;
-    for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) ustream[i] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    uint32_t pos = incl - len;
+    for (int i = 0; i < Sw<W>::NW; ++i) wout[i] = 0u;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      pos += q[e];
-      if (param > 0 && pos < 32u * min(uw, (uint32_t)UMAX)) atomicOr(&ustream[pos >> 5], 1u << (pos & 31));
-      pos += 1u;
+      const uint32_t z = coded ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
+      set_sample<W>(wout, e, unzigzag<W>(z));
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (param > 0) {
-      const uint64_t ubase = off + 2u * (uint32_t)k;
-      for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) payload[ubase + i] = ustream[i];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();  // the next step's zeroing must not overtake these reads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
 }
 
@@ -331,7 +420,7 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
   constexpr int NP = Sw<W>::NP, NW = Sw<W>::NW;
   constexpr int SPAN = 8 * (2 * W + 2);  // payload words of a wave step's 8 blocks, at most
   constexpr int S = kTileSteps;
-  __shared__ uint32_t span_lds[4][SPAN];
+  __shared__ uint32_t span_lds[4][S * SPAN];  // each wave's payload words (contiguous in the payload)
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t wbad[4];
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, j = lane & 7, g8 = lane >> 3;
@@ -381,21 +470,35 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
   if (tile_bad && tid == 0) atomicAdd(bad_out, 1ull);
   uint32_t wbase = 0;
   for (int q = 0; q < wv; ++q) wbase += wsum[q];
-  const uint32_t* payload = (const uint32_t*)(blob + payload_off);
+  // ---- the wave's payload words (all S steps: one contiguous span) staged in LDS at once, 8
+  // loads per lane in flight (a span per step paid one memory latency per step) ----
   uint32_t* const wspan = span_lds[wv];
-  // ---- per step: stage the 8 blocks' words in LDS, unpack ----
+  {
+    const uint32_t* src = (const uint32_t*)(blob + payload_off) + (start + wbase);
+    const int cnt = tile_bad ? 0 : (int)min(wtot, (uint32_t)(S * SPAN));
+    for (int i0 = 0; i0 < cnt; i0 += 64 * 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u + lane;
+        v[u] = i < cnt ? src[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 64 * u + lane;
+        if (i < cnt) wspan[i] = v[u];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  // ---- per step: unpack the 8 blocks ----
 #pragma unroll 1
   for (int st = 0; st < S; ++st) {
     int param = tile_bad ? 0 : prm[st];
     const int words = tile_bad ? 0 : wds[st];
-    const uint32_t sw = (st + 1 < S ? stp[st + 1] : wtot) - stp[st];  // this step's words
-    const uint64_t sstart = start + wbase + stp[st];
-    const int cnt = tile_bad ? 0 : (int)min<uint64_t>((uint64_t)sw, (uint64_t)SPAN);
-    for (int i = lane; i < cnt; i += 64) wspan[i] = payload[sstart + i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const uint32_t* const bp = wspan + (tile_bad ? 0 : bex[st]);
+    const uint32_t* const bp = wspan + (tile_bad ? 0 : stp[st] + bex[st]);
     const int k = param > 0 ? param - 1 : 0;
     const int uw = param > 0 ? words - 2 * k : 0;
     uint32_t Z[NP][2];
@@ -433,47 +536,49 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
       }
       int wi = (int)(pos >> 5);
       const uint32_t sh = pos & 31u;
-      const uint32_t a0 = wi < uw ? us[wi] : 0u, b0 = wi + 1 < uw ? us[wi + 1] : 0u, c0 = wi + 2 < uw ? us[wi + 2] : 0u;
-      uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c0, b0, sh) << 32) | __builtin_amdgcn_alignbit(b0, a0, sh);
-      if (__builtin_popcountll(win) >= 8) {
+      const uint32_t a0 = wi < uw ? us[wi] : 0u, b0 = wi + 1 < uw ? us[wi + 1] : 0u;
+      uint32_t x = __builtin_amdgcn_alignbit(b0, a0, sh);
+      if (__builtin_popcount(x) >= 8) {  // the lane's 8 codes within 32 bits (the common case)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const uint32_t tz = (uint32_t)__builtin_ctzll(win);
+          const uint32_t tz = (uint32_t)__builtin_ctz(x);
           q[e] = tz;
-          win = (win >> tz) >> 1;
+          x = (x >> tz) >> 1;
         }
       } else {
-        uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
-        uint32_t base = pos;
+        const uint32_t c0 = wi + 2 < uw ? us[wi + 2] : 0u;
+        uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(c0, b0, sh) << 32) | x;
+        if (__builtin_popcountll(win) >= 8) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          while (cur == 0u && wi + 1 < uw) {
-            ++wi;
-            cur = us[wi];
-            base = 32u * wi;
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t tz = (uint32_t)__builtin_ctzll(win);
+            q[e] = tz;
+            win = (win >> tz) >> 1;
           }
-          if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
-          const uint32_t tz = __builtin_ctz(cur);
-          q[e] = base + tz - pos;
-          pos = base + tz + 1u;
-          cur = tz == 31u ? 0u : cur >> (tz + 1u);
-          base = pos;
+        } else {
+          uint32_t cur = wi < uw ? us[wi] >> sh : 0u;
+          uint32_t base = pos;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            while (cur == 0u && wi + 1 < uw) {
+              ++wi;
+              cur = us[wi];
+              base = 32u * wi;
+            }
+            if (cur == 0u) break;  // a corrupt stream with fewer than 64 terminators
+            const uint32_t tz = __builtin_ctz(cur);
+            q[e] = base + tz - pos;
+            pos = base + tz + 1u;
+            cur = tz == 31u ? 0u : cur >> (tz + 1u);
+            base = pos;
+          }
         }
       }
     }
     uint32_t wout[NW];
-#pragma unroll
-    for (int i = 0; i < NW; ++i) wout[i] = 0u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t z = param > 0 ? (q[e] << k) | sample_of<W>(lowv, e) : 0u;
-      set_sample<W>(wout, e, unzigzag<W>(z));
-    }
+    samples_from_codes<W>(q, k, lowv, param > 0, wout);
     const int64_t blk = blk0 + 8 * st + g8;
     if (blk < R.nb) store8s<W>((void*)R.x, R.n, blk * 64 + j * 8, wout);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();  // the next step's staging must not overtake these reads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
 }
 
@@ -587,9 +692,9 @@ int kmp_rice_bundle_encode(int32_t dtype, const kmp_rice_array* arrays, int32_t 
   if (hipMemsetAsync(ticket, 0, sizeof(unsigned), s) != hipSuccess) return fail(KMP_ERR_LAUNCH, "rice bundle: memset");
   if (tiles == 0) return KMP_OK;
   KMP_REQUIRE(tiles < ((int64_t)1 << 31), "rice bundle: too many tiles in one call");
-  if (W == 8) rc::rice_bundle_encode_kernel<8><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
-  else if (W == 16) rc::rice_bundle_encode_kernel<16><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
-  else rc::rice_bundle_encode_kernel<32><<<(unsigned)tiles, 256, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  if (W == 8) rc::rice_bundle_encode_kernel<8><<<(unsigned)tiles, 64 * rc::kEncWaves, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  else if (W == 16) rc::rice_bundle_encode_kernel<16><<<(unsigned)tiles, 64 * rc::kEncWaves, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
+  else rc::rice_bundle_encode_kernel<32><<<(unsigned)tiles, 64 * rc::kEncWaves, 0, s>>>(A, tile_begin, tiles_total, bundle, payload_off, state, ticket);
   return check_launch("rice_bundle_encode");
 }
 

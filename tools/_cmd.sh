@@ -1,16 +1,10 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/chk; rm -rf $O; mkdir -p $O
-timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 tools/chunks_probe.py 5 > $O/run.log 2>&1 || { tail -20 $O/run.log; exit 1; }
-tail -1 $O/run.log
-f=$(find $O/p -name 'run_kernel_stats.csv'); python3 -c "
-import csv
-for r in csv.DictReader(open('$f')):
-    print(r['Calls'], round(float(r['AverageNs'])/1e3,2), r['Name'][:110])
-"
-f=$(find $O/p -name 'run_kernel_trace.csv'); python3 -c "
-import csv
-rows=list(csv.DictReader(open('$f')))
-for r in rows[-12:]:
-    print(round((int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1e3,2), r['Grid_Size_X'] if 'Grid_Size_X' in r else r.get('Grid_Size',''), r['Kernel_Name'][:80])
-"
+O=gpurun_out/r3s10; mkdir -p $O
+timeout -k 10 300 python tools/bench_rows.py --no-cpu --rows rice > $O/rows.log 2>&1 || exit 1
+grep -h '"rice:noise[0-9]*"' $O/rows.log | python3 -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print(d['row'], d['pack_encoded_ms'], d['unpack_encoded_ms'], d['pack_device_us'], d['unpack_device_us'])"
+timeout -k 10 300 bash tools/sq_counters.sh $O/sq "rice 4 10" > $O/sq.log 2>&1 || exit 1
+cat $O/sq.log
