@@ -249,6 +249,17 @@ def _rice_arrays(ts, ptrs, offs, first, count):
     return arr
 
 
+def _rice_arrays_n(ns, offs, first, count):
+    arr = (_lib.RiceArray * count)()
+    for q in range(count):
+        i = first + q
+        arr[q].samples = 0
+        arr[q].n = ns[i]
+        arr[q].side_off, arr[q].toff_off = offs[i]
+        arr[q].rec_off = _RHEAD.size + _RREC.size * i + 112
+    return arr
+
+
 def _rice_pack_bundle(arrays, dims):
     out, poff, launched, keep = _rice_encode_launch(arrays, dims)
     if launched:
@@ -257,14 +268,30 @@ def _rice_pack_bundle(arrays, dims):
             out[poff + 4 * words:total].zero_()
     else:
         total = poff
-    del keep  # the header copy is complete (synchronised above, or nothing launched after it)
+    del keep
     return out[:total]
 
 
-def _rice_encode_launch(arrays, dims):
-    """Everything of a rice pack up to the synchronisation: ``(worst-case sized output, payload
-    offset, whether a kernel ran, host objects the queued copy still reads)``."""
-    ts = [dev.to_device(a)[0].contiguous() for a in arrays]
+# Layouts of recent bundle shapes (header bytes, offsets, tile counts, launch records), keyed by
+# the arrays' dtypes and shapes: a repeated pack of same-shaped results (a volume's chunks, a
+# series) skips the host-side layout work.  The header is copied from a device copy.
+_ENC_PLANS = {}
+_DEC_PLANS = {}
+_PLAN_CACHE_MAX = 64
+
+
+def _remember(cache, key, plan):
+    if len(cache) >= _PLAN_CACHE_MAX:
+        cache.clear()
+    cache[key] = plan
+    return plan
+
+
+def _rice_enc_plan(ts, dims):
+    key = (tuple((t.dtype, tuple(t.shape)) for t in ts), tuple(int(d) for d in dims))
+    plan = _ENC_PLANS.get(key)
+    if plan is not None:
+        return plan
     if not ts or len(ts) > _MAX_ARRAYS or len(dims) > 8:
         raise ValueError(f'a bundle holds 1 .. {_MAX_ARRAYS} arrays and <= 8 dims')
     for t in ts:
@@ -274,27 +301,41 @@ def _rice_encode_launch(arrays, dims):
     ns = [t.numel() for t in ts]
     head, offs, poff = _bundle_layout(ns)
     tiles = [int(lib.kmp_rice_tiles(n)) for n in ns]
-    T = sum(tiles)
     worst = sum(int(lib.kmp_pack_blocks(n)) * (2 * 8 * t.element_size() + 2) * 4 for n, t in zip(ns, ts))
-    out = dev.empty((poff + worst + 8,), torch.uint8)
-    out[:poff].zero_()
     hdr = bytearray(_RHEAD.pack(BUNDLE_MAGIC, RICE_VERSION, len(ts), len(dims), 0,
                                 *(list(int(d) for d in dims) + [0] * (8 - len(dims))), poff, 0, poff, 0))
     for t, (side, toff), nt in zip(ts, offs, tiles):
         hdr += _RREC.pack(dev.dtype_code(t), t.dim(), *(list(t.shape) + [0] * (8 - t.dim())), t.numel(),
                           int(lib.kmp_pack_blocks(t.numel())), nt, side, toff, 0, 0)
-    pinned = torch.frombuffer(hdr, dtype=torch.uint8).pin_memory()
-    out[:head].copy_(pinned, non_blocking=True)
-    if T:
-        ws = dev.empty((int(lib.kmp_rice_bundle_workspace_bytes(T)),), torch.uint8)
-        ptrs = [t.data_ptr() for t in ts]
-        tile_begin = 0
-        for first, count in _runs(ts):
-            arr = _rice_arrays(ts, ptrs, offs, first, count)
-            check(lib.kmp_rice_bundle_encode(dev.dtype_code(ts[first]), arr, count, tile_begin, T, out.data_ptr(),
-                                             poff, ws.data_ptr(), dev.stream()), 'rice bundle')
-            tile_begin += sum(tiles[first:first + count])
-    return out, poff, T > 0, (pinned, ts)
+    T = sum(tiles)
+    runs = []
+    tile_begin = 0
+    for first, count in _runs(ts):
+        runs.append((first, count, tile_begin, dev.dtype_code(ts[first]), _rice_arrays(ts, [0] * len(ts), offs, first, count)))
+        tile_begin += sum(tiles[first:first + count])
+    return _remember(_ENC_PLANS, key, {
+        'head': head, 'poff': poff, 'worst': worst, 'T': T, 'runs': runs,
+        'hdr': torch.frombuffer(hdr, dtype=torch.uint8).to('cuda'),
+        'ws_bytes': int(lib.kmp_rice_bundle_workspace_bytes(T)) if T else 0})
+
+
+def _rice_encode_launch(arrays, dims):
+    """Everything of a rice pack up to the synchronisation: ``(worst-case sized output, payload
+    offset, whether a kernel ran, objects the queued work still reads)``."""
+    ts = [dev.to_device(a)[0] for a in arrays]
+    plan = _rice_enc_plan(ts, dims)
+    poff, head = plan['poff'], plan['head']
+    out = dev.empty((poff + plan['worst'] + 8,), torch.uint8)
+    out[:head].copy_(plan['hdr'], non_blocking=True)
+    out[head:poff].zero_()
+    if plan['T']:
+        ws = dev.empty((plan['ws_bytes'],), torch.uint8)
+        for first, count, tile_begin, code, arr in plan['runs']:
+            for q in range(count):
+                arr[q].samples = ts[first + q].data_ptr()
+            check(lib.kmp_rice_bundle_encode(code, arr, count, tile_begin, plan['T'], out.data_ptr(), poff,
+                                             ws.data_ptr(), dev.stream()), 'rice bundle')
+    return out, poff, plan['T'] > 0, ts
 
 
 def _rice_unpack_bundle(b, hb):
@@ -310,6 +351,34 @@ def _rice_unpack_bundle(b, hb):
 def _rice_decode_launch(b, hb):
     """Header checks and the decode launches, no synchronisation: ``(arrays, dims, bad-tile
     counter or None)``."""
+    if len(hb) < _RHEAD.size:
+        raise ValueError('truncated bundle')
+    f = _RHEAD.unpack(hb[:_RHEAD.size])
+    count = f[2]
+    head = _RHEAD.size + _RREC.size * count if 1 <= count <= _MAX_ARRAYS else _RHEAD.size
+    if len(hb) < head:
+        hb = b[:head].cpu().numpy().tobytes()
+    key = bytes(hb[:head])  # the plan depends on these bytes only (the blob size is checked per call)
+    plan = _DEC_PLANS.get(key)
+    if plan is None:
+        plan = _remember(_DEC_PLANS, key, _rice_dec_plan(b, hb))
+    if plan['total'] > b.numel():
+        raise ValueError(f'truncated bundle ({b.numel()} < {plan["total"]} bytes)')
+    outs = [dev.empty(shape, dev.CODE_TO_TORCH[code]) for shape, code in zip(plan['shapes'], plan['codes'])]
+    if plan['T']:
+        bad = torch.zeros((1,), dtype=torch.int64, device='cuda')
+        for first, count, tile_begin, code, arr in plan['runs']:
+            for q in range(count):
+                arr[q].samples = outs[first + q].data_ptr()
+            check(lib.kmp_rice_bundle_decode(code, arr, count, tile_begin, b.data_ptr(), plan['poff'], plan['words'],
+                                             bad.data_ptr(), dev.stream()), 'rice bundle')
+    else:
+        bad = None
+    return outs, plan['dims'], bad
+
+
+def _rice_dec_plan(b, hb):
+    """The checked layout of a v2 bundle header (everything a decode needs but the payload)."""
     if len(hb) < _RHEAD.size:
         raise ValueError('truncated bundle')
     f = _RHEAD.unpack(hb[:_RHEAD.size])
@@ -340,8 +409,8 @@ def _rice_decode_launch(b, hb):
     ehead, offs, epoff = _bundle_layout(ns)
     if poff != epoff or [(r[13], r[14]) for r in recs] != offs:
         raise ValueError('bundle layout does not match its records')
-    if total != poff + _pad8(4 * words) or total > b.numel():
-        raise ValueError(f'truncated bundle ({b.numel()} < {total} bytes)')
+    if total != poff + _pad8(4 * words):
+        raise ValueError(f'bundle size field {total} does not match its payload')
     prev_end = 0
     for r, n, code in zip(recs, ns, codes):
         first, end = r[15], r[16]
@@ -352,20 +421,14 @@ def _rice_decode_launch(b, hb):
             prev_end = end
     if prev_end != words:
         raise ValueError('bundle payload words do not match its arrays')
-    outs = [dev.empty(shape, dev.CODE_TO_TORCH[code]) for shape, code in zip(shapes, codes)]
     tiles = [int(lib.kmp_rice_tiles(n)) for n in ns]
-    if sum(tiles):
-        bad = torch.zeros((1,), dtype=torch.int64, device='cuda')
-        ptrs = [o.data_ptr() for o in outs]
-        tile_begin = 0
-        for first, count in _runs(outs):
-            arr = _rice_arrays(outs, ptrs, offs, first, count)
-            check(lib.kmp_rice_bundle_decode(codes[first], arr, count, tile_begin, b.data_ptr(), poff, words,
-                                             bad.data_ptr(), dev.stream()), 'rice bundle')
-            tile_begin += sum(tiles[first:first + count])
-    else:
-        bad = None
-    return outs, tuple(int(d) for d in dims[:nsp]), bad
+    runs = []
+    tile_begin = 0
+    for first, count in _runs([torch.empty(0, dtype=dev.CODE_TO_TORCH[c]) for c in codes]):
+        runs.append((first, count, tile_begin, codes[first], _rice_arrays_n(ns, offs, first, count)))
+        tile_begin += sum(tiles[first:first + count])
+    return {'shapes': shapes, 'codes': codes, 'dims': tuple(int(d) for d in dims[:nsp]), 'poff': poff,
+            'words': words, 'total': total, 'T': sum(tiles), 'runs': runs}
 
 
 # ---------------------------------------------------------------------------------------------
