@@ -88,6 +88,14 @@ __device__ __forceinline__ uint32_t group8_last(uint32_t x, int j) {
   return (j & 4) ? t : u;
 }
 
+// sum over the group (every lane of the group ends with it)
+__device__ __forceinline__ uint32_t group8_sum(uint32_t v, int j) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  const uint32_t up = dpp<0x104>(v), dn = dpp<0x114>(v);
+  return v + ((j & 4) ? dn : up);
+}
+
 // minimum over the group (every lane of the group ends with it)
 __device__ __forceinline__ uint32_t group8_min(uint32_t v, int j) {
   v = min(v, dpp<0xB1>(v));
@@ -520,9 +528,30 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
     uint32_t q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = 0u;
+    // lane j's first code follows terminator 8j - 1.  Streams of at most 8 words (the usual case):
+    // lane m holds word m and its popcount c_m; with the group's inclusive counts cum_m, the word
+    // holding terminator 8j - 1 is #{m : cum_m >> 3 < j}, counted for all j at once as nibble j of
+    // a group sum (lane m adds 1 to the nibbles j > cum_m >> 3); then one select in that word.
+    // No loop and no LDS round trip per word (a walk word by word measured slower)
+    uint32_t pos8 = 0;
+    const bool short_stream = __all(!(param > 0) || uw <= 8);
+    if (short_stream) {
+      const uint32_t wm = (param > 0 && j < uw) ? us[j] : 0u;
+      const uint32_t cm = __builtin_popcount(wm);
+      const uint32_t cum = group8_incl(cm, j);
+      const uint32_t d = cum >> 3;
+      const uint32_t f = d >= 7u ? 0u : 0x11111110u & (~0u << (4u * (d + 1u)));
+      const uint32_t F = group8_sum(f, j);
+      const uint32_t wi = (F >> (4 * j)) & 15u;  // j > 0
+      const int src = (lane & ~7) | (int)min(wi, 7u);
+      const uint32_t wsel = (uint32_t)__shfl((int)wm, src, 64);
+      const uint32_t before = (uint32_t)__shfl((int)(cum - cm), src, 64);
+      pos8 = j == 0 ? 0u : wi < 8u && wi < (uint32_t)uw ? 32u * wi + select32(wsel, 8u * j - 1u - before) + 1u
+                                                         : 32u * (uint32_t)uw;
+    }
     if (param > 0 && uw > 0) {
-      uint32_t pos = 0;
-      if (j > 0) {
+      uint32_t pos = pos8;
+      if (!short_stream && j > 0) {
         const uint32_t r = 8u * j - 1u;
         uint32_t acc = 0, word = 0;
         int wi = 0;
