@@ -63,11 +63,14 @@ struct OutRows {
   uint2 mv[7];
 };
 
-// Store policy (STC, stp8 in kmp_wave.h): the encode's lowres and maps are what the next kernel
-// reads (a decode, a pack, a copy to the host), so by default they are stored cached: at C3 the
-// following decode reads part of its 256 MiB of maps from the MALL (decode 90.7 -> 85.2 us, encode
-// unchanged; profiles/round2/ab_wave3d_store_policy.log).  The decode's highres stays non-temporal:
-// cached, its dirty lines drain during the next encode (+7 us).  KMP_W3_ST_ENC=0: non-temporal.
+// Store policy (STC, stp8 in kmp_wave.h), chosen on the pipelines that follow an encode at C3
+// (tools/pipeline_rows.py, profiles/round3/pipeline_store_policy_r3.log; DESIGN §5 "pipeline"):
+// the encode's lowres and maps are stored non-temporal.  Cached (MALL-allocating) stores let a
+// decode that immediately re-reads the same maps find part of them in the MALL (bench.py's
+// encode -> decode loop: 177 -> 171 us per pair), but their dirty lines drain during the next
+// encode when encodes run back to back (a producer of chunks: 85 -> 103 us per encode), and encode
+// -> Rice pack / Rice unpack -> decode are within 3 us either way.  The decode's highres is
+// non-temporal too (cached: +7 us on the next encode).  KMP_W3_ST_ENC=1: cached encode stores.
 
 // WPE: the amdgpu_waves_per_eu register budget (PL = 2 encode: 3 waves / SIMD without spills).
 template <typename T, bool DEC, int PL, bool ONE, bool STC>
@@ -440,8 +443,8 @@ static void launch_wave3d_s(int pl, dim3 grid, dim3 block, hipStream_t stream, c
 
 template <typename T, bool DEC>
 static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
-  // the decode's stores stay non-temporal; the encode's are cached unless KMP_W3_ST_ENC=0 (stp8)
-  if (!DEC && w3_env("KMP_W3_ST_ENC", 1)) launch_wave3d_s<T, DEC, true>(pl, grid, block, stream, a);
+  // non-temporal stores in both directions; KMP_W3_ST_ENC=1: the encode's cached (stp8)
+  if (!DEC && w3_env("KMP_W3_ST_ENC", 0)) launch_wave3d_s<T, DEC, true>(pl, grid, block, stream, a);
   else launch_wave3d_s<T, DEC, false>(pl, grid, block, stream, a);
 }
 

@@ -672,10 +672,12 @@ static int w3p_roll(int P, int bytes) {
   return zr >= 2 ? (zr + 1) / 2 * 2 : 0;
 }
 
-// the encode's lowres / map stores: cached (MALL-allocating, stp8 in kmp_wave.h; alternating encode /
-// decode pairs at C3: p = 1 -0.5 us, p = 2 -10 us per pair, profiles/round2/ab_wave3dp_store_policy.log) unless
-// KMP_W3P_ST_ENC=0 (non-temporal)
-static bool w3p_stc(bool dec) { return !dec && w3p_env("KMP_W3P_ST_ENC", 1); }
+// the encode's lowres / map stores, chosen on the pipelines that follow an encode at C3
+// (tools/pipeline_rows.py, profiles/round3/pipeline_store_policy_r3.log; DESIGN §5 "pipeline"):
+// p = 1 non-temporal (encodes back to back 103 -> 91 us, encode -> Rice pack and Rice unpack ->
+// decode within 1-4 us either way); p = 2 cached, MALL-allocating (stp8 in kmp_wave.h: back to back
+// the same, encode -> Rice pack -13 us, encode -> decode -35 us).  KMP_W3P_ST_ENC=0 / 1 forces one
+static bool w3p_stc(bool dec, int P) { return !dec && w3p_env("KMP_W3P_ST_ENC", P == 2 ? 1 : 0); }
 
 template <typename T, bool DEC, bool STC>
 static void launch_wave3dr_s(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
@@ -684,7 +686,7 @@ static void launch_wave3dr_s(int P, dim3 grid, dim3 block, hipStream_t stream, c
 }
 template <typename T, bool DEC>
 static void launch_wave3dr(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
-  if (w3p_stc(DEC)) launch_wave3dr_s<T, DEC, true>(P, grid, block, stream, a);
+  if (w3p_stc(DEC, P)) launch_wave3dr_s<T, DEC, true>(P, grid, block, stream, a);
   else launch_wave3dr_s<T, DEC, false>(P, grid, block, stream, a);
 }
 
@@ -711,7 +713,7 @@ static void launch_wave3dp_s(int P, int pl, int wpe, dim3 grid, dim3 block, hipS
 
 template <typename T, bool DEC>
 static void launch_wave3dp(int P, int pl, int wpe, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
-  if (w3p_stc(DEC)) launch_wave3dp_s<T, DEC, true>(P, pl, wpe, grid, block, stream, a);
+  if (w3p_stc(DEC, P)) launch_wave3dp_s<T, DEC, true>(P, pl, wpe, grid, block, stream, a);
   else launch_wave3dp_s<T, DEC, false>(P, pl, wpe, grid, block, stream, a);
 }
 

@@ -658,9 +658,10 @@ def test_trace_ranges_do_not_change_results(kom, monkeypatch):
 ])
 @pytest.mark.parametrize('cached', ['0', '1'])
 def test_encode_store_policy_is_output_neutral(kom, case, cached, monkeypatch):
-    """The encode kernels' lowres / map stores are cached (MALL-allocating) by default and
-    non-temporal with KMP_*_ST_ENC=0 (INTEGRATION.md knobs): both policies give the oracle's bytes
-    and a lossless decode, and the wave kernel family served the call."""
+    """The encode kernels' lowres / map stores are cached (MALL-allocating) or non-temporal
+    (KMP_*_ST_ENC = 1 / 0, INTEGRATION.md knobs; the defaults per kernel and padding were chosen on
+    the pipeline rows): both policies give the oracle's bytes and a lossless decode, and
+    the wave kernel family served the call."""
     knob, shape, dtype, p, family = case
     monkeypatch.setenv(knob, cached)
     import oracle
