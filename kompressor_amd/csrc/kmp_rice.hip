@@ -382,10 +382,14 @@ __global__ void __launch_bounds__(64 * kEncWaves) rice_bundle_encode_kernel(RArr
       ((uint64_t*)(blob + R.toff_off))[t] = excl;
       uint64_t* rec = (uint64_t*)(blob + R.rec_off);
       if (t == 0) rec[0] = excl;
-      if (t == R.ntile - 1) rec[1] = excl + agg;
+      if (t == R.ntile - 1) {
+        rec[1] = excl + agg;
+        for (int64_t b = R.nb; b < ((R.nb + 7) & ~(int64_t)7); ++b) params[b] = bw[b] = 0;  // the side arrays' padding
+      }
       if (g == tiles_total - 1) {  // the bundle's payload words and byte size (header fields 56, 64)
         ((uint64_t*)blob)[7] = excl + agg;
         ((uint64_t*)blob)[8] = (uint64_t)payload_off + (((excl + agg) * 4 + 7) & ~7ull);
+        if ((excl + agg) & 1) ((uint32_t*)(blob + payload_off))[excl + agg] = 0u;  // the payload's padding to 8 bytes
       }
     }
   }

@@ -262,10 +262,8 @@ def _rice_arrays_n(ns, offs, first, count):
 
 def _rice_pack_bundle(arrays, dims):
     out, poff, launched, keep = _rice_encode_launch(arrays, dims)
-    if launched:
+    if launched:  # the kernel zeroes the side arrays' and the payload's padding
         words, total = out[56:72].view(torch.int64).tolist()  # the one synchronisation
-        if poff + 4 * words < total:
-            out[poff + 4 * words:total].zero_()
     else:
         total = poff
     del keep
@@ -327,7 +325,8 @@ def _rice_encode_launch(arrays, dims):
     poff, head = plan['poff'], plan['head']
     out = dev.empty((poff + plan['worst'] + 8,), torch.uint8)
     out[:head].copy_(plan['hdr'], non_blocking=True)
-    out[head:poff].zero_()
+    if not plan['T'] and poff > head:
+        out[head:poff].zero_()
     if plan['T']:
         ws = dev.empty((plan['ws_bytes'],), torch.uint8)
         for first, count, tile_begin, code, arr in plan['runs']:
