@@ -112,6 +112,7 @@ __device__ __forceinline__ void map_ext(const Geo& g, int nsp, int k, int64_t (&
 struct MapExt {
   int32_t u[7][3], e[7][3];
   int32_t par[7][3];
+  int32_t mn[3];  // the smallest trimmed extent per axis over the lowres and the maps
 };
 
 static MapExt map_exts(const Geo& g, int nsp) {
@@ -125,6 +126,10 @@ static MapExt map_exts(const Geo& g, int nsp) {
       m.u[k][a] = (int32_t)(par[a] ? g.Lc[a] : g.L[a]);
       m.e[k][a] = (int32_t)(par[a] ? g.Lc[a] : g.E[a]);
     }
+  }
+  for (int a = 0; a < 3; ++a) {
+    m.mn[a] = a < 3 - nsp ? 1 : (int32_t)g.E[a];
+    for (int k = 0; k < (nsp == 3 ? 7 : 3); ++k) m.mn[a] = std::min(m.mn[a], m.e[k][a]);
   }
   return m;
 }
@@ -206,9 +211,90 @@ __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __re
   using TO = typename coder_out<CODER>::type;
   static_assert(sizeof(TO) == sizeof(T), "same-width coder");
   constexpr int V = Vec16<T>::V;
+  constexpr int NPZ = NSP == 3 ? 2 : 1, NK = NSP == 3 ? 7 : 3, VP = Vec16<P>::V;
   for (int32_t t = blockIdx.x * kThreads + threadIdx.x; t < items; t += gridDim.x * kThreads) {
     const RowItem q = row_item((uint32_t)t, E0, E1, nch);
     const int32_t oz = q.z, oy = q.y, x0 = q.j * V;
+    // interior item (every class row full and inside, the usual case): all loads of the item
+    // (2 x 2^(d-1) highres vectors, every class's prediction row and, decoding, its coded row)
+    // issued before any compute -- one memory latency per item instead of one per class row.
+    // Measured per call at 512 C3 tiles, the three forms alternating on one box
+    // (profiles/round3/ab_callback_coder_r3s20.log): sample-dtype predictions, encode 249-250 ->
+    // 239-243 us; float32 predictions, decode 382-387 -> 376-382 us.  The other two directions are
+    // slower this way (u16 decode 251 -> 262 us: 81 VGPRs, 6 waves per SIMD instead of 8; float32
+    // encode 373 -> 379 us), so they keep the per-class-row path below
+    constexpr bool kFast = DEC ? sizeof(P) > sizeof(T) : sizeof(P) == sizeof(T);
+    if (kFast && oz < me.mn[0] && oy < me.mn[1] && x0 + V <= me.mn[2] && 2 * x0 + 2 * V <= n2) {
+      Vec16<P> pv[NK][V / VP];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const P* pp = (const P*)preds.p[k] + ((q.b * me.u[k][0] + oz) * me.u[k][1] + oy) * me.u[k][2] + x0;
+#pragma unroll
+        for (int c = 0; c < V / VP; ++c) pv[k][c].load(pp + c * VP);
+      }
+      auto cls_off = [&](int k) { return ((q.b * me.e[k][0] + oz) * me.e[k][1] + oy) * me.e[k][2] + x0; };
+      const int32_t lo_off = ((q.b * E0 + oz) * E1 + oy) * E2 + x0;
+      if constexpr (!DEC) {
+        Vec16<T> h[NPZ][2][2];
+#pragma unroll
+        for (int pz = 0; pz < NPZ; ++pz)
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            const int32_t hoff = ((q.b * n0 + 2 * oz + pz) * n1 + 2 * oy + py) * n2 + 2 * x0;
+            h[pz][py][0].load(src + hoff);
+            h[pz][py][1].load(src + hoff + V);
+          }
+#pragma unroll
+        for (int pz = 0; pz < NPZ; ++pz)
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            Vec16<T> ev, od;
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) {
+              ev.e[i] = h[pz][py][0].e[2 * i]; od.e[i] = h[pz][py][0].e[2 * i + 1];
+              ev.e[V / 2 + i] = h[pz][py][1].e[2 * i]; od.e[V / 2 + i] = h[pz][py][1].e[2 * i + 1];
+            }
+            const int k0 = class_index(NSP, pz, py, 0), k1 = class_index(NSP, pz, py, 1);
+            auto code_row = [&](int k, const Vec16<T>& gt) {
+              Vec16<T> res;
+#pragma unroll
+              for (int i = 0; i < V; ++i) res.e[i] = (T)code_encode<CODER>(to_i32(pv[k][i / VP].e[i % VP]), to_i32(gt.e[i]));
+              res.store((T*)maps_out.p[k] + cls_off(k));
+            };
+            if (k0 < 0) ev.store(dst + lo_off);
+            else code_row(k0, ev);
+            code_row(k1, od);
+          }
+      } else {
+        Vec16<T> lov, en[NK];
+        lov.load(src + lo_off);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) en[k].load((const T*)maps_in.p[k] + cls_off(k));
+#pragma unroll
+        for (int pz = 0; pz < NPZ; ++pz)
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            const int k0 = class_index(NSP, pz, py, 0), k1 = class_index(NSP, pz, py, 1);
+            const int k0c = k0 < 0 ? 0 : k0;
+            Vec16<T> ev, od, a, b2;
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+              ev.e[i] = k0 < 0 ? lov.e[i]
+                               : (T)code_decode<CODER>(to_i32(pv[k0c][i / VP].e[i % VP]), to_i32((TO)en[k0c].e[i]));
+              od.e[i] = (T)code_decode<CODER>(to_i32(pv[k1][i / VP].e[i % VP]), to_i32((TO)en[k1].e[i]));
+            }
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) {
+              a.e[2 * i] = ev.e[i]; a.e[2 * i + 1] = od.e[i];
+              b2.e[2 * i] = ev.e[V / 2 + i]; b2.e[2 * i + 1] = od.e[V / 2 + i];
+            }
+            const int32_t hoff = ((q.b * n0 + 2 * oz + pz) * n1 + 2 * oy + py) * n2 + 2 * x0;
+            a.store(dst + hoff);
+            b2.store(dst + hoff + V);
+          }
+      }
+      continue;
+    }
 #pragma unroll
     for (int pz = 0; pz < (NSP == 3 ? 2 : 1); ++pz)
 #pragma unroll
