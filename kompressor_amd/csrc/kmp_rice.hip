@@ -33,6 +33,10 @@ using namespace pk;
 
 constexpr uint32_t kSumCap = 1u << 20;  // S_k past this can never be the optimum (see plan)
 
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 template <int W>
 __device__ __forceinline__ uint32_t sample_of(const uint32_t (&w)[Sw<W>::NW], int e) {
   if constexpr (W == 8) return (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
@@ -62,6 +66,45 @@ __device__ __forceinline__ void zplanes(const uint32_t (&w)[Sw<W>::NW], uint32_t
     const uint32_t prev = i ? X[(i - 1) >> 1][(i - 1) & 1] : 0u;
     Z[i >> 1][i & 1] = __builtin_amdgcn_alignbit(cur, prev, 24) ^ sg;
   }
+}
+
+// the lane's 8 samples all in [-128, 127] as signed W-bit values (their z < 256)
+template <int W>
+__device__ __forceinline__ bool byte_residuals(const uint32_t (&w)[Sw<W>::NW]) {
+  uint32_t hb = 0;
+  if constexpr (W == 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w[i]) + (u16x2){0x80, 0x80});
+      hb |= t & 0xff00ff00u;
+    }
+  } else if constexpr (W == 32) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hb |= (w[i] + 0x80u) & 0xffffff00u;
+  }
+  return hb == 0;
+}
+
+// zplanes when every sample is in [-128, 127]: plane group 0 only (its sign plane is plane 7, which
+// equals every higher s-plane), the others zero
+template <int W>
+__device__ __forceinline__ void zplanes_lo(const uint32_t (&w)[Sw<W>::NW], uint32_t (&Z)[Sw<W>::NP][2]) {
+  constexpr int NP = Sw<W>::NP;
+  static_assert(W == 16 || W == 32, "8-bit samples have one plane group");
+  uint32_t X0, X1;
+  if constexpr (W == 16) {
+    X0 = perm(w[1], w[0], 0x06040200u);
+    X1 = perm(w[3], w[2], 0x06040200u);
+  } else {
+    X0 = perm(w[1], w[0], 0x0c0c0400u) | perm(w[3], w[2], 0x04000c0cu);
+    X1 = perm(w[5], w[4], 0x0c0c0400u) | perm(w[7], w[6], 0x04000c0cu);
+  }
+  tr8x8(X0, X1);
+  const uint32_t sg = perm(X1, X1, 0x07070707u);
+  Z[0][0] = __builtin_amdgcn_alignbit(X0, 0u, 24) ^ sg;
+  Z[0][1] = __builtin_amdgcn_alignbit(X1, X0, 24) ^ sg;
+#pragma unroll
+  for (int p = 1; p < NP; ++p) Z[p][0] = Z[p][1] = 0u;
 }
 
 // lane j of a block's 8-lane group ends with sum_{m=j..7} x_m 2^(m-j) (row_shl:d reads lane l+d;
@@ -190,9 +233,6 @@ __device__ __forceinline__ uint32_t wave_groups_excl(uint32_t v, int lane, uint3
   return x - v;
 }
 
-typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // q[e] = zigzag(sample e) >> k for the lane's 8 samples; 16-bit samples two at a time (packed
 // 16-bit shifts: zigzag = (s << 1) ^ (s >> 15) per half)
@@ -249,22 +289,38 @@ __global__ void __launch_bounds__(64 * kEncWaves) rice_bundle_encode_kernel(RArr
   for (int st = 0; st < S; ++st) {
     const int64_t blk = blk0 + 8 * st + g8;
     const bool has = blk < R.nb;
-    zplanes<W>(w[st], Zt[st]);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) xtr8(Zt[st][p][0], Zt[st][p][1], j);
     // S_k = sum_i (z_i >> k) = sum_{b >= k} count_b 2^(b - k) for this lane's k = 8p + j: a doubling
     // suffix sum of the plane counts over the group, plus S_{8(p+1)} (group lane 0) << (8 - j).
     // Equal to the Horner recurrence S_k = 2 S_{k+1} + count_k of the oracle (capped at kSumCap
     // for 32-bit samples: min(S_k, cap), which is what the capped recurrence yields)
-    uint32_t key = 0xffffffffu, above = 0;
+    uint32_t key = 0xffffffffu;
+    bool lo = false;
+    if constexpr (NP > 1) {
+      lo = __all(byte_residuals<W>(w[st]));
+      if (lo) {
+        // every sample of the wave step in [-128, 127] (the usual residual map): z < 256, so the
+        // z-planes from 8 up are zero -- transpose and count plane group 0 only; the sign plane
+        // is plane 7; the keys of k >= 8 are those of S_k = 0
+        zplanes_lo<W>(w[st], Zt[st]);
+        xtr8(Zt[st][0][0], Zt[st][0][1], j);
+        const uint32_t sk = group8_suffix2(__builtin_popcount(Zt[st][0][0]) + __builtin_popcount(Zt[st][0][1]), j);
+        key = min(((sk + 95u) & ~31u) + 65u * (uint32_t)j, 64u + 65u * (uint32_t)(8 + j));
+      }
+    }
+    if (!lo) {
+      zplanes<W>(w[st], Zt[st]);
 #pragma unroll
-    for (int p = NP - 1; p >= 0; --p) {
-      const uint32_t c = __builtin_popcount(Zt[st][p][0]) + __builtin_popcount(Zt[st][p][1]);
-      uint32_t sk = group8_suffix2(c, j);
-      if (p < NP - 1) sk += above << (8 - j);
-      if constexpr (W > 16) sk = min(sk, kSumCap);
-      key = min(key, ((sk + 95u) & ~31u) + 65u * (uint32_t)(8 * p + j));
-      if (p > 0) above = group8_first(sk, j);
+      for (int p = 0; p < NP; ++p) xtr8(Zt[st][p][0], Zt[st][p][1], j);
+      uint32_t above = 0;
+#pragma unroll
+      for (int p = NP - 1; p >= 0; --p) {
+        const uint32_t c = __builtin_popcount(Zt[st][p][0]) + __builtin_popcount(Zt[st][p][1]);
+        uint32_t sk = group8_suffix2(c, j);
+        if (p < NP - 1) sk += above << (8 - j);
+        if constexpr (W > 16) sk = min(sk, kSumCap);
+        key = min(key, ((sk + 95u) & ~31u) + 65u * (uint32_t)(8 * p + j));
+        if (p > 0) above = group8_first(sk, j);
+      }
     }
     key = group8_min(key, j);
     // key == 64 <=> k = 0 with 2 words <=> S_0 == 0: an all-zero block
@@ -521,8 +577,12 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
       Z[p][0] = hv ? bp[2 * b] : 0u;
       Z[p][1] = hv ? bp[2 * b + 1] : 0u;
     }
+    // every block of the wave step with k <= 8 (the usual residual map): plane groups from 1 up
+    // hold no stored planes (all zero), so only group 0 is transposed back
+    const bool lo8 = __all(param <= 9);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
+      if (p > 0 && lo8) continue;
       xtr8(Z[p][0], Z[p][1], j);
       tr8x8(Z[p][0], Z[p][1]);
     }
