@@ -1,16 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r3s27; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_packing.py tests/test_gpu_container.py tests/test_gpu_fuzz_rice.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-for lib in libkompressor_hip.so libkompressor_hip_prev.so libkompressor_hip.so libkompressor_hip_prev.so; do
-  rm -rf $O/p
-  KOMPRESSOR_HIP_LIB=$PWD/kompressor_amd/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 tools/rice_time.py 4 20 > $O/run_$lib.log 2>&1 || exit 1
-  echo "== $lib $(tail -1 $O/run_$lib.log)"
-  python3 tools/kcsv.py $(find $O/p -name 'run_kernel_stats.csv' | head -1) rice
-done
-timeout -k 10 300 python tools/bench_rows.py --no-cpu --rows rice > $O/rows.log 2>&1 || exit 1
-grep -h '"rice:noise[0-9]*"' $O/rows.log | python3 -c "
-import sys,json
-for l in sys.stdin:
-    d=json.loads(l); print(d['row'], d['pack_encoded_ms'], d['unpack_encoded_ms'], d['pack_device_us'], d['unpack_device_us'])"
+O=gpurun_out/r3fin1; mkdir -p $O
+step() { local name=$1; shift; timeout -k 10 "$@" > $O/$name.log 2>&1; local rc=$?; echo "[$name] rc=$rc"; return $rc; }
+step debug_parity 600 env KMP_DEBUG=1 python -u -m pytest tests/test_gpu_codec.py tests/test_gpu_linear.py tests/test_packing.py tests/test_gpu_fuzz_rice.py -m gpu -x -q --timeout 120 --timeout-method thread && \
+step bench_n2_gloo 300 env KMP_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-e2e
+rc=$?
+tail -2 $O/debug_parity.log; tail -1 $O/bench_n2_gloo.log | cut -c1-300
+exit $rc

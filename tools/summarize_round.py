@@ -30,9 +30,13 @@ def pmc(kind):
         for r in csv.DictReader(open(f[0])):
             if 'kmp' in r['Kernel_Name']:
                 # the DEC template argument: first of wave2d_u8_kernel<DEC>, second of <T, DEC, ...>
-                args = [a.strip() for a in r['Kernel_Name'].split('<', 1)[1].split('>', 1)[0].split(',')]
-                dec = args[0] if 'u8_kernel' in r['Kernel_Name'] else args[1]
-                direction = 'decode' if dec == 'true' else 'encode'
+                name = r['Kernel_Name']
+                if '<' not in name:  # untemplated kernels name their direction (wave2d_u8_dec_kernel)
+                    direction = 'decode' if '_dec_' in name else 'encode'
+                else:
+                    args = [a.strip() for a in name.split('<', 1)[1].split('>', 1)[0].split(',')]
+                    dec = args[0] if 'u8_kernel' in name else args[1]
+                    direction = 'decode' if dec == 'true' else 'encode'
                 vals[(direction, r['Counter_Name'])].append(float(r['Counter_Value']))
     out = {}
     for d in ('encode', 'decode'):
