@@ -336,6 +336,22 @@ def main():
                  raw + b_r.numel(), t_enc_dev)
             emit(f'rice:noise{int(noise)}:unpack_device', 'rice bundle decode: one launch for lowres + 7 maps',
                  raw + b_r.numel(), t_dec_dev)
+            # the file pipeline on the device, no host synchronisation: compress = the fused encode +
+            # the bundle encode of its outputs, decompress = the bundle decode + the fused decode
+            # (algorithmic bytes: the codec's read + write and the bundle stage's read + write)
+            coder = _nd.NATURAL_CODER[tiles.dtype]
+            lo3, maps3, dims3 = _nd._alloc_encoded(tiles, coder, 3)
+            rec3 = torch.empty_like(tiles)
+            ws3 = torch.empty(max(1, _nd.workspace_bytes(tiles, pred, 3)), dtype=torch.uint8, device='cuda')
+            t_cmp = gpu_time(lambda: (_nd.fused_encode_into(tiles, pred, coder, lo3, maps3, 3, workspace=ws3),
+                                      kpk._rice_encode_launch((lo3, *maps3), dims3)), args.reps)
+            t_dcm = gpu_time(lambda: (kpk._rice_decode_launch(b_r, hb),
+                                      _nd.fused_decode_into(lo, maps, dims, pred, coder, rec3, 3, workspace=ws3)), args.reps)
+            emit(f'rice:noise{int(noise)}:compress_device', 'fused encode + rice bundle encode (device, no sync)',
+                 3 * raw + b_r.numel(), t_cmp)
+            emit(f'rice:noise{int(noise)}:decompress_device', 'rice bundle decode + fused decode (device, no sync)',
+                 3 * raw + b_r.numel(), t_dcm)
+            del lo3, maps3, rec3, ws3
             del tiles, lo, maps, maps2, lo2, b_r, b_p, vol512, res, cnt
         del field
 
