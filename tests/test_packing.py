@@ -343,3 +343,29 @@ def test_rice_bundle_spec_round_trip():
     assert dims == (1, 0)
     for a, b in zip(arrays, back):
         assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_rice_layout_caches_follow_the_shapes_and_bytes(kom):
+    """packing.py caches bundle layouts by the arrays' dtypes / shapes (pack) and by the header
+    bytes (unpack): interleaved packs of differently shaped results give the spec's bytes each
+    time; a cached header with a flipped record or a truncated blob still raises."""
+    from oracle import rice as ORC
+    rng = np.random.default_rng(77)
+    a = [rng.integers(-40, 40, size=s).astype(np.int16).view(np.uint16) for s in [(3, 17, 19), (5000,), (64,)]]
+    b = [rng.integers(0, 256, size=s).astype(np.uint8) for s in [(2, 70000), (1,)]]
+    import torch
+    ta = [torch.from_numpy(x).cuda() for x in a]
+    tb = [torch.from_numpy(x).cuda() for x in b]
+    wa, wb = ORC.pack_bundle(a, (1, 0, 1)), ORC.pack_bundle(b, (1,))
+    for _ in range(2):  # the second round hits the caches
+        ga = kom.packing.pack_encoded(ta[0], (tuple(ta[1:]), (1, 0, 1))).cpu().numpy()
+        gb = kom.packing.pack_encoded(tb[0], (tuple(tb[1:]), (1,))).cpu().numpy()
+        assert np.array_equal(ga, wa) and np.array_equal(gb, wb)
+        for blob, want in ((ga, a), (gb, b)):
+            lo, (maps, _) = kom.packing.unpack_encoded(blob)
+            assert all(np.array_equal(x, y) for x, y in zip((lo, *maps), want))
+    with pytest.raises(ValueError):
+        kom.packing.unpack_encoded(_poke(ga, 80 + 72, '<q', 999))   # record sample count of a cached layout
+    with pytest.raises(ValueError):
+        kom.packing.unpack_encoded(ga[:-8])                          # truncated blob, cached header
