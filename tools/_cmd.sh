@@ -1,7 +1,11 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r3s35; mkdir -p $O
-KMP_FUZZ_RICE_CASES=4000 KMP_FUZZ_SEED0=3000 timeout -k 10 1000 python -u -m pytest tests/test_gpu_fuzz_rice.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/fuzz_rice.log 2>&1 || { tail -20 $O/fuzz_rice.log; exit 1; }
-tail -1 $O/fuzz_rice.log
-KMP_FUZZ_CASES=10000 KMP_FUZZ_SEED0=40000 timeout -k 10 1000 python -u -m pytest tests/test_gpu_fuzz.py tests/test_gpu_fuzz_primitives.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/fuzz.log 2>&1 || { tail -20 $O/fuzz.log; exit 1; }
-tail -1 $O/fuzz.log
+O=gpurun_out/r3s37; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_codec.py -m gpu -x -q --timeout 120 --timeout-method thread -k categorical > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for r in 1 2; do
+for lib in libkompressor_hip.so libkompressor_hip_prev.so; do
+  KOMPRESSOR_HIP_LIB=$PWD/kompressor_amd/$lib timeout -k 10 300 python tools/bench_rows.py --no-cpu --rows categorical > $O/rows_$lib.log 2>&1 || exit 1
+  echo "== $lib $(grep '^{' $O/rows_$lib.log | python3 -c "import sys,json; print(' '.join(json.loads(l)['row'].split(':')[1]+'='+str(json.loads(l)['us']) for l in sys.stdin))")"
+done
+done
