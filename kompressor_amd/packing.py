@@ -59,6 +59,22 @@ _HEAD_MAX = _HEAD.size + 8 * 8       # header + the largest shape (ndim <= 8)
 _SAMPLE_BITS = {1: 8, 2: 16, 4: 32}
 
 
+_HOST_HEAD = None  # a pinned staging buffer for header reads (reused: every read synchronises)
+
+
+def _head_bytes(b, n):
+    """The first ``n`` bytes of the device blob ``b`` on the host: one copy into a reused pinned
+    buffer and one stream synchronisation (a pageable ``.cpu()`` copy costs a fresh allocation)."""
+    global _HOST_HEAD
+    n = min(int(n), b.numel())
+    if _HOST_HEAD is None or _HOST_HEAD.numel() < n:
+        _HOST_HEAD = torch.empty((max(n, 4096),), dtype=torch.uint8, pin_memory=True)
+    _HOST_HEAD[:n].copy_(b[:n], non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    return _HOST_HEAD[:n].numpy().tobytes()
+
+
+
 def _pad8(n):
     return (n + 7) // 8 * 8
 
@@ -263,7 +279,7 @@ def _rice_arrays_n(ns, offs, first, count):
 def _rice_pack_bundle(arrays, dims):
     out, poff, launched, keep = _rice_encode_launch(arrays, dims)
     if launched:  # the kernel zeroes the side arrays' and the payload's padding
-        words, total = out[56:72].view(torch.int64).tolist()  # the one synchronisation
+        words, total = struct.unpack('<2q', _head_bytes(out[56:72], 16))  # the one synchronisation
     else:
         total = poff
     del keep
@@ -455,7 +471,7 @@ def pack(x, method='rice'):
 def unpack(blob):
     """Inverse of :func:`pack`: the array, bit for bit."""
     b, kind = dev.to_device(blob)
-    hb = b[:min(b.numel(), 4096)].cpu().numpy().tobytes()
+    hb = _head_bytes(b, 4096)
     if hb[:4] == BUNDLE_MAGIC:
         arrays, _ = _rice_unpack_bundle(b, hb)
         if len(arrays) != 1:
@@ -493,7 +509,7 @@ def pack_encoded(lowres, encoded, method='rice'):
 def unpack_encoded(blob):
     """Inverse of :func:`pack_encoded`: ``(lowres, (maps, dims))``."""
     b, kind = dev.to_device(blob)
-    hb = b[:min(b.numel(), 4096)].cpu().numpy().tobytes()
+    hb = _head_bytes(b, 4096)
     if len(hb) < 12:
         raise ValueError('truncated bundle')
     magic, version, count, nsp = struct.unpack('<4sHHI', hb[:12])
