@@ -295,6 +295,51 @@ __global__ void __launch_bounds__(kThreads) rows_code_preds_kernel(const T* __re
       }
       continue;
     }
+    // the sample-dtype decode's interior items: the loads of one highres plane parity (up to 4
+    // class rows and their prediction rows) issued together -- twice the loads in flight of the
+    // per-class-row path at its register budget (the all-loads-first form needs 81 VGPRs)
+    if constexpr (DEC && std::is_same<P, T>::value) {
+      if (oz < me.mn[0] && oy < me.mn[1] && x0 + V <= me.mn[2] && 2 * x0 + 2 * V <= n2) {
+        auto cls_off = [&](int k) { return ((q.b * me.e[k][0] + oz) * me.e[k][1] + oy) * me.e[k][2] + x0; };
+        auto pred_off = [&](int k) { return ((q.b * me.u[k][0] + oz) * me.u[k][1] + oy) * me.u[k][2] + x0; };
+        const int32_t lo_off = ((q.b * E0 + oz) * E1 + oy) * E2 + x0;
+#pragma unroll
+        for (int pz = 0; pz < NPZ; ++pz) {
+          Vec16<T> en[2][2], pr[2][2];
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            const int k0 = class_index(NSP, pz, py, 0), k1 = class_index(NSP, pz, py, 1);
+            if (k0 < 0) {
+              en[py][0].load(src + lo_off);
+            } else {
+              en[py][0].load((const T*)maps_in.p[k0] + cls_off(k0));
+              pr[py][0].load((const T*)preds.p[k0] + pred_off(k0));
+            }
+            en[py][1].load((const T*)maps_in.p[k1] + cls_off(k1));
+            pr[py][1].load((const T*)preds.p[k1] + pred_off(k1));
+          }
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            const int k0 = class_index(NSP, pz, py, 0);
+            Vec16<T> a, b2;
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) {
+              auto dec0 = [&](int e) {
+                return k0 < 0 ? en[py][0].e[e]
+                              : (T)code_decode<CODER>(to_i32(pr[py][0].e[e]), to_i32((TO)en[py][0].e[e]));
+              };
+              auto dec1 = [&](int e) { return (T)code_decode<CODER>(to_i32(pr[py][1].e[e]), to_i32((TO)en[py][1].e[e])); };
+              a.e[2 * i] = dec0(i); a.e[2 * i + 1] = dec1(i);
+              b2.e[2 * i] = dec0(V / 2 + i); b2.e[2 * i + 1] = dec1(V / 2 + i);
+            }
+            const int32_t hoff = ((q.b * n0 + 2 * oz + pz) * n1 + 2 * oy + py) * n2 + 2 * x0;
+            a.store(dst + hoff);
+            b2.store(dst + hoff + V);
+          }
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int pz = 0; pz < (NSP == 3 ? 2 : 1); ++pz)
 #pragma unroll
