@@ -187,38 +187,57 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_select_kern
 
 // ---- 16-byte vector form (L % 4 == 0, L <= 256 * E4, rows 16-B aligned) -----------------------
 // Lane l holds classes s * 256 + 4 l + q (q = 0..3) of slot s as one float4: one 16-B load per lane
-// and slot instead of four 4-B loads; classes past L are loaded as NaN.  Each wave walks its
-// elements (wave-uniform indices: loop control and addressing on the scalar unit) with a ring of
-// kCatPF rows in registers, refilling a slot as soon as it is ranked.  The VALU work per element
-// is what bounds this kernel, so:
+// and slot instead of four 4-B loads; classes past L are loaded as NaN.  Each wave walks one
+// contiguous range of elements (loop control and addressing on the scalar unit) with a ring of
+// kCatPF rows -- and their values, in a VGPR -- in registers, refilling a slot as soon as it is
+// ranked.  (A value read as a uniform scalar load was waited out at the load: every element paid a
+// memory latency, 260 / 390 us per 1 M x 256 encode / decode; with the value in the ring 190 /
+// 380 us.)  Instruction issue per element is what bounds this kernel, so:
 //   encode: #{j : l_j < l_i, or l_j == l_i and j < i} from two float compares per class (NaN rows
 //   of the reference order handled by a uniform branch; padding NaNs never count), the j < i part
 //   as a scalar lane mask.
 //   decode: order_key integers; rank 0 by one wave max; otherwise a 256-bin histogram (LDS
 //   atomics) of the 8 highest bits in which the keys differ (DPP OR-reduce), a DPP prefix scan
-//   over the bins to pick the one that holds rank k, and a bitwise radix select inside that bin,
-//   stopping as soon as the key range [t, hi) that holds rank k contains one key.  Then the m-th
-//   highest class index with a key in [t, hi).
-constexpr int kCatPF = 4;  // 8 measured no faster (the loads are not what bounds it)
+//   over the bins to pick the one that holds rank k (its lane by one ballot, the bin inside the
+//   lane on the scalar unit), and a bitwise radix select inside that bin, stopping as soon as the
+//   key range [t, hi) that holds rank k contains one key.  Then the m-th highest class index with
+//   a key in [t, hi).
+constexpr int kCatPF = 4;  // 8 measured no faster (r3s54: decode 394-397 vs 376-385 us)
 typedef float cat_f32x4 __attribute__((ext_vector_type(4)));
 
 template <int E4>
 struct CatRow {
   cat_f32x4 v[E4];
-  int64_t x;
+  uint32_t xv;  // the element's value (gt / enc), raw 32-bit pattern, in a VGPR
 };
 
+// The value is read as the aligned dword that holds it (cat_xval shifts it out when the element
+// is ranked), through an address with a divergent zero (zero0 below): a wave-uniform load, or a
+// sub-dword one, is moved to a scalar register or masked right at the load, which waits the load
+// out there instead of when the element is ranked PF elements later.
 template <typename T, int E4, bool FULL>
-__device__ __forceinline__ void cat_load(const float* __restrict__ logits, int64_t L, const T* __restrict__ x,
-                                         int64_t el, int lane, CatRow<E4>& r) {
-  const cat_f32x4* row = (const cat_f32x4*)(logits + el * L);
+__device__ __forceinline__ void cat_load(const cat_f32x4* __restrict__ row, const T* __restrict__ xe, int64_t L,
+                                         int lane, uint32_t zero0, CatRow<E4>& r) {
   const float qnan = __builtin_nanf("");
 #pragma unroll
   for (int s = 0; s < E4; ++s) {
     const int c4 = s * 64 + lane;
     r.v[s] = FULL || 4 * c4 < L ? __builtin_nontemporal_load(row + c4) : (cat_f32x4){qnan, qnan, qnan, qnan};
   }
-  r.x = std::is_signed<T>::value ? (int64_t)x[el] : (int64_t)(uint64_t)x[el];
+  // the dword lies in the same page as the element: reading its other bytes cannot fault
+  const char* a = (const char*)xe;
+  a -= (uintptr_t)a & 3;  // scalar; pointer arithmetic keeps it a global (not flat) load
+  r.xv = *(const uint32_t*)(a + zero0);  // scalar base + 32-bit vector offset: no address VALU
+}
+template <typename T>
+__device__ __forceinline__ int64_t cat_xval(const T* xe, uint32_t word) {  // xe: the element's value
+  if constexpr (sizeof(T) == 4) {
+    return std::is_signed<T>::value ? (int64_t)(int32_t)word : (int64_t)word;
+  } else {
+    static_assert(!std::is_signed<T>::value, "sub-dword value dtypes are unsigned");
+    const uint32_t sh = (uint32_t)((uintptr_t)xe & 3) * 8;
+    return (int64_t)((word >> sh) & ((1u << (8 * sizeof(T))) - 1));
+  }
 }
 
 // DPP steps (row_shr:1,2,4,8 inside rows of 16, then row_bcast:15 / row_bcast:31 across rows):
@@ -253,10 +272,10 @@ __device__ __forceinline__ uint64_t lanes_below(int nl) {  // mask of lanes 0 ..
 }
 
 template <typename T, int DIR, int E4, bool FULL>
-__device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins, int peel,
-                                         T* __restrict__ out, int64_t el) {
+__device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins, int peel,
+                                      int64_t xv) {  // the element's code (wave-uniform)
   if constexpr (DIR == KMP_ENCODE) {
-    const int64_t g = cur.x;
+    const int64_t g = xv;
     int64_t best = -1;
     if (g >= 0)
       for (int64_t i = g; i < L; i += class_mod<T>()) {
@@ -297,7 +316,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
         const int64_t p = L - 1 - (int64_t)asc;
         best = (best < 0 || p < best) ? p : best;
       }
-    if (lane == 0) out[el] = (T)(best < 0 ? 0 : best);
+    return (T)(best < 0 ? 0 : best);
   } else {
     uint32_t key[E4][4];
     bool ok[E4][4];
@@ -331,7 +350,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
         for (int q = 0; q < 4; ++q) c += __popcll(__ballot(pred(key[s][q])));
       return c;
     };
-    const int64_t kk = cur.x;
+    const int64_t kk = xv;
     const uint32_t k = (uint32_t)(kk < 0 ? 0 : (kk >= L ? L - 1 : kk));
     uint32_t t = 0, m = 0;
     uint64_t hi = 1ull << 32;  // the answer's key lies in [t, hi); m = its rank among those keys
@@ -358,8 +377,9 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
     } else {
       // radix select on digits of up to 8 bits from the top of the bits in which the keys differ
       // (P of them below the common prefix): per round a 256-bin LDS histogram of the digit over
-      // the keys in the current range [t, hi), a DPP scan over the bins (descending digit order:
-      // bin 255 - digit), the bin that holds rank k; the range narrows to that bin.  Stops when
+      // the keys in the current range [t, hi) (bin = digit, one bit-field extract per key), a DPP
+      // scan over the bins in descending digit order, the bin that holds rank k; the range narrows
+      // to that bin.  Stops when
       // the bin holds one key or the digits run out (ties).  Two rounds isolate the key for
       // softmax rows, whose first digit is mostly exponent bits (up to half the keys in one bin)
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[0][0]);  // class 0 exists
@@ -377,33 +397,44 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
         *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
         __builtin_amdgcn_wave_barrier();
         const uint32_t dm = (1u << wd) - 1u;
-        const uint32_t hm = sh + wd >= 32 ? 0u : ~0u << (sh + wd);  // the range: key & hm == t & hm
+        if (round == 0) {
 #pragma unroll
-        for (int s = 0; s < E4; ++s)
+          for (int s = 0; s < E4; ++s)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (ok[s][q] && (round == 0 || ((key[s][q] ^ t) & hm) == 0))
-              atomicAdd(bins + (255 - ((key[s][q] >> sh) & dm)), 1u);
+            for (int q = 0; q < 4; ++q)
+              if (ok[s][q]) atomicAdd(bins + __builtin_amdgcn_ubfe(key[s][q], (uint32_t)sh, (uint32_t)wd), 1u);
+        } else {  // keys in the range [t, t + 2^(sh + wd)): (key >> sh) - (t >> sh) <= dm, and that is the digit
+          const uint32_t lo = t >> sh;
+#pragma unroll
+          for (int s = 0; s < E4; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t d = (key[s][q] >> sh) - lo;
+              if (ok[s][q] && d <= dm) atomicAdd(bins + d, 1u);
+            }
+        }
         __builtin_amdgcn_wave_barrier();
-        const uint4 b = *(const uint4*)(bins + 4 * lane);
-        const uint32_t tot = b.x + b.y + b.z + b.w;
+        // bins in ascending digit order; lane l takes digits 255 - 4 l down to 252 - 4 l
+        const uint4 bu = *(const uint4*)(bins + 4 * (63 - lane));
+        const uint32_t tot = bu.x + bu.y + bu.z + bu.w;
         const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
-        const uint32_t base = incl - tot;
         const uint32_t r = k - c_hi;
-        const uint64_t hit = __ballot(base <= r && r < incl);
-        const int ls = (int)__builtin_ctzll(hit);
-        // inside the lane: the bin whose cumulative range holds r
-        uint32_t cb = base, cnt = b.x, q = 0;
-        if (r >= cb + b.x) {
-          cb += b.x; cnt = b.y; q = 1;
-          if (r >= cb + b.y) {
-            cb += b.y; cnt = b.z; q = 2;
-            if (r >= cb + b.z) { cb += b.z; cnt = b.w; q = 3; }
+        const int ls = (int)__builtin_ctzll(__ballot(r < incl));  // the first lane past r (incl ascends)
+        // inside that lane, on the scalar unit: the bin whose cumulative range holds r
+        uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)(incl - tot), ls);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bu.w, ls);
+        const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)bu.z, ls);
+        const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)bu.y, ls);
+        const uint32_t b3 = (uint32_t)__builtin_amdgcn_readlane((int)bu.x, ls);
+        uint32_t cnt = b0, q = 0;
+        if (r >= cb + b0) {
+          cb += b0; cnt = b1; q = 1;
+          if (r >= cb + b1) {
+            cb += b1; cnt = b2; q = 2;
+            if (r >= cb + b2) { cb += b2; cnt = b3; q = 3; }
           }
         }
-        c_hi += (uint32_t)__builtin_amdgcn_readlane((int)cb, ls);
-        cnt = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ls);
-        q = (uint32_t)__builtin_amdgcn_readlane((int)q, ls);
+        c_hi += cb;
         const uint32_t digit = (255u - (uint32_t)(4 * ls + (int)q)) & dm;
         t |= digit << sh;
         if (cnt <= 1 || sh == 0) break;
@@ -418,13 +449,16 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
     // the m-th highest class index among the classes with key in [t, hi); padding keys (0) are
     // below every valid key (>= 1), so the range starts at 1 at the least
     const uint32_t tlo = t > 0 ? t : 1u;
+    // key in [tlo, hi) as one unsigned compare: key - tlo <= span (hi - 1 < tlo: no key, no class)
+    const bool none = hi - 1 < (uint64_t)tlo;
+    const uint32_t span = (uint32_t)(hi - 1 - tlo);
     int64_t cls = 0;
     for (int s = E4 - 1; s >= 0; --s) {
       uint64_t w[4];
       uint32_t tot = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        w[q] = __ballot(key[s][q] >= tlo && (uint64_t)key[s][q] < hi);
+        w[q] = none ? 0ull : __ballot(key[s][q] - tlo <= span);
         tot += __popcll(w[q]);
       }
       if (m >= tot) {
@@ -448,7 +482,7 @@ __device__ __forceinline__ void cat_rank(const CatRow<E4>& cur, int64_t L, int l
       }
       break;
     }
-    if (lane == 0) out[el] = (T)cls;
+    return (T)cls;
   }
 }
 
@@ -460,24 +494,63 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
   uint32_t* bins = bins_all[wv];
-  const int64_t ws = (int64_t)gridDim.x * kCatWaves;
-  const int64_t el0 = (int64_t)blockIdx.x * kCatWaves + wv;
-  if (el0 >= n) return;
+  // each wave codes one contiguous range of elements
+  const int64_t nw = (int64_t)gridDim.x * kCatWaves;
+  const int64_t per = (n + nw - 1) / nw;
+  const int64_t b = ((int64_t)blockIdx.x * kCatWaves + wv) * per;
+  const int64_t end = b + per < n ? b + per : n;
+  if (b >= end) return;
+  // Element b + j sits in ring[j % PF]: it is ranked in place and its slot reloaded right after,
+  // so no register copies tie a wait to the newest load, and every load of the main loop is issued
+  // (the loop stops PF elements before the range's end) so the outstanding count at each use is
+  // the same PF - 1.  Row, value and code pointers advance on the scalar unit.
+  const uint32_t zero0 = (threadIdx.x >> 6) - (uint32_t)wv;  // 0, but not provably wave-uniform
+  const int64_t L4 = L / 4;
+  const cat_f32x4* rp = (const cat_f32x4*)logits + b * L4;
+  const T* xp = x + b;
+  T* op = out + b;
+  int64_t e = b;
   CatRow<E4> ring[PF];
+  auto rank = [&](int u, const T* xe) {
+    const uint32_t xw = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[u].xv);
+    return cat_rank<T, DIR, E4, FULL>(ring[u], L, lane, bins, peel, cat_xval<T>(xe, xw));
+  };
+  const bool main = b + 2 * PF <= end;
+  if (main) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) cat_load<T, E4, FULL>(rp + u * L4, xp + u, L, lane, zero0, ring[u]);
+    do {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const T code = rank(u, xp + u);
+        if (lane == 0) op[u] = code;
+        cat_load<T, E4, FULL>(rp + (u + PF) * L4, xp + u + PF, L, lane, zero0, ring[u]);
+      }
+      rp += PF * L4;
+      xp += PF;
+      op += PF;
+      e += PF;
+    } while (e + 2 * PF <= end);
+  } else {
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (e + u < end) cat_load<T, E4, FULL>(rp + u * L4, xp + u, L, lane, zero0, ring[u]);
+  }
+  // the range's last elements (PF to 2 PF - 1 after the main loop, fewer without it): ring[u]
+  // holds element e + u; reload a slot only while elements remain
 #pragma unroll
   for (int u = 0; u < PF; ++u)
-    if (el0 + u * ws < n) cat_load<T, E4, FULL>(logits, L, x, el0 + u * ws, lane, ring[u]);
-  for (int64_t base = el0; base < n; base += PF * ws) {
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int64_t e = base + u * ws;
-      if (e >= n) break;
-      const CatRow<E4> cur = ring[u];
-      const int64_t ep = e + PF * ws;
-      if (ep < n) cat_load<T, E4, FULL>(logits, L, x, ep, lane, ring[u]);
-      cat_rank<T, DIR, E4, FULL>(cur, L, lane, bins, peel, out, e);
+    if (e + u < end) {
+      const T code = rank(u, xp + u);
+      if (lane == 0) op[u] = code;
+      if (e + u + PF < end) cat_load<T, E4, FULL>(rp + (u + PF) * L4, xp + u + PF, L, lane, zero0, ring[u]);
     }
-  }
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+    if (e + PF + u < end) {
+      const T code = rank(u, xp + PF + u);
+      if (lane == 0) op[PF + u] = code;
+    }
 }
 
 }  // namespace kmp

@@ -421,6 +421,37 @@ def test_categorical_coder_vs_oracle(kom, vec):
                               oracle.common.decode_categorical(logits, x)), L
 
 
+@pytest.mark.parametrize('L,dt,rows', [(8, np.uint8, None), (8, np.uint16, None), (12, np.int32, None),
+                                       (260, np.uint16, 3000), (256, np.uint8, 3000)])
+def test_categorical_long_ranges(kom, L, dt, rows):
+    """Enough elements that every wave of the vector kernels codes a long contiguous range (8 192
+    waves x 139 elements, the last range ragged): whole batches of 64 values and codes, whole
+    prefetch rounds, and a tail of 3.  Small L: every element vs the oracle; large L: all elements
+    through the round trip and `rows` sampled elements (with every range's first and last) vs the
+    oracle."""
+    import oracle
+    n = 8192 * 139 - 5
+    rng = np.random.default_rng(11)
+    lg = torch.rand((n, L), device='cuda')
+    lg[::11, 1] = lg[::11, 0]  # ties
+    lg[::13] = torch.softmax(lg[::13] * 8, dim=1)
+    xh = rng.integers(0, L, n).astype(dt)
+    xg = torch.from_numpy(xh).cuda()
+    enc = kom.utils.encode_categorical(lg, xg)
+    dec = kom.utils.decode_categorical(lg, enc).cpu().numpy()
+    assert np.array_equal(dec, xh)  # every x < L <= 2^bits: decode inverts encode
+    if rows is None:
+        idx = np.arange(n)
+    else:
+        ends = np.arange(0, n, 139)
+        idx = np.unique(np.concatenate([ends, np.minimum(ends + 138, n - 1), rng.integers(0, n, rows)]))
+    lh = lg[torch.from_numpy(idx).cuda()].cpu().numpy()
+    assert np.array_equal(enc.cpu().numpy()[idx], oracle.common.encode_categorical(lh, xh[idx]))
+    r = rng.integers(0, L, n).astype(dt)  # uniform ranks
+    rd = kom.utils.decode_categorical(lg, torch.from_numpy(r).cuda()).cpu().numpy()
+    assert np.array_equal(rd[idx], oracle.common.decode_categorical(lh, r[idx]))
+
+
 @pytest.mark.parametrize('shape,dtype,p', [
     ((1, 6, 8, 512, 1), np.uint16, 0),    # 64 lanes per output row: one-row waves (both halos)
     ((2, 7, 5, 512, 1), np.uint16, 0),    # odd depth / height
