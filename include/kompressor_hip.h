@@ -307,6 +307,14 @@ int kmp_rice_bundle_decode(int32_t dtype, const kmp_rice_array* arrays, int32_t 
                            const uint8_t* bundle, int64_t payload_off, uint64_t payload_words,
                            unsigned long long* bad, kmp_stream_t stream);
 
+/* CRC-32 (zlib / IEEE: reflected 0xEDB88320, init and final xor 0xFFFFFFFF; == zlib.crc32) of   */
+/* ``data`` into the device uint32 *crc_out (kmp_crc.hip): the container file's integrity check    */
+/* (container.py; the reference has no file format, volume/encode_decode.py:56   */
+/* returns arrays in memory).  ``n_max`` bytes are covered, or -- when ``n_dev`` is a device       */
+/* int64 -- min(*n_dev, n_max), the length read by the kernel (a bundle's size field, no host sync). */
+/* ``data`` 16-byte aligned.  One memset of *crc_out + one launch.                               */
+int kmp_crc32(const uint8_t* data, int64_t n_max, const int64_t* n_dev, uint32_t* crc_out, kmp_stream_t stream);
+
 /* Bit-plane side-information check (the planes format): count the blocks whose stored widths   */
 /* no encoder produces (> W) -- format 0 -- or, format 1, Rice params / bw -- into the uint64 at  */
 /* workspace + kmp_pack_total_offset(n) + 8, beside the payload length of the last scan          */

@@ -107,6 +107,7 @@ _PROTOS = {
     'kmp_rice_bundle_workspace_bytes': (ctypes.c_int64, [_i64]),
     'kmp_rice_bundle_encode': (ctypes.c_int, [_i32, _vp, _i32, _i64, _i64, _vp, _i64, _vp, _vp]),
     'kmp_rice_bundle_decode': (ctypes.c_int, [_i32, _vp, _i32, _i64, _vp, _i64, ctypes.c_uint64, _vp, _vp]),
+    'kmp_crc32': (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp]),
     'kmp_decode_with_predictions': (ctypes.c_int, [_i32, _i32, _i32, _vp, _vpp, _i64, _i64p, _i64, _i32p, _vpp,
                                                    _vp, _vp]),
     'kmp_encode_with_predictions_typed': (ctypes.c_int, [_i32, _i32, _i32, _i32, _vp, _i64, _i64p, _i64, _vpp, _vp,

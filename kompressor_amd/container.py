@@ -106,9 +106,13 @@ def _read(path):
         if len(head) < _HEAD.size:
             raise ValueError(f'{path}: not a kompressor_amd file (too short)')
         magic, version, _, mlen = _HEAD.unpack(head)
-        if magic != MAGIC or version != VERSION or mlen > (1 << 26):
+        if magic != MAGIC or version not in (1, VERSION) or mlen > (1 << 26):
             raise ValueError(f'{path}: not a kompressor_amd file (magic {magic!r}, version {version})')
         meta = json.loads(f.read(mlen).decode())
+        if version == 1 and meta.get('method') != 'planes':
+            # version-1 'rice' payloads were the per-array KMPR format, replaced by the v2 bundle;
+            # version-1 'planes' payloads are unchanged and still read
+            raise ValueError(f'{path}: a version-1 rice file (the retired per-array KMPR format): re-compress it')
         body = np.fromfile(f, dtype=np.uint8, count=int(meta['bundle_bytes']))
     if body.size != meta['bundle_bytes']:
         raise ValueError(f'{path}: truncated ({body.size} of {meta["bundle_bytes"]} payload bytes)')

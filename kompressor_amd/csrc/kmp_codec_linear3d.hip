@@ -443,11 +443,376 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #undef KMP_CH
 }
 
+// ---------------------------------------------------------------------------------------------
+// The y-rolling form (FULL tiles whose rows split into whole wave steps, e.g. C3's 64^3): one wave
+// owns one output plane and walks it in STEPS steps of ``rows`` lowres rows, the loads of step
+// s+1 in flight while step s computes.  The row-below node values come from the lanes one row down
+// by ONE rotation (lane L reads lane L + txn mod 64; the step's last row reads the next step's first
+// row, which is already loaded), and the row-above channels (3, 9, 10, 16 of plane c, 17 of plane
+// c-1) by the opposite rotation (the first row reads the previous step's last row, carried in
+// registers): no halo rows, no LDS and no barrier, and 6 loads per lane per step (encode) where the
+// plane-block form issues 9.  The arithmetic per cell -- the k-ordered fma chains, casts, masks,
+// aggregation and coder -- is the FULL body of linear3d_kernel, so the results are bit-identical.
+
+// the VX node values of a lane's row segment packed into 8 bytes: the decode's lowres row as
+// loaded; the encode's highres row keeps its even elements (one byte permute per dword)
+template <typename T>
+__device__ __forceinline__ uint2 node_words(const uint2& v) { return v; }
+template <typename T>
+__device__ __forceinline__ uint2 node_words(const uint4& v) {
+  constexpr uint32_t sel = sizeof(T) == 2 ? 0x05040100u : 0x06040200u;
+  return make_uint2(__builtin_amdgcn_perm(v.y, v.x, sel), __builtin_amdgcn_perm(v.w, v.z, sel));
+}
+
+// lane L reads lane addr/4 of ``v``.  Call it as a statement of its own, never inside one arm of
+// a per-lane select: the empty volatile asm pins the permute where it is written, with every lane
+// active (inside ``r0 ? prev : rot(v)`` it runs with the r0 lanes disabled, and a permute that
+// reads a disabled lane returns a stale value)
+__device__ __forceinline__ uint32_t rot(uint32_t v, int addr) {
+  uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+template <typename T, bool DEC, int STEPS, int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) linear3y_kernel(L3 a) {
+  constexpr int VX = 8 / (int)sizeof(T);
+  static_assert(VX == 4 || VX == 8, "u16 / u8");
+  constexpr int G = VX / 4;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+  const CFloat Wc = (CFloat)a.W, Bc = (CFloat)a.b;
+
+  const int lane = threadIdx.x;
+  const int tx = lane & (a.txn - 1);
+  const int r = lane / a.txn;
+  const int rows = a.rows;
+  const int X = tx * VX;
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int nplanes = a.zend - a.zbegin;
+  const int c = a.zbegin + blk % nplanes;
+  const int64_t b = blk / nplanes;
+  const bool xlast = tx == a.txn - 1;
+  const bool r0 = r == 0, rlast = r == rows - 1;
+  const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+  const CFloat Zc = (CFloat)kZeroWeights;
+  const CFloat WcP0 = !vz1 ? Zc : Wc, BcP0 = !vz1 ? Zc + 152 : Bc;
+  const CFloat WcQ0 = !vz0 ? Zc : Wc, BcQ0 = !vz0 ? Zc + 152 : Bc;
+  const int adn = ((lane + a.txn) & 63) << 2, aup = ((lane - a.txn) & 63) << 2;
+
+  const int hplane = a.H * a.W_;
+  const int lplane = a.Ey * a.Ex;
+  const int hx = 2 * X;
+  // Addresses: a uniform (scalar) base per row stream plus ONE 32-bit lane offset per layout, so the
+  // loads and stores take the scalar-base form (no 64-bit vector address arithmetic per access)
+  // and no per-stream 64-bit pointers occupy vector registers.  Node rows of node planes c-1, c,
+  // c+1: a lowres row is one row of the decode's lowres / two rows of the encode's highres.
+  constexpr int SZ = (int)sizeof(T);
+  const int nstride = DEC ? a.Ex : 2 * a.W_;  // elements per lowres row in the node planes
+  const uint32_t lon = (uint32_t)((r * nstride + (DEC ? X : hx)) * SZ);  // node / stream / highres rows
+  const uint32_t lonx = (uint32_t)((DEC ? X : hx) * SZ);                 // the same at row 0
+  const uint32_t lom = (uint32_t)((r * a.Ex + X) * SZ);                  // lowres / map rows
+  const uint32_t loh = (uint32_t)((2 * r * a.W_ + hx) * SZ);             // highres rows (the decode's output)
+  const char* un[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int q = c - 1 + t;
+    const int zq = lsrc(q < 0 ? 0 : q, a.Lz, a.Ez);
+    un[t] = DEC ? (const char*)a.lo_in + (b * a.Ez + zq) * (int64_t)lplane * SZ
+                : (const char*)a.hi_in + (b * a.D + 2 * zq) * (int64_t)hplane * SZ;
+  }
+  // encode: the stream rows (plane 2c row 2Y+1, plane 2c+1 rows 2Y / 2Y+1; plane 2c+1 is plane 2c
+  // again where the tile has no such plane); decode: the 7 map rows (a map's missing last cell plane
+  // clamped to the one before: the masks discard it)
+  const char* us = DEC ? nullptr : (const char*)a.hi_in + (b * a.D + 2 * c) * (int64_t)hplane * SZ;
+  const int p1 = (2 * c + 1 < a.D ? hplane : 0) * SZ;
+  char* um[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    int par[3];
+    map_parity(3, k, par);
+    const int ez = par[0] ? a.Lcz : a.Ez;
+    const int cz = par[0] ? (c < a.Lcz ? c : a.Lcz - 1) : c;
+    um[k] = (char*)a.maps.p[k] + (b * ez + cz) * (int64_t)lplane * SZ;  // FULL: every map is Ey x Ex
+  }
+  char* ulo = DEC ? nullptr : (char*)a.lo_out + (b * a.Ez + c) * (int64_t)lplane * SZ;
+  char* uho = DEC ? (char*)a.hi_out + (b * a.D + 2 * c) * (int64_t)hplane * SZ : nullptr;
+  const int nstep = rows * nstride * SZ, mstep = rows * a.Ex * SZ, hstep = rows * 2 * a.W_ * SZ;
+
+  // node rows: a ring of three steps -- the current one, the next (its first row is the current
+  // last row's row below) and the one after, in flight; stream / map rows: the next step's in flight
+  V cur[3], nxt[3], nx2[3];
+  uint4 cs[3], ns[3];  // encode stream rows e1, o0, o1
+  uint2 cm[7], nm[7];  // decode map rows
+  auto load_nodes = [&](int s, V (&o)[3]) {
+    // the step past the last reads the mirrored row Ey - 1 (only row 0's values are used)
+    const bool past = s >= STEPS;
+    const int so = past ? (a.Ey - 1) * nstride * SZ : s * nstep;
+    const uint32_t lo = past ? lonx : lon;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if constexpr (DEC) o[t] = ld8c(un[t] + so + lo);
+      else o[t] = ld16c(un[t] + so + lo);
+    }
+  };
+  auto load_rest = [&](int s, uint4 (&os)[3], uint2 (&om)[7]) {
+    if constexpr (DEC) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) om[k] = ld8(um[k] + s * mstep + lom);
+    } else {
+      const char* p = us + s * hstep;
+      const int rw = a.W_ * SZ;
+      os[0] = ld16(p + rw + lon);
+      os[1] = ld16(p + p1 + lon);
+      os[2] = ld16(p + p1 + rw + lon);
+    }
+  };
+  load_nodes(0, cur);
+  load_rest(0, cs, cm);
+  load_nodes(1, nxt);
+
+  // The channels 3, 9, 10, 16 (plane c) and 17 (plane c-1) that row Y+1 reads from row Y go
+  // through an LDS ring of rows + 1 row slots (row Y in slot Y mod (rows + 1)): a step writes its
+  // rows' channels, then reads the slots of the rows above -- the previous step's last row is in a
+  // slot the current step does not overwrite.  Slot rows (row -1) starts zeroed: row 0 has no row
+  // above.  One wave per workgroup: its own LDS accesses are ordered, so no barrier.
+  extern __shared__ __attribute__((aligned(16))) uint32_t xring[];  // [rows + 1][txn][kXch][VX]
+  const int xslot = a.txn * kXch * VX;  // words per row slot
+  if (r0) {
+#pragma unroll
+    for (int q = 0; q < kXch; ++q)
+#pragma unroll
+      for (int i = 0; i < VX; ++i) xring[rows * xslot + (tx * kXch + q) * VX + i] = 0;
+  }
+  int wslot = r;  // Y mod (rows + 1): rows advance by rows == -1 (mod rows + 1) per step
+
+#pragma unroll 1
+  for (int s = 0; s < STEPS; ++s) {
+    if (s + 2 <= STEPS) load_nodes(s + 2, nx2);
+    if (s + 1 < STEPS) load_rest(s + 1, ns, nm);
+    // the weights are re-read (scalar loads, cache hits) in every step rather than hoisted out of
+    // the loop: 171 values do not fit the scalar register file
+    CFloat WcP = WcP0, BcP = BcP0, WcQ = WcQ0, BcQ = BcQ0;
+    asm volatile("" : "+s"(WcP), "+s"(BcP), "+s"(WcQ), "+s"(BcQ));
+    const int Y = s * rows + r;
+    const bool vy0 = Y >= 1;
+
+    // ---- node values: own row Y, row Y+1 (one rotation: the step's last row reads the next's first) ----
+    f32x2 NP[3][G][3], NP1[3][G][3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const uint2 nw = node_words<T>(cur[t]);
+      const uint2 nn = node_words<T>(nxt[t]);
+      const uint2 dw = make_uint2(rot(r0 ? nn.x : nw.x, adn), rot(r0 ? nn.y : nw.y, adn));
+      float nY[VX + 1], nY1[VX + 1];
+      uint32_t n[VX], nd[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        n[i] = el8<T>(nw, i);
+        nd[i] = el8<T>(dw, i);
+        nY[i] = (float)n[i];
+        nY1[i] = (float)nd[i];
+      }
+      uint32_t nx = shdn(n[0], 1), ndx = shdn(nd[0], 1);
+      if (xlast) {  // node Ex: mirror of node Ex-1 (even pad)
+        nx = n[VX - 1];
+        ndx = nd[VX - 1];
+      }
+      nY[VX] = (float)nx;
+      nY1[VX] = (float)ndx;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          NP[t][g][q] = (f32x2){nY[4 * g + q], nY[4 * g + q + 2]};
+          NP1[t][g][q] = (f32x2){nY1[4 * g + q], nY1[4 * g + q + 2]};
+        }
+    }
+
+#define KMP_CH(OUT, PLANE, K)                                                     \
+  _Pragma("unroll") for (int g = 0; g < G; ++g) {                                 \
+    uint32_t o[4];                                                                \
+    channel<T, K, G>(NP, NP1, PLANE, g, PLANE ? WcP : WcQ, PLANE ? BcP : BcQ, o); \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) OUT[4 * g + j + 1] = o[j];      \
+  }
+    // 1. the channels row Y+1 reads from row Y; row Y reads row Y-1's by the opposite rotation (row
+    // 0 of step 0 reads the zero-initialised carry: no masks on the row-above channels)
+    uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
+    {
+      uint32_t P3[VX + 1], P9[VX + 1], P10[VX + 1], P16[VX + 1], Q17[VX + 1];
+      KMP_CH(P3, 1, 3) KMP_CH(P9, 1, 9) KMP_CH(P10, 1, 10) KMP_CH(P16, 1, 16) KMP_CH(Q17, 0, 17)
+      {
+        uint32_t* w = xring + (wslot * xslot + tx * kXch * VX);
+#pragma unroll
+        for (int i = 0; i < VX; ++i) {
+          w[0 * VX + i] = P3[i + 1];
+          w[1 * VX + i] = P9[i + 1];
+          w[2 * VX + i] = P10[i + 1];
+          w[3 * VX + i] = P16[i + 1];
+          w[4 * VX + i] = Q17[i + 1];
+        }
+      }
+      const int rslot = wslot == 0 ? rows : wslot - 1;  // row Y - 1
+      const uint32_t* rd = xring + (rslot * xslot + tx * kXch * VX);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        A3[i + 1] = rd[0 * VX + i];
+        A9[i + 1] = rd[1 * VX + i];
+        A10[i + 1] = rd[2 * VX + i];
+        A16[i + 1] = rd[3 * VX + i];
+        QA17[i + 1] = rd[4 * VX + i];
+      }
+    }
+    A9[0] = shup(A9[VX], 1);  // cell (Y-1, X-1): the lane to the left
+
+    bool vx[VX + 1];
+#pragma unroll
+    for (int q = 0; q <= VX; ++q) vx[q] = q >= 1 || X >= 1;
+    const uint32_t ny = (uint32_t)vy0 + 1u;
+    const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+    auto m = [&](const uint32_t (&v)[VX + 1], int q, bool yok) { return (yok && vx[q]) ? v[q] : 0u; };
+    auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };
+    auto put8 = [&](int k, const uint32_t (&res)[VX]) {
+      int par[3];
+      map_parity(3, k, par);
+      if (!par[0] || vz1) st8(um[k] + s * mstep + lom, pack8<T, VX>(res));
+    };
+    const uint4 e0 = DEC ? uint4{} : *(const uint4*)&cur[1];
+    const uint4 e1 = cs[0], o0 = cs[1], o1 = cs[2];
+    char* h0 = DEC ? uho + s * hstep : nullptr;  // + loh: plane 2c, row 2Y
+    uint32_t ownv[VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&cur[1], i);
+      else ownv[i] = el16<T>(e0, 2 * i);
+    }
+    auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        if constexpr (DEC) outv[i] = (pred[i] + el8<T>(cm[k], i)) & MASK;
+        else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+      }
+    };
+
+    // 2. X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y)
+    {
+      uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
+      KMP_CH(P15, 1, 15) KMP_CH(Q18, 0, 18)
+#pragma unroll
+      for (int i = 0; i < VX; ++i)
+        pred[i] = (m(P15, i + 1, true) + m(A16, i + 1, true) + m(QA17, i + 1, true) + m(Q18, i + 1, true)) >>
+                  ((nz * ny) >> 1);
+      code(6, pred, e0, 1, outv);
+      if constexpr (DEC) {
+        st16(h0 + loh, pack16<T, VX>(ownv, outv));  // plane 2c, row 2Y: lowres | X
+      } else {
+        st8(ulo + s * mstep + lom, pack8<T, VX>(ownv));
+        put8(6, outv);
+      }
+    }
+    // 3. Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
+    {
+      uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
+      uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
+      KMP_CH(P7, 1, 7) KMP_CH(P8, 1, 8) KMP_CH(P2, 1, 2)
+      left(P8);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pZ[i] = (m(P7, i + 1, true) + m(P8, i, true) + m(A9, i, true) + m(A10, i + 1, true)) >> ((ny * nx) >> 1);
+        pU[i] = (P2[i + 1] + m(A3, i + 1, true)) >> (ny >> 1);
+      }
+      code(4, pZ, o0, 0, oZ);
+      code(1, pU, o0, 1, oU);
+      if constexpr (DEC) {
+        if (vz1) st16(h0 + hplane * SZ + loh, pack16<T, VX>(oZ, oU));  // plane 2c+1, row 2Y: Z | UD
+      } else {
+        put8(4, oZ);
+        put8(1, oU);
+      }
+    }
+    // 4. Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
+    {
+      uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
+      uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
+      KMP_CH(P11, 1, 11) KMP_CH(P12, 1, 12) KMP_CH(Q13, 0, 13) KMP_CH(Q14, 0, 14) KMP_CH(P4, 1, 4) KMP_CH(Q5, 0, 5)
+      left(P12);
+      left(Q13);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pY[i] = (m(P11, i + 1, true) + m(P12, i, true) + m(Q13, i, true) + m(Q14, i + 1, true)) >> ((nz * nx) >> 1);
+        pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
+      }
+      code(5, pY, e1, 0, oY);
+      code(2, pF, e1, 1, oF);
+      if constexpr (DEC) {
+        st16(h0 + a.W_ * SZ + loh, pack16<T, VX>(oY, oF));  // plane 2c, row 2Y+1: Y | FB
+      } else {
+        put8(5, oY);
+        put8(2, oF);
+      }
+    }
+    // 5. LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
+    {
+      uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
+      uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
+      KMP_CH(P0, 1, 0) KMP_CH(P1, 1, 1) KMP_CH(P6, 1, 6)
+      left(P1);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pL[i] = (P0[i + 1] + m(P1, i, true)) >> (nx >> 1);
+        pC[i] = P6[i + 1];
+      }
+      code(0, pL, o1, 0, oL);
+      code(3, pC, o1, 1, oC);
+      if constexpr (DEC) {
+        if (vz1) st16(h0 + (hplane + a.W_) * SZ + loh, pack16<T, VX>(oL, oC));  // plane 2c+1, row 2Y+1: LR | C
+      } else {
+        put8(0, oL);
+        put8(3, oC);
+      }
+    }
+#undef KMP_CH
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      cur[t] = nxt[t];
+      nxt[t] = nx2[t];
+    }
+    wslot = wslot == 0 ? rows : wslot - 1;
+    if (s + 1 < STEPS) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) cs[q] = ns[q];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) cm[k] = nm[k];
+    }
+  }
+}
+
 }  // namespace l3
 
 static int l3_env(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
+}
+
+// the y-rolling kernel serves FULL tiles whose rows split into 1, 2, 4 or 8 whole wave steps
+// (KMP_L3Y=0: the plane-block kernel, for A/B)
+// waves per SIMD: 16-bit samples 160 / 149 VGPRs (encode / decode), 8-bit 231 / 221
+#define L3Y_WPE (sizeof(T) == 2 ? L3Y_W16 : 2)
+#ifndef L3Y_W16
+#define L3Y_W16 3
+#endif
+static int l3y_steps(const l3::L3& a) {
+  if (!a.full || a.Lcz < 1 || !l3_env("KMP_L3Y", 1)) return 0;
+  if (a.Ey % a.rows != 0) return 0;
+  const int steps = a.Ey / a.rows;
+  return (steps == 1 || steps == 2 || steps == 4 || steps == 8) ? steps : 0;
 }
 
 template <typename T>
@@ -463,7 +828,7 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
   const int64_t rows = 64 / txn;
   const int64_t waves = ceil_div(g.E[1], rows);
-  if (waves > 4) return false;  // the workgroup covers the whole plane (row exchange through LDS)
+  const bool tall = waves > 4;  // the plane-block workgroup covers the whole plane (row exchange through LDS)
   int64_t zb = 0, ze = g.E[0];
   if (region) {
     if (region->begin[1] > 0 || region->begin[2] > 0 || region->end[1] < g.E[1] || region->end[2] < g.E[2]) return false;
@@ -483,6 +848,7 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   lds = (size_t)(waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * waves));
+  if (tall && !l3y_steps(a)) return false;  // only the y-rolling kernel serves it
   return nblk < ((int64_t)1 << 31);
 }
 
@@ -502,6 +868,16 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
     a.maps = maps;
     a.W = pred->weights;
     a.b = pred->bias;
+    if (const int steps = l3y_steps(a)) {
+      const dim3 g1(grid.x), b1(64);  // one wave per output plane
+      const size_t xl = (size_t)(a.rows + 1) * a.txn * l3::kXch * (8 / sizeof(T)) * 4;  // the row ring
+      if (steps == 1) l3::linear3y_kernel<T, false, 1, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 2) l3::linear3y_kernel<T, false, 2, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 4 && sizeof(T) == 2 && l3_env("KMP_L3Y_W", 3) == 4) l3::linear3y_kernel<T, false, 4, 4><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 4) l3::linear3y_kernel<T, false, 4, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else l3::linear3y_kernel<T, false, 8, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      return check_launch("linear3y_encode");
+    }
     if (a.full) l3::linear3d_kernel<T, false, true, 5><<<grid, block, lds, stream>>>(a);
     else l3::linear3d_kernel<T, false, false, 1><<<grid, block, lds, stream>>>(a);
     return check_launch("linear3d_encode");
@@ -527,6 +903,16 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
     a.W = pred->weights;
     a.b = pred->bias;
     a.uld = a.Lcz > 0 && a.Lcy > 0;  // clamped map planes / rows exist
+    if (const int steps = l3y_steps(a)) {
+      const dim3 g1(grid.x), b1(64);  // one wave per output plane
+      const size_t xl = (size_t)(a.rows + 1) * a.txn * l3::kXch * (8 / sizeof(T)) * 4;  // the row ring
+      if (steps == 1) l3::linear3y_kernel<T, true, 1, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 2) l3::linear3y_kernel<T, true, 2, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 4 && sizeof(T) == 2 && l3_env("KMP_L3Y_W", 3) == 4) l3::linear3y_kernel<T, true, 4, 4><<<g1, b1, xl, stream>>>(a);
+      else if (steps == 4) l3::linear3y_kernel<T, true, 4, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else l3::linear3y_kernel<T, true, 8, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      return check_launch("linear3y_decode");
+    }
     if (a.full && a.uld) l3::linear3d_kernel<T, true, true, 5, true><<<grid, block, lds, stream>>>(a);
     else if (a.full) l3::linear3d_kernel<T, true, true, 5><<<grid, block, lds, stream>>>(a);
     else l3::linear3d_kernel<T, true, false, 1><<<grid, block, lds, stream>>>(a);

@@ -411,10 +411,6 @@ __global__ void __launch_bounds__(64 * kEncWaves) rice_bundle_encode_kernel(RArr
   if (wv == 0) {
     uint64_t excl = 0;
     if (g > 0) {
-#ifdef KMP_RICE_EXP_NOLOOKBACK
-      excl = (uint64_t)g * 8192u;
-      if (true) {} else
-#endif
       while (true) {
         while (__any((v >> 62) == 0)) {  // a predecessor has not published yet: re-read those
           __builtin_amdgcn_s_sleep(1);

@@ -42,6 +42,7 @@ u16 count u32 nsp``, ``i32 dims[nsp]`` padded to 8, ``i64 lengths[count]``, then
 """
 
 import struct
+import threading
 
 import torch
 
@@ -59,19 +60,20 @@ _HEAD_MAX = _HEAD.size + 8 * 8       # header + the largest shape (ndim <= 8)
 _SAMPLE_BITS = {1: 8, 2: 16, 4: 32}
 
 
-_HOST_HEAD = None  # a pinned staging buffer for header reads (reused: every read synchronises)
+_TLS = threading.local()  # per thread: a pinned staging buffer for header reads (reused: every read synchronises)
 
 
 def _head_bytes(b, n):
     """The first ``n`` bytes of the device blob ``b`` on the host: one copy into a reused pinned
-    buffer and one stream synchronisation (a pageable ``.cpu()`` copy costs a fresh allocation)."""
-    global _HOST_HEAD
+    buffer (one per thread) and one stream synchronisation (a pageable ``.cpu()`` copy costs a
+    fresh allocation)."""
     n = min(int(n), b.numel())
-    if _HOST_HEAD is None or _HOST_HEAD.numel() < n:
-        _HOST_HEAD = torch.empty((max(n, 4096),), dtype=torch.uint8, pin_memory=True)
-    _HOST_HEAD[:n].copy_(b[:n], non_blocking=True)
+    buf = getattr(_TLS, 'head', None)
+    if buf is None or buf.numel() < n:
+        buf = _TLS.head = torch.empty((max(n, 4096),), dtype=torch.uint8, pin_memory=True)
+    buf[:n].copy_(b[:n], non_blocking=True)
     torch.cuda.current_stream().synchronize()
-    return _HOST_HEAD[:n].numpy().tobytes()
+    return buf[:n].numpy().tobytes()
 
 
 
@@ -254,36 +256,30 @@ def _runs(ts):
     return runs
 
 
-def _rice_arrays(ts, ptrs, offs, first, count):
+def _rice_arrays_n(ns, offs, first, count, ptrs):
+    """The launch records of arrays ``first .. first + count - 1`` (a fresh ctypes array per call)."""
     arr = (_lib.RiceArray * count)()
     for q in range(count):
         i = first + q
         arr[q].samples = ptrs[i]
-        arr[q].n = ts[i].numel()
-        arr[q].side_off, arr[q].toff_off = offs[i]
-        arr[q].rec_off = _RHEAD.size + _RREC.size * i + 112
-    return arr
-
-
-def _rice_arrays_n(ns, offs, first, count):
-    arr = (_lib.RiceArray * count)()
-    for q in range(count):
-        i = first + q
-        arr[q].samples = 0
         arr[q].n = ns[i]
         arr[q].side_off, arr[q].toff_off = offs[i]
         arr[q].rec_off = _RHEAD.size + _RREC.size * i + 112
     return arr
 
 
-def _rice_pack_bundle(arrays, dims):
+def _rice_pack_bundle(arrays, dims, exact=True):
+    """The bundle as a device byte tensor.  The encode writes into a worst-case sized buffer (the
+    size is known only after the launch); ``exact`` returns a copy of the ``total`` bytes so the
+    blob does not hold the worst-case allocation alive (callers that copy the blob to the host
+    right away pass False and take the view)."""
     out, poff, launched, keep = _rice_encode_launch(arrays, dims)
     if launched:  # the kernel zeroes the side arrays' and the payload's padding
         words, total = struct.unpack('<2q', _head_bytes(out[56:72], 16))  # the one synchronisation
     else:
         total = poff
     del keep
-    return out[:total]
+    return out[:total].clone() if exact else out[:total]
 
 
 # Layouts of recent bundle shapes (header bytes, offsets, tile counts, launch records), keyed by
@@ -325,9 +321,10 @@ def _rice_enc_plan(ts, dims):
     runs = []
     tile_begin = 0
     for first, count in _runs(ts):
-        runs.append((first, count, tile_begin, dev.dtype_code(ts[first]), _rice_arrays(ts, [0] * len(ts), offs, first, count)))
+        runs.append((first, count, tile_begin, dev.dtype_code(ts[first])))
         tile_begin += sum(tiles[first:first + count])
     return _remember(_ENC_PLANS, key, {
+        'ns': ns, 'offs': offs,
         'head': head, 'poff': poff, 'worst': worst, 'T': T, 'runs': runs,
         'hdr': torch.frombuffer(hdr, dtype=torch.uint8).to('cuda'),
         'ws_bytes': int(lib.kmp_rice_bundle_workspace_bytes(T)) if T else 0})
@@ -345,9 +342,10 @@ def _rice_encode_launch(arrays, dims):
         out[head:poff].zero_()
     if plan['T']:
         ws = dev.empty((plan['ws_bytes'],), torch.uint8)
-        for first, count, tile_begin, code, arr in plan['runs']:
-            for q in range(count):
-                arr[q].samples = ts[first + q].data_ptr()
+        for first, count, tile_begin, code in plan['runs']:
+            # the launch records are built per call (a cached ctypes record shared between threads
+            # could be rewritten by another thread while a launch reads it)
+            arr = _rice_arrays_n(plan['ns'], plan['offs'], first, count, [t.data_ptr() for t in ts])
             check(lib.kmp_rice_bundle_encode(code, arr, count, tile_begin, plan['T'], out.data_ptr(), poff,
                                              ws.data_ptr(), dev.stream()), 'rice bundle')
     return out, poff, plan['T'] > 0, ts
@@ -382,9 +380,8 @@ def _rice_decode_launch(b, hb):
     outs = [dev.empty(shape, dev.CODE_TO_TORCH[code]) for shape, code in zip(plan['shapes'], plan['codes'])]
     if plan['T']:
         bad = torch.zeros((1,), dtype=torch.int64, device='cuda')
-        for first, count, tile_begin, code, arr in plan['runs']:
-            for q in range(count):
-                arr[q].samples = outs[first + q].data_ptr()
+        for first, count, tile_begin, code in plan['runs']:
+            arr = _rice_arrays_n(plan['ns'], plan['offs'], first, count, [t.data_ptr() for t in outs])
             check(lib.kmp_rice_bundle_decode(code, arr, count, tile_begin, b.data_ptr(), plan['poff'], plan['words'],
                                              bad.data_ptr(), dev.stream()), 'rice bundle')
     else:
@@ -397,7 +394,9 @@ def _rice_dec_plan(b, hb):
     if len(hb) < _RHEAD.size:
         raise ValueError('truncated bundle')
     f = _RHEAD.unpack(hb[:_RHEAD.size])
-    _, _, count, nsp, flags = f[:5]
+    magic, version, count, nsp, flags = f[:5]
+    if magic != BUNDLE_MAGIC or version != RICE_VERSION:
+        raise ValueError(f'not a rice bundle (magic {magic!r}, version {version}; expected {RICE_VERSION})')
     dims = f[5:13]
     poff, words, total, _ = f[13:17]
     if count < 1 or count > _MAX_ARRAYS or nsp > 8 or flags:
@@ -440,9 +439,9 @@ def _rice_dec_plan(b, hb):
     runs = []
     tile_begin = 0
     for first, count in _runs([torch.empty(0, dtype=dev.CODE_TO_TORCH[c]) for c in codes]):
-        runs.append((first, count, tile_begin, codes[first], _rice_arrays_n(ns, offs, first, count)))
+        runs.append((first, count, tile_begin, codes[first]))
         tile_begin += sum(tiles[first:first + count])
-    return {'shapes': shapes, 'codes': codes, 'dims': tuple(int(d) for d in dims[:nsp]), 'poff': poff,
+    return {'ns': ns, 'offs': offs, 'shapes': shapes, 'codes': codes, 'dims': tuple(int(d) for d in dims[:nsp]), 'poff': poff,
             'words': words, 'total': total, 'T': sum(tiles), 'runs': runs}
 
 
@@ -473,6 +472,11 @@ def unpack(blob):
     b, kind = dev.to_device(blob)
     hb = _head_bytes(b, 4096)
     if hb[:4] == BUNDLE_MAGIC:
+        version = struct.unpack('<H', hb[4:6])[0] if len(hb) >= 6 else None
+        if version == VERSION:
+            raise ValueError('a planes bundle of several arrays (pack_encoded(method="planes")): use unpack_encoded')
+        if version != RICE_VERSION:
+            raise ValueError(f'unknown bundle version {version}')
         arrays, _ = _rice_unpack_bundle(b, hb)
         if len(arrays) != 1:
             raise ValueError(f'a bundle of {len(arrays)} arrays: use unpack_encoded')

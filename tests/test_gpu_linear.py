@@ -105,16 +105,23 @@ def test_linear_fused_p1(kom, shape):
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
 
 
-@pytest.mark.parametrize('shape,dtype', [((4, 64, 64, 64, 1), np.uint16), ((2, 17, 30, 16, 1), np.uint16),
-                                         ((2, 12, 33, 32, 1), np.uint16), ((1, 9, 14, 128, 1), np.uint8),
-                                         ((3, 10, 9, 64, 1), np.uint8)])
-def test_linear_fused_p0(kom, shape, dtype):
-    """The fused LinearPredictor p = 0 volume kernel (kmp_codec_linear3d.hip: weights in scalar
-    registers, the decode's unconditional loads, the FULL body for even y / x -- only row-0 / lane-0
-    masks, missing z planes through zero weights -- and the general body for odd heights):
-    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, chunked.  The
-    shapes cover FULL with an odd depth (the last output plane has no cell plane c) and the general
-    body."""
+@pytest.mark.parametrize('shape,dtype,kernel', [
+    # the y-rolling kernel (FULL tiles whose rows split into 1, 2, 4 or 8 wave steps)
+    ((4, 64, 64, 64, 1), np.uint16, 'linear3y'), ((1, 7, 64, 64, 1), np.uint16, 'linear3y'),
+    ((2, 6, 32, 32, 1), np.uint16, 'linear3y'), ((1, 4, 128, 64, 1), np.uint16, 'linear3y'),
+    ((1, 6, 64, 32, 1), np.uint16, 'linear3y'), ((2, 8, 32, 64, 1), np.uint8, 'linear3y'),
+    ((1, 9, 64, 64, 1), np.uint8, 'linear3y'), ((1, 4, 64, 128, 1), np.uint8, 'linear3y'),
+    # the plane-block kernel: FULL rows that do not split into wave steps, and odd heights
+    ((2, 17, 30, 16, 1), np.uint16, 'linear3d'), ((2, 12, 33, 32, 1), np.uint16, 'linear3d'),
+    ((1, 9, 14, 128, 1), np.uint8, 'linear3d'), ((3, 10, 9, 64, 1), np.uint8, 'linear3d')])
+def test_linear_fused_p0(kom, shape, dtype, kernel):
+    """The fused LinearPredictor p = 0 volume kernels (kmp_codec_linear3d.hip: weights in scalar
+    registers; the y-rolling kernel for FULL tiles -- one wave per output plane, row steps with the
+    next step's loads in flight, row neighbours by lane rotations; the plane-block kernel's FULL body
+    -- only row-0 / lane-0 masks, missing z planes through zero weights -- and its general body for
+    odd heights): residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless,
+    chunked.  The shapes cover FULL with an odd depth (the last output plane has no cell plane c),
+    1 / 2 / 4 / 8 row steps for both sample sizes, and the general body."""
     hi = _data(shape, dtype, 9)
     w, b = _weights(3, 0, 10, dtype)
     pred = kom.LinearPredictor(w, b, 0, 3)
@@ -123,11 +130,11 @@ def test_linear_fused_p0(kom, shape, dtype):
                       else (V.encode_values_uint8, V.decode_values_uint8, OV.encode_values_uint8))
     want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(0, w, b, 3), oenc, hi, padding=0)
     lo, (maps, dims) = V.encode(pred, enc, hi, padding=0)
-    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3d_encode'
+    assert kom._lib.lib.kmp_last_launch().decode() == kernel + '_encode'
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, c) in enumerate(zip(maps, want_maps)):
         assert np.array_equal(a, c), f'map {i}'
     assert np.array_equal(V.decode(pred, dec, lo, (maps, dims), padding=0), hi)
-    assert kom._lib.lib.kmp_last_launch().decode() == 'linear3d_decode'
+    assert kom._lib.lib.kmp_last_launch().decode() == kernel + '_decode'
     rec = V.decode_chunks(pred, dec, lo, (maps, dims), chunk=6, padding=0)
     assert np.array_equal(rec, hi)

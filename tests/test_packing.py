@@ -369,3 +369,68 @@ def test_rice_layout_caches_follow_the_shapes_and_bytes(kom):
         kom.packing.unpack_encoded(_poke(ga, 80 + 72, '<q', 999))   # record sample count of a cached layout
     with pytest.raises(ValueError):
         kom.packing.unpack_encoded(ga[:-8])                          # truncated blob, cached header
+
+
+@pytest.mark.gpu
+def test_rice_blob_holds_only_its_bytes(kom):
+    """A device blob is an exact-size tensor, not a view into the encode's worst-case buffer (which
+    is ~1.06x the raw samples for u16): holding many compressed results keeps only their bytes."""
+    import torch
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.integers(-3, 4, size=(200_000,)).astype(np.int16).view(np.uint16)).cuda()
+    blob = kom.packing.pack(x)
+    assert blob.untyped_storage().nbytes() == blob.numel()
+    lo = x[:1000].contiguous()
+    blob2 = kom.packing.pack_encoded(lo, ((x,), (0,)))
+    assert blob2.untyped_storage().nbytes() == blob2.numel()
+    assert torch.equal(kom.packing.unpack(blob), x)
+
+
+@pytest.mark.gpu
+def test_rice_pack_unpack_from_threads(kom):
+    """pack / unpack from several threads at once on same-shaped inputs (the layout caches are
+    shared; the launch records and the pinned header buffer are per call / per thread): every
+    thread gets its own blob and its own arrays back."""
+    import threading
+    import torch
+    rng = np.random.default_rng(11)
+    xs = [torch.from_numpy(rng.integers(-50, 50, size=(8, 4096)).astype(np.int16).view(np.uint16)).cuda()
+          for _ in range(8)]
+    want = [ORC.pack_bundle([x.cpu().numpy()], ()) for x in xs]
+    errors = []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(0)
+            for _ in range(20):
+                blob = kom.packing.pack(xs[i])
+                if not np.array_equal(blob.cpu().numpy(), want[i]):
+                    errors.append(f'thread {i}: pack bytes')
+                if not torch.equal(kom.packing.unpack(blob), xs[i]):
+                    errors.append(f'thread {i}: unpack')
+        except Exception as e:  # noqa: BLE001
+            errors.append(f'thread {i}: {e!r}')
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(xs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+
+
+@pytest.mark.gpu
+def test_unpack_names_the_bundle_kind(kom):
+    """unpack() of a several-array 'planes' bundle (format v1) names the function to use instead of
+    reading it as a rice (v2) header; a rice header with another version is rejected."""
+    import torch
+    x = torch.from_numpy(np.arange(300, dtype=np.uint16)).cuda()
+    b1 = kom.packing.pack_encoded(x, ((x, x), (1, 1)), method='planes')
+    with pytest.raises(ValueError, match='unpack_encoded'):
+        kom.packing.unpack(b1)
+    lo, (maps, dims) = kom.packing.unpack_encoded(b1)
+    assert torch.equal(lo, x) and tuple(dims) == (1, 1)
+    b2 = kom.packing.pack(x).cpu().numpy().copy()
+    b2[4:6] = np.frombuffer(np.uint16(7).tobytes(), np.uint8)
+    with pytest.raises(ValueError):
+        kom.packing.unpack(b2)
