@@ -590,10 +590,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   int wslot = r;  // Y mod (rows + 1): rows advance by rows == -1 (mod rows + 1) per step
 
-#pragma unroll 1
+#pragma unroll
   for (int s = 0; s < STEPS; ++s) {
-    if (s + 2 <= STEPS) load_nodes(s + 2, nx2);
-    if (s + 1 < STEPS) load_rest(s + 1, ns, nm);
+    // unconditional (clamped: the last steps re-read rows already loaded), so every iteration
+    // issues the same loads and the waits stay counted (vmcnt(N)) instead of draining (vmcnt(0))
+    load_nodes(s + 2 <= STEPS ? s + 2 : STEPS, nx2);
+    load_rest(s + 1 < STEPS ? s + 1 : STEPS - 1, ns, nm);
     // the weights are re-read (scalar loads, cache hits) in every step rather than hoisted out of
     // the loop: 171 values do not fit the scalar register file
     CFloat WcP = WcP0, BcP = BcP0, WcQ = WcQ0, BcQ = BcQ0;
@@ -785,12 +787,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       nxt[t] = nx2[t];
     }
     wslot = wslot == 0 ? rows : wslot - 1;
-    if (s + 1 < STEPS) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) cs[q] = ns[q];
+    for (int q = 0; q < 3; ++q) cs[q] = ns[q];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) cm[k] = nm[k];
-    }
+    for (int k = 0; k < 7; ++k) cm[k] = nm[k];
   }
 }
 
@@ -803,10 +803,11 @@ static int l3_env(const char* name, int dflt) {
 
 // the y-rolling kernel serves FULL tiles whose rows split into 1, 2, 4 or 8 whole wave steps
 // (KMP_L3Y=0: the plane-block kernel, for A/B)
-// waves per SIMD: 16-bit samples 160 / 149 VGPRs (encode / decode), 8-bit 231 / 221
+// waves per SIMD: 16-bit samples 127 / 123 VGPRs (encode / decode, 4 steps fully unrolled; 8 steps
+// at 3 waves), 8-bit ~200 (2 waves)
 #define L3Y_WPE (sizeof(T) == 2 ? L3Y_W16 : 2)
 #ifndef L3Y_W16
-#define L3Y_W16 3
+#define L3Y_W16 4
 #endif
 static int l3y_steps(const l3::L3& a) {
   if (!a.full || a.Lcz < 1 || !l3_env("KMP_L3Y", 1)) return 0;
@@ -873,9 +874,8 @@ int try_linear3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const k
       const size_t xl = (size_t)(a.rows + 1) * a.txn * l3::kXch * (8 / sizeof(T)) * 4;  // the row ring
       if (steps == 1) l3::linear3y_kernel<T, false, 1, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
       else if (steps == 2) l3::linear3y_kernel<T, false, 2, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
-      else if (steps == 4 && sizeof(T) == 2 && l3_env("KMP_L3Y_W", 3) == 4) l3::linear3y_kernel<T, false, 4, 4><<<g1, b1, xl, stream>>>(a);
       else if (steps == 4) l3::linear3y_kernel<T, false, 4, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
-      else l3::linear3y_kernel<T, false, 8, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else l3::linear3y_kernel<T, false, 8, (sizeof(T) == 2 ? 3 : 2)><<<g1, b1, xl, stream>>>(a);
       return check_launch("linear3y_encode");
     }
     if (a.full) l3::linear3d_kernel<T, false, true, 5><<<grid, block, lds, stream>>>(a);
@@ -908,9 +908,8 @@ int try_linear3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int
       const size_t xl = (size_t)(a.rows + 1) * a.txn * l3::kXch * (8 / sizeof(T)) * 4;  // the row ring
       if (steps == 1) l3::linear3y_kernel<T, true, 1, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
       else if (steps == 2) l3::linear3y_kernel<T, true, 2, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
-      else if (steps == 4 && sizeof(T) == 2 && l3_env("KMP_L3Y_W", 3) == 4) l3::linear3y_kernel<T, true, 4, 4><<<g1, b1, xl, stream>>>(a);
       else if (steps == 4) l3::linear3y_kernel<T, true, 4, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
-      else l3::linear3y_kernel<T, true, 8, L3Y_WPE><<<g1, b1, xl, stream>>>(a);
+      else l3::linear3y_kernel<T, true, 8, (sizeof(T) == 2 ? 3 : 2)><<<g1, b1, xl, stream>>>(a);
       return check_launch("linear3y_decode");
     }
     if (a.full && a.uld) l3::linear3d_kernel<T, true, true, 5, true><<<grid, block, lds, stream>>>(a);
