@@ -49,6 +49,10 @@ typedef enum {
   /* pred[k] = sum_n feat[n] * W[n, k] + b[k] in float32 (MFMA), cast to the dtype
      (build-defined; fills the reference's predictions_fn slot, volume/encode_decode.py:48) */
   KMP_PRED_LINEAR = 1,
+  /* the same predictor on the matrix cores: bf16x2 split of features and weights, one
+     v_mfma_f32_16x16x32_bf16 per chunk of 8 features (kmp_bf16x2.h); within the north star's 1e-5
+     of the f64 value rather than bit-equal to the f32 fma chain; uint8 / uint16 samples */
+  KMP_PRED_LINEAR_MFMA = 2,
 } kmp_predictor_kind;
 
 typedef struct {
@@ -177,6 +181,11 @@ int kmp_mean_predict_maps_typed(int32_t nsp, int32_t dtype, int32_t out_dtype, c
 int kmp_linear_predict(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],
                        int64_t C, int32_t padding, const float* weights, const float* bias, void* preds_out,
                        float* preds_f32, kmp_stream_t stream);
+/* the same for KMP_PRED_LINEAR_MFMA (kmp_bf16x2.h): the matrix-core arithmetic every fused kernel of
+   that kind reproduces bit for bit; uint8 / uint16 samples */
+int kmp_linear_predict_mfma(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B, const int64_t shape[3],
+                            int64_t C, int32_t padding, const float* weights, const float* bias, void* preds_out,
+                            float* preds_f32, kmp_stream_t stream);
 
 /* jnp.pad on the spatial axes (volume/utils.py:213-260, image/utils.py:132-178):
    mode 0 = 'symmetric', 1 = 'reflect'.  Negative pads crop (== trim, volume/utils.py:263-276). */

@@ -34,11 +34,20 @@ def _headers_mtime():
     return max(os.path.getmtime(h) for h in hs)
 
 
+# per-file flags: the matrix-core LinearPredictor kernels keep MFMA accumulators in ordinary VGPRs
+# (-amdgpu-mfma-vgpr-form): with AGPRs every tile paid 4 accvgpr writes (the bias) and 4 reads
+# (the results) per MFMA, 256 VALU instructions per wave step of kmp_codec_linear3m.hip
+FILE_FLAGS = {'kmp_codec_linear3m.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form'],
+              'kmp_linear.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form']}
+
+
 def _compile(src, hdr_mtime, verbose, debug=False):
     obj = os.path.join(BUILD_DEBUG if debug else BUILD, os.path.basename(src).replace('.hip', '.o'))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime,
+                                                            os.path.getmtime(os.path.abspath(__file__))):
         return obj
-    cmd = [HIPCC, *FLAGS, *(['-DKMP_DEBUG'] if debug else []), '-c', src, '-o', obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *(['-DKMP_DEBUG'] if debug else []),
+           '-c', src, '-o', obj]
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -32,7 +32,7 @@ KMP_OK, KMP_ERR_ARG, KMP_ERR_UNSUPPORTED, KMP_ERR_LAUNCH = 0, -1, -2, -3
 U8, U16, I32, F32, U32 = 0, 1, 2, 3, 4
 CODER_RAW, CODER_U8, CODER_U16, CODER_U32 = 0, 1, 2, 3
 ENCODE, DECODE = 0, 1
-PRED_MEAN, PRED_LINEAR = 0, 1
+PRED_MEAN, PRED_LINEAR, PRED_LINEAR_MFMA = 0, 1, 2
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -84,6 +84,7 @@ _PROTOS = {
     'kmp_mean_predict_maps': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vpp, _vp]),
     'kmp_mean_predict_maps_typed': (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vpp, _vp]),
     'kmp_linear_predict': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
+    'kmp_linear_predict_mfma': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     'kmp_pad': (ctypes.c_int, [_i32, _i32, _vp, _i64, _i64p, _i64, _i64p, _i64p, _i32, _vp, _vp]),
     'kmp_copy_box': (ctypes.c_int, [_i32, _i32, _vp, _i64p, _i64p, _i32, _vp, _i64p, _i64p, _i64, _i64, _i64p,
                                     _vp]),

@@ -1,0 +1,84 @@
+// kmp_bf16x2.h -- the LinearPredictor's matrix-core arithmetic (KMP_PRED_LINEAR_MFMA), shared by
+// every kernel that evaluates it (kmp_linear.hip: any shape / padding, the callback path and the
+// generic codec; kmp_codec_linear3m.hip: the fused p = 0 volume codec), so all of them produce
+// bit-identical predictions and a volume encoded by one path decodes losslessly through another.
+//
+// pred[cell, k] = b[k] + sum_n f_n * W[n, k]  (the north star's 1e-5 FP contract, not the f32
+// fma chain of KMP_PRED_LINEAR):
+//   * a u8 / u16 feature f = 256 * hi + lo splits into two bf16-exact bytes (hi, lo <= 255);
+//   * a weight splits into w1 = bf16(w), w2 = bf16(w - w1) (round to nearest even), so
+//     |w - w1 - w2| <= 2^-18 |w|; the hi parts take 256 * w1, 256 * w2 (exact: a power of two);
+//   * features are taken in chunks of 8 in the reference's order (features_from_lowres,
+//     volume/utils.py:199-210); per chunk ONE v_mfma_f32_16x16x32_bf16 with
+//         K = 32 = [hi_0, lo_0, ..., hi_7, lo_7 | the same 16] x [u1 of the chunk | u2 of the chunk],
+//     accumulated from the bias: acc = b[k]; acc = mfma(A_0, B_0, acc); acc = mfma(A_1, B_1, acc) ...
+//     (features past N and padded columns are zeros);
+//   * then the sample dtype's truncating, saturating cast (XLA astype).
+// Error: <= 2^-18 sum|f w| from the split plus the f32 accumulation inside the MFMA, well within
+// 1e-5 of sum|f w| + |b| (tests/test_gpu_linear.py).  An MFMA output element depends only on its
+// A row, B column and C value, so the lane / tile position of a cell or channel does not matter.
+//
+// Fragment maps (cdna_hip_programming.md §3): lane l = 16 g + m holds A[row m][k = 8g + j] and
+// B[k = 8g + j][col m], j = 0..7, as 4 dwords of bf16 pairs (element 2i in the low half); C/D:
+// col m, rows 4g .. 4g + 3.  So lane group g carries features 4(g & 1) .. 4(g & 1) + 3 of the
+// chunk, against u1 (g < 2) or u2 (g >= 2).
+#pragma once
+
+#include "kmp_common.h"
+
+namespace kmp {
+namespace bx {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// f32 -> bf16 bits, round to nearest even (NaN stays NaN)
+__host__ __device__ __forceinline__ uint32_t bf16_rne(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__host__ __device__ __forceinline__ float bf16_f32(uint32_t h) {
+  const uint32_t u = h << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+
+// The two bf16 terms of a weight, part = 0 / 1, and the hi-byte feature's scaled copy (hi = 1).
+__host__ __device__ __forceinline__ uint32_t weight_part(float w, int part, int hi) {
+  const uint32_t w1 = bf16_rne(w);
+  const uint32_t v = part == 0 ? w1 : bf16_rne(w - bf16_f32(w1));
+  return hi ? bf16_rne(bf16_f32(v) * 256.0f) : v;
+}
+
+// A feature's fragment dword: bf16(hi) in the low half, bf16(lo) in the high half.  For a byte b,
+// f32(b)'s upper half IS bf16(b) (8 significant bits at most).
+__device__ __forceinline__ uint32_t feature_dword(uint32_t v) {
+  const uint32_t fh = __float_as_uint((float)(v >> 8)), fl = __float_as_uint((float)(v & 0xffu));
+  return __builtin_amdgcn_perm(fl, fh, 0x07060302u);  // {fh[31:16], fl[31:16]} -> low, high
+}
+
+// B fragment of one chunk for the lane of group g, column weights Wcol[n * ldw] (n < N, else 0):
+// element j of K = 8g + j -> feature 8q + 4(g & 1) + (j >> 1), byte j & 1 (0 = hi), term g >> 1
+__device__ __forceinline__ u32x4 b_fragment(const float* Wcol, int ldw, int N, int q, int g, bool valid) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = 8 * q + 4 * (g & 1) + i;
+    const float w = (valid && n < N) ? Wcol[(int64_t)n * ldw] : 0.0f;
+    r[i] = weight_part(w, g >> 1, 1) | (weight_part(w, g >> 1, 0) << 16);
+  }
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+}  // namespace bx
+}  // namespace kmp

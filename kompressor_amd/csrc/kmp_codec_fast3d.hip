@@ -491,6 +491,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3d32_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // 32-bit samples
     if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3m_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // matrix-core linear p = 0
+    if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3d_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, stream);  // p = 1, 2
@@ -524,6 +526,8 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     int st = try_wave3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_wave3d32_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3m_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3d_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;

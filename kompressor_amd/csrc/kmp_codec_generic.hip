@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
 // Host side of the generic path
 // ------------------------------------------------------------------------------------------
 int64_t generic_workspace_bytes(int dtype, int nsp, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred) {
-  const bool lin = pred && pred->kind == KMP_PRED_LINEAR;
+  const bool lin = pred && (pred->kind == KMP_PRED_LINEAR || pred->kind == KMP_PRED_LINEAR_MFMA);
   const int K = lin ? (nsp == 3 ? 19 : 5) : 1;
   int64_t need = B * g.Lc[0] * g.Lc[1] * g.Lc[2] * K * C * dtype_size(dtype);
   if (lin && B > 0) {  // the fused LinearPredictor kernels keep a reordered copy of W [N, K] there
@@ -250,9 +250,11 @@ static int dispatch_natural(int dtype, int coder, F&& f) {
 static int check_predictor(const kmp_predictor* pred, int dtype) {
   KMP_REQUIRE(pred, "null predictor");
   KMP_REQUIRE(pred->padding >= 0, "negative padding");
-  KMP_REQUIRE(pred->kind == KMP_PRED_MEAN || pred->kind == KMP_PRED_LINEAR, "unknown predictor kind");
-  if (pred->kind == KMP_PRED_LINEAR) KMP_REQUIRE(pred->weights && pred->bias, "linear predictor needs weights and bias");
-  (void)dtype;
+  KMP_REQUIRE(pred->kind == KMP_PRED_MEAN || pred->kind == KMP_PRED_LINEAR || pred->kind == KMP_PRED_LINEAR_MFMA,
+              "unknown predictor kind");
+  if (pred->kind != KMP_PRED_MEAN) KMP_REQUIRE(pred->weights && pred->bias, "linear predictor needs weights and bias");
+  if (pred->kind == KMP_PRED_LINEAR_MFMA)
+    KMP_REQUIRE(dtype == KMP_U8 || dtype == KMP_U16, "the matrix-core LinearPredictor takes uint8 / uint16 samples");
   return KMP_OK;
 }
 

@@ -11,6 +11,7 @@
 // 32x32x2 MFMAs with the accumulator seeded by the bias; the oracle reproduces the chain exactly.
 // Lane l feeds A[cell l&31][feature 2s + (l>>5)] and B[feature 2s + (l>>5)][output l&31]; the
 // result row (cell) of accumulator register r is (r&3) + 8(r>>2) + 4(l>>5), column l&31.
+#include "kmp_bf16x2.h"
 #include "kmp_codec.h"
 
 namespace kmp {
@@ -101,14 +102,80 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
   }
 }
 
+// KMP_PRED_LINEAR_MFMA (kmp_bf16x2.h): one wave per 16-row tile (rows = (b, cell, c) as above),
+// the K outputs in column tiles of 16, per chunk of 8 features one v_mfma_f32_16x16x32_bf16 per
+// column tile.  u8 / u16 samples only (the byte split is exact for them).
+template <typename T>
+__global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict__ src, LinSrc s, int nsp, int p,
+                                                            int64_t B, int64_t C, const float* __restrict__ W,
+                                                            const float* __restrict__ bias, int N, int K,
+                                                            T* __restrict__ out, float* __restrict__ out_f32,
+                                                            int64_t rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int m = lane & 15, g = lane >> 4;
+  const int nq = (N + 7) / 8, nct = (K + 15) / 16;
+  for (int64_t tile = wave; tile * 16 < rows; tile += nwaves) {
+    const int64_t row = tile * 16 + m;  // this lane's A row (cell)
+    const bool row_ok = row < rows;
+    int64_t b, z, y, x, c;
+    unflat5(row_ok ? row : 0, s.cext[0], s.cext[1], s.cext[2], C, b, z, y, x, c);
+    z += s.cbeg[0];
+    y += s.cbeg[1];
+    x += s.cbeg[2];
+    for (int ct = 0; ct < nct; ++ct) {
+      const int k = 16 * ct + m;  // this lane's B / D column
+      const bool col_ok = k < K;
+      const float bk = col_ok ? bias[k] : 0.0f;
+      bx::f32x4 acc = {bk, bk, bk, bk};
+      for (int q = 0; q < nq; ++q) {
+        bx::u32x4 a;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 8 * q + 4 * (g & 1) + i;
+          const uint32_t v = (row_ok && n < N) ? (uint32_t)lin_feature(src, s, nsp, p, b, c, C, z, y, x, n) : 0u;
+          a[i] = bx::feature_dword(v);
+        }
+        acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, q, g, col_ok), acc);
+      }
+      if (!col_ok) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t orow = tile * 16 + 4 * g + r;
+        if (orow >= rows) continue;
+        int64_t ob, oz, oy, ox, oc;
+        unflat5(orow, s.cext[0], s.cext[1], s.cext[2], C, ob, oz, oy, ox, oc);
+        oz += s.cbeg[0];
+        oy += s.cbeg[1];
+        ox += s.cbeg[2];
+        const int64_t cell = ((ob * s.Lc[0] + oz) * s.Lc[1] + oy) * s.Lc[2] + ox;
+        const int64_t o = (cell * K + k) * C + oc;
+        out[o] = cast_f32<T>(acc[r]);
+        if (out_f32) out_f32[o] = acc[r];
+      }
+    }
+  }
+}
+
 template <typename T>
 static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t B, int64_t C, const float* W,
-                         const float* bias, T* out, float* out_f32, hipStream_t stream) {
+                         const float* bias, T* out, float* out_f32, hipStream_t stream, int kind = KMP_PRED_LINEAR) {
   const int k = 2 * p + 2;
   const int N = nsp == 3 ? k * k * k : k * k;
   const int K = nsp == 3 ? 19 : 5;
   const int64_t rows = B * s.cext[0] * s.cext[1] * s.cext[2] * C;
   if (rows == 0) return KMP_OK;
+  if (kind == KMP_PRED_LINEAR_MFMA) {
+    if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
+      int64_t blocks = ceil_div(ceil_div(rows, 16), 4);
+      if (blocks > 65536) blocks = 65536;
+      linear_bf16x2_kernel<T><<<(unsigned)blocks, 256, 0, stream>>>(src, s, nsp, p, B, C, W, bias, N, K, out, out_f32,
+                                                                    rows);
+      return check_launch("linear_bf16x2");
+    }
+    return fail(KMP_ERR_UNSUPPORTED, "the matrix-core LinearPredictor (bf16x2) takes uint8 / uint16 samples");
+  }
   int64_t waves = ceil_div(rows, 32);
   int64_t blocks = ceil_div(waves, 4);
   if (blocks > 65536) blocks = 65536;
@@ -129,7 +196,8 @@ int linear_cells(const T* src, const int64_t* S, int mult, const Geo& g, int nsp
     s.Lc[a] = g.Lc[a];
   }
   s.mult = mult;
-  return launch_linear<T>(src, s, nsp, pred->padding, B, C, pred->weights, pred->bias, cells, nullptr, stream);
+  return launch_linear<T>(src, s, nsp, pred->padding, B, C, pred->weights, pred->bias, cells, nullptr, stream,
+                          pred->kind);
 }
 
 #define KMP_INSTL(T)                                                                                             \
@@ -144,9 +212,27 @@ KMP_INSTL(uint32_t)
 
 using namespace kmp;
 
+static int linear_predict(int kind, int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B,
+                          const int64_t shape[3], int64_t C, int32_t padding, const float* weights, const float* bias,
+                          void* preds_out, float* preds_f32, kmp_stream_t stream);
+
 extern "C" int kmp_linear_predict(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B,
                                   const int64_t shape[3], int64_t C, int32_t padding, const float* weights,
                                   const float* bias, void* preds_out, float* preds_f32, kmp_stream_t stream) {
+  return linear_predict(KMP_PRED_LINEAR, nsp, dtype, padded_lowres, B, shape, C, padding, weights, bias, preds_out,
+                        preds_f32, stream);
+}
+
+extern "C" int kmp_linear_predict_mfma(int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B,
+                                       const int64_t shape[3], int64_t C, int32_t padding, const float* weights,
+                                       const float* bias, void* preds_out, float* preds_f32, kmp_stream_t stream) {
+  return linear_predict(KMP_PRED_LINEAR_MFMA, nsp, dtype, padded_lowres, B, shape, C, padding, weights, bias,
+                        preds_out, preds_f32, stream);
+}
+
+static int linear_predict(int kind, int32_t nsp, int32_t dtype, const void* padded_lowres, int64_t B,
+                          const int64_t shape[3], int64_t C, int32_t padding, const float* weights, const float* bias,
+                          void* preds_out, float* preds_f32, kmp_stream_t stream) {
   KMP_REQUIRE(nsp == 2 || nsp == 3, "nsp must be 2 or 3");
   KMP_REQUIRE(padded_lowres && weights && bias && preds_out && shape && padding >= 0, "bad argument");
   KMP_REQUIRE(B >= 0 && C >= 1, "bad batch or channel count");
@@ -167,6 +253,6 @@ extern "C" int kmp_linear_predict(int32_t nsp, int32_t dtype, const void* padded
   return dispatch_int_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     return launch_linear<T>((const T*)padded_lowres, s, nsp, padding, B, C, weights, bias, (T*)preds_out, preds_f32,
-                            (hipStream_t)stream);
+                            (hipStream_t)stream, kind);
   });
 }

@@ -52,13 +52,29 @@ class MeanPredictor:
         return f'MeanPredictor(padding={self.padding}, ndim={self.ndim}{md})'
 
 
-class LinearPredictor:
-    """``pred[cell, k] = sum_n features[cell, n] * W[n, k] + b[k]`` (float32, MFMA), cast to the
-    sample dtype, then ``maps_from_predictions``.  ``W`` is ``[(2p+2)^ndim, 19 or 5]``."""
+ARITHS = ('f32', 'bf16x2')
 
-    def __init__(self, weights, bias, padding=0, ndim=3):
+
+class LinearPredictor:
+    """``pred[cell, k] = sum_n features[cell, n] * W[n, k] + b[k]``, cast to the sample dtype, then
+    ``maps_from_predictions``.  ``W`` is ``[(2p+2)^ndim, 19 or 5]``.
+
+    ``arith`` picks the arithmetic, and every path (fused codec kernels, the callable, the generic
+    codec) evaluates a predictor with the same one, so encode and decode agree bit for bit:
+
+    * ``'f32'`` (default): the k-ordered float32 fma chain from the bias -- bit-identical to the
+      oracle's restatement (``oracle.predictors.linear_fma_chain``);
+    * ``'bf16x2'``: the matrix cores (kmp_bf16x2.h) -- features split into two exact bf16 bytes,
+      weights into two bf16 terms, one ``v_mfma_f32_16x16x32_bf16`` per 8 features; within the north
+      star's 1e-5 (relative to sum|f w| + |b|) of the float64 value rather than equal to the f32
+      chain.  uint8 / uint16 samples."""
+
+    def __init__(self, weights, bias, padding=0, ndim=3, arith='f32'):
         if ndim not in (2, 3):
             raise ValueError('ndim must be 2 (image) or 3 (volume)')
+        if arith not in ARITHS:
+            raise ValueError(f'arith must be one of {ARITHS}')
+        self.arith = arith
         n, k = (2 * padding + 2) ** ndim, NPRED[ndim]
         w = torch.as_tensor(np.asarray(weights, dtype=np.float32) if not isinstance(weights, torch.Tensor)
                             else weights, dtype=torch.float32)
@@ -87,7 +103,8 @@ class LinearPredictor:
 
     def _kmp_predictor(self):
         w, b = self._device_params()
-        return _lib.Predictor(_lib.PRED_LINEAR, self.padding, w.data_ptr(), b.data_ptr())
+        kind = _lib.PRED_LINEAR if self.arith == 'f32' else _lib.PRED_LINEAR_MFMA
+        return _lib.Predictor(kind, self.padding, w.data_ptr(), b.data_ptr())
 
     def predict_cells(self, lowres, with_f32=False):
         """Per-cell predictions ``[B, cells..., K, C...]`` in the sample dtype (and the f32 pre-cast
@@ -100,7 +117,8 @@ class LinearPredictor:
         shape = (t.shape[0], *cells, NPRED[nsp], *_ch(t.shape, nsp))
         out = dev.empty(shape, t.dtype)
         f32 = dev.empty(shape, torch.float32) if with_f32 else None
-        check(lib.kmp_linear_predict(nsp, dev.dtype_code(t), t.data_ptr(), t.shape[0], _lib.i64x3(S),
+        fn = lib.kmp_linear_predict if self.arith == 'f32' else lib.kmp_linear_predict_mfma
+        check(fn(nsp, dev.dtype_code(t), t.data_ptr(), t.shape[0], _lib.i64x3(S),
                                      _C(t.shape, nsp), self.padding, w.data_ptr(), b.data_ptr(), out.data_ptr(),
                                      f32.data_ptr() if f32 is not None else None, dev.stream()), 'linear_predict')
         if with_f32:
@@ -113,4 +131,5 @@ class LinearPredictor:
         return tuple(dev.from_device(m, kind) for m in d_maps_from_predictions(cells, self.ndim))
 
     def __repr__(self):
-        return f'LinearPredictor(padding={self.padding}, ndim={self.ndim})'
+        ar = '' if self.arith == 'f32' else f", arith='{self.arith}'"
+        return f'LinearPredictor(padding={self.padding}, ndim={self.ndim}{ar})'

@@ -137,3 +137,27 @@ def linear_predictions_fn(padding, weights, bias, ndim=3):
         return ns.maps_from_predictions(pred)
 
     return predictions_fn
+
+
+def bf16_rne(x):
+    """float32 -> bfloat16 (round to nearest even), returned as float32 values (the bf16 set)."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7fff + ((u >> 16) & 1)) & 0xffff0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+def bf16x2_weights(weights):
+    """The two bf16 terms of the build's matrix-core LinearPredictor arithmetic (kmp_bf16x2.h):
+    w1 = bf16(w), w2 = bf16(w - w1), so |w - w1 - w2| <= 2^-18 |w|."""
+    w = np.asarray(weights, np.float32)
+    w1 = bf16_rne(w)
+    w2 = bf16_rne((w - w1).astype(np.float32))
+    return w1, w2
+
+
+def linear_bf16x2_split(features, weights, bias):
+    """float64 value of what the bf16x2 MFMAs multiply: sum_n f_n (w1 + w2)[n, k] + b[k], each
+    product exact (features are u8 / u16, split into two exact bytes, and 256 * w_i is exact) -- the
+    kernel's float32 result differs from this only by the rounding of its f32 accumulation."""
+    w1, w2 = bf16x2_weights(weights)
+    return linear_predictions(features, w1.astype(np.float64) + w2.astype(np.float64), bias, np.float32)[0]

@@ -39,6 +39,7 @@ CASES = [
     ('mean0_u8_img', 2, (16, 256, 256, 1), np.uint8, 1.0),
     ('mean0_f32', 3, (2, 64, 64, 64, 1), np.float32, 0.5),
     ('linear0_u16', 3, (2, 32, 32, 32, 1), np.uint16, 2.0),
+    ('linearmx0_u16', 3, (2, 32, 64, 64, 1), np.uint16, 2.0),  # arith='bf16x2' (the matrix cores)
     ('mean2_u16', 3, (2, 40, 36, 64, 1), np.uint16, 2.0),      # the z-rolling p = 2 kernel
     ('mean2_u8_img', 2, (4, 100, 256, 1), np.uint8, 1.0),      # the y-rolling image kernel
 ]
@@ -49,7 +50,8 @@ def _predictor(kom, name, ndim):
     if name.startswith('linear'):
         n, k = 8, 19
         w = (np.full((n, k), 1.0 / n) + np.random.default_rng(3).standard_normal((n, k)) * 0.01).astype(np.float32)
-        return kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim)
+        return kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim,
+                                   arith='bf16x2' if name.startswith('linearmx') else 'f32')
     return kom.MeanPredictor(p, ndim)
 
 
@@ -166,3 +168,43 @@ def test_corrupt_files_raise(kom, tmp_path):
     for name in ('flip.kmp', 'trunc.kmp', 'foreign.kmp'):
         with pytest.raises(ValueError):
             kom.container.decompress(str(tmp_path / name))
+
+
+@pytest.mark.gpu
+def test_device_crc_matches_zlib(kom):
+    """kmp_crc32 (the file CRC, computed on the device) equals zlib.crc32 for lengths around its
+    16-byte chunks, 1 KiB wave steps and 32 KiB wave regions, with the length given directly or read
+    by the kernel from device memory (capped at the buffer)."""
+    import zlib
+    from kompressor_amd import container
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, size=(3 << 20) + 77, dtype=np.uint8)
+    dev_data = torch.from_numpy(data).cuda()
+    for n in [0, 1, 15, 16, 17, 1023, 1024, 1025, 32767, 32768, 32769, 100000, (1 << 20) + 3, data.size]:
+        got = int(container._device_crc(dev_data, n).cpu().view(torch.uint32).item())
+        assert got == zlib.crc32(data[:n].tobytes()), n
+    lens = torch.tensor([5000, 10 ** 9], dtype=torch.int64, device='cuda')
+    got = int(container._device_crc(dev_data, 70000, lens[0:1].data_ptr()).cpu().view(torch.uint32).item())
+    assert got == zlib.crc32(data[:5000].tobytes())
+    got = int(container._device_crc(dev_data, 70000, lens[1:2].data_ptr()).cpu().view(torch.uint32).item())
+    assert got == zlib.crc32(data[:70000].tobytes())  # a length past the buffer is capped
+
+
+@pytest.mark.gpu
+def test_file_crc_is_zlib_and_split_is_recorded(kom, tmp_path):
+    """The CRC a file stores is zlib's CRC-32 of its bundle bytes (files stay readable by any zlib),
+    and compress / decompress record their host / device time split."""
+    import json
+    import struct
+    import zlib
+    x = structured((2, 32, 32, 32, 1), np.uint16, 2.0)
+    path = str(tmp_path / 'z.kmp')
+    kom.container.compress(path, x, kom.MeanPredictor(0, 3))
+    assert set(kom.container.last_timing) >= {'device', 'd2h', 'write', 'total'}
+    raw = open(path, 'rb').read()
+    mlen = struct.unpack('<4sHHQ', raw[:16])[3]
+    meta = json.loads(raw[16:16 + mlen])
+    body = raw[16 + mlen:]
+    assert len(body) == meta['bundle_bytes'] and zlib.crc32(body) == meta['crc32']
+    assert np.array_equal(kom.container.decompress(path), x)
+    assert set(kom.container.last_timing) >= {'read', 'upload_crc', 'device', 'd2h', 'total'}

@@ -1,5 +1,6 @@
-"""LinearPredictor (f32 MFMA) parity: float32 intermediates bit-exact to the oracle's fma chain and
-within the north star's 1e-5 of a float64 reference; residual maps bit-exact; lossless."""
+"""LinearPredictor parity.  arith='f32' (default): float32 intermediates bit-exact to the oracle's
+fma chain and within the north star's 1e-5 of a float64 reference; residual maps bit-exact;
+lossless.  arith='bf16x2' (the matrix cores): see the section at the end."""
 
 import numpy as np
 import pytest
@@ -138,3 +139,82 @@ def test_linear_fused_p0(kom, shape, dtype, kernel):
     assert kom._lib.lib.kmp_last_launch().decode() == kernel + '_decode'
     rec = V.decode_chunks(pred, dec, lo, (maps, dims), chunk=6, padding=0)
     assert np.array_equal(rec, hi)
+
+
+# ---------------------------------------------------------------------------------------------
+# arith='bf16x2': the matrix-core arithmetic (kmp_bf16x2.h).  Not equal to the f32 fma chain by
+# design; pinned by (1) the float32 channel values within the north star's 1e-5 of float64 (and
+# within f32 accumulation rounding of the exactly split products), (2) every path -- fused
+# linear3m kernel, the callable / callback path, the generic codec -- producing the same bits,
+# (3) the residuals equal to the oracle's coder applied to the kernel's own prediction maps, and
+# (4) lossless round trips, including across paths.
+# ---------------------------------------------------------------------------------------------
+
+BF_CASES = [(3, 0, (4, 64, 64, 64, 1), np.uint16), (3, 0, (2, 16, 32, 32, 1), np.uint16),
+            (3, 0, (1, 7, 32, 64, 1), np.uint16), (3, 0, (2, 9, 10, 12, 1), np.uint16),
+            (3, 0, (2, 8, 32, 64, 1), np.uint8), (3, 0, (1, 9, 64, 32, 1), np.uint8),
+            (3, 1, (2, 8, 9, 7, 1), np.uint16), (2, 0, (3, 33, 20, 1), np.uint8), (2, 1, (2, 30, 31, 2), np.uint16)]
+
+
+@pytest.mark.parametrize('ndim,p,shape,dtype', BF_CASES)
+def test_linear_bf16x2_cells_within_tolerance(kom, ndim, p, shape, dtype):
+    ons = oracle.volume if ndim == 3 else oracle.image
+    hi = _data(shape, dtype, 11)
+    w, b = _weights(ndim, p, 12, dtype)
+    window = ons.pad_neighborhood(ons.lowres_from_highres(ons.pad_highres(hi)[0]), p)
+    pred = kom.LinearPredictor(w, b, p, ndim, arith='bf16x2')
+    cells, cells_f = pred.predict_cells(window, with_f32=True)
+    feats = ons.features_from_lowres(window, p)
+    exact, _ = OP.linear_predictions(feats, w, b, dtype)
+    split = OP.linear_bf16x2_split(feats, w, b)
+    n_axis = feats.ndim - 2
+    scale = np.tensordot(np.moveaxis(np.abs(feats.astype(np.float64)), n_axis, -1), np.abs(w.astype(np.float64)),
+                         axes=([-1], [0]))
+    scale = np.moveaxis(scale, -1, ndim + 1) + np.abs(b).reshape(-1, 1)
+    assert cells_f.shape == exact.shape
+    assert np.all(np.abs(cells_f - exact) <= 1e-5 * scale), np.max(np.abs(cells_f - exact) / scale)
+    assert np.all(np.abs(cells_f - split) <= 2e-6 * scale), np.max(np.abs(cells_f - split) / scale)
+    assert np.array_equal(cells, OP.cast_from_f32(cells_f, dtype))
+
+
+@pytest.mark.parametrize('ndim,p,shape,dtype', BF_CASES)
+def test_linear_bf16x2_codec_paths_agree(kom, ndim, p, shape, dtype):
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    hi = _data(shape, dtype, 13)
+    w, b = _weights(ndim, p, 14, dtype)
+    pred = kom.LinearPredictor(w, b, p, ndim, arith='bf16x2')
+    enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if dtype == np.uint16 else \
+               (ns.encode_values_uint8, ns.decode_values_uint8)
+    oenc = ons.encode_values_uint16 if dtype == np.uint16 else ons.encode_values_uint8
+    lo, (maps, dims) = ns.encode(pred, enc, hi, padding=p)
+    # the fused matrix-core kernel serves FULL volumes whose 16 / 32-wide rows split into 1, 2 or 4
+    # wave steps; the rest runs the generic codec on the same arithmetic
+    ex, ey, vx = shape[3] // 2, shape[2] // 2, 8 // np.dtype(dtype).itemsize
+    rows = 64 // max(1, ex // vx)
+    fused = (ndim == 3 and p == 0 and shape[2] % 2 == 0 and shape[3] % 2 == 0 and ex in (16, 32)
+             and ey % rows == 0 and ey // rows in (1, 2, 4))
+    assert kom._lib.lib.kmp_last_launch().decode() == ('linear3m_encode' if fused else 'encode_generic')
+    # (3) residuals == the oracle's coder on the kernel's own predictions (the callable's maps)
+    padded = ons.pad_highres(hi)[0]
+    pmaps = pred(ons.pad_neighborhood(ons.lowres_from_highres(padded), p))
+    want = ons.trim_maps([oenc(pm, g) for pm, g in zip(pmaps, ons.maps_from_highres(padded))], dims)
+    for i, (a, c) in enumerate(zip(maps, want)):
+        assert np.array_equal(a, c), f'map {i}: {np.count_nonzero(a != c)} mismatches'
+    # (2) the callback path (opaque predictions_fn = the same predictor) gives the same bits
+    lo2, (maps2, _) = ns.encode(lambda x: pred(x), enc, hi, padding=p)
+    assert np.array_equal(lo2, lo) and all(np.array_equal(a, c) for a, c in zip(maps2, maps))
+    # (4) lossless, fused and across paths, and chunked
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), hi)
+    assert np.array_equal(ns.decode(lambda x: pred(x), dec, lo, (maps, dims), padding=p), hi)
+    assert np.array_equal(ns.decode_chunks(pred, dec, lo, (maps, dims), chunk=6, padding=p), hi)
+    lo3, (maps3, _) = ns.encode_chunks(pred, enc, hi, chunk=6, padding=p)
+    assert np.array_equal(lo3, lo) and all(np.array_equal(a, c) for a, c in zip(maps3, maps))
+
+
+def test_linear_bf16x2_rejects_32bit_samples(kom):
+    """The byte split is exact only for 8 / 16-bit samples: 32-bit samples raise, never round."""
+    hi = _data((1, 9, 9, 9, 1), np.uint16, 1).astype(np.int32)
+    w, b = _weights(3, 0, 2, np.uint16)
+    pred = kom.LinearPredictor(w, b, 0, 3, arith='bf16x2')
+    with pytest.raises(Exception):
+        kom.volume.encode(pred, kom.volume.encode_values_raw, hi)

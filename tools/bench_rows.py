@@ -128,6 +128,14 @@ def main():
                    OP.linear_predictions_fn(p, w, b, 3), V.encode_values_uint16, V.decode_values_uint16,
                    OV.encode_values_uint16, OV.decode_values_uint16, p, raw_v, 3)
 
+    rng_bf = np.random.default_rng(1)
+    for p in (0, 1):  # the matrix-core arithmetic (arith='bf16x2'), the same weights as the f32 rows
+        n = (2 * p + 2) ** 3
+        w = (1.0 / n + rng_bf.standard_normal((n, 19)) * (0.3 / n)).astype(np.float32)
+        b = np.zeros(19, np.float32)
+        codec_rows(f'volume_linear_bf16x2_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3, arith='bf16x2'),
+                   None, V.encode_values_uint16, V.decode_values_uint16, None, None, p, raw_v, 3, with_cpu=False)
+
     for p in (0,):
         n = (2 * p + 2) ** 2
         w = (1.0 / n + rng.standard_normal((n, 5)) * (0.3 / n)).astype(np.float32)
@@ -354,6 +362,47 @@ def main():
             del lo3, maps3, rec3, ws3
             del tiles, lo, maps, maps2, lo2, b_r, b_p, vol512, res, cnt
         del field
+
+    # the file path end to end (the user's view of compress / decompress):
+    # numpy C3 volume -> container.compress -> file -> container.decompress -> numpy, host-inclusive
+    # wall time (H2D, device pipeline, device CRC-32, D2H through pinned staging, file write / read),
+    # with the split of the last call; structured volume (smooth field + N(0, 4^2) noise)
+    if not want or 'file' in want:
+        import tempfile
+        zz, yy, xx = torch.meshgrid(*[torch.arange(512, device='cuda', dtype=torch.float32)] * 3, indexing='ij')
+        field = torch.sin(xx / 41.0) * torch.cos(yy / 29.0) + torch.sin(zz / 53.0 + xx / 97.0)
+        field = 4000 + 9000 * (field - field.min()) / (field.max() - field.min())
+        del zz, yy, xx
+        gen = torch.Generator(device='cuda').manual_seed(0)
+        v = (field + 4.0 * torch.randn(field.shape, device='cuda', generator=gen)).round().clamp(0, 65535)
+        del field
+        host = v.to(torch.int32).to(torch.uint16).view(8, 64, 8, 64, 8, 64).permute(0, 2, 4, 1, 3, 5) \
+            .reshape(512, 64, 64, 64, 1).contiguous().cpu().numpy()
+        del v
+        pred = kom.MeanPredictor(0, 3)
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, 'c3.kmp')
+            for levels in (1, 'auto'):
+                kom.container.compress(path, host, pred, levels=levels)
+                assert np.array_equal(kom.container.decompress(path), host)
+                tc, td_ = [], []
+                for _ in range(max(3, args.reps // 2)):
+                    t = time.perf_counter()
+                    info = kom.container.compress(path, host, pred, levels=levels)
+                    tc.append(time.perf_counter() - t)
+                    split_c = dict(kom.container.last_timing)
+                    t = time.perf_counter()
+                    kom.container.decompress(path)
+                    td_.append(time.perf_counter() - t)
+                    split_d = dict(kom.container.last_timing)
+                tcm, tdm = float(np.median(tc)), float(np.median(td_))
+                tag = f'file_l{levels}'
+                for name, tm, split in (('compress', tcm, split_c), ('decompress', tdm, split_d)):
+                    print(json.dumps({'row': f'{tag}:{name}', 'what': f'numpy 512^3 u16 (512 x 64^3) -> file -> numpy, '
+                                      f'levels={levels}, MeanPredictor(0), host-inclusive',
+                                      'GBps_raw': round(raw_v / tm / 1e9, 2), 'ms': round(tm * 1e3, 2),
+                                      'ratio': round(info['ratio'], 3), 'file_bytes': info['bytes'],
+                                      'split_ms': {k: round(v * 1e3, 2) for k, v in split.items()}}), flush=True)
 
     # geometry primitives (volume/utils.py) on the C3 tile batch
     if not want or 'primitives' in want:

@@ -1,5 +1,5 @@
 """Launch the fused volume/image codec N times per direction (for rocprofv3 --kernel-trace --stats).
-    python tools/ktime.py [volume|image] [padding] [reps] [mean|linear]
+    python tools/ktime.py [volume|image] [padding] [reps] [mean|linear|linearmx]
     python tools/ktime.py rice SIGMA [reps]   (the Rice bundle kernels on a C3 encode result)"""
 import os, sys
 import numpy as np, torch
@@ -41,10 +41,11 @@ ndim = 3 if wl == 'volume' else 2
 shape, dt = ((512, 64, 64, 64, 1), np.uint16) if ndim == 3 else ((1024, 256, 256, 1), np.uint8)
 host = np.random.default_rng(0).integers(0, np.iinfo(dt).max + 1, size=shape, dtype=np.int64).astype(dt)
 hi = torch.from_numpy(host).cuda()
-if len(sys.argv) > 4 and sys.argv[4] == 'linear':
+if len(sys.argv) > 4 and sys.argv[4] in ('linear', 'linearmx'):
     n, k = (2 * p + 2) ** ndim, 19 if ndim == 3 else 5
     w = (1.0 / n + np.random.default_rng(1).standard_normal((n, k)) * (0.3 / n)).astype(np.float32)
-    pred = kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim)
+    pred = kom.LinearPredictor(w, np.zeros(k, np.float32), p, ndim,
+                               arith='bf16x2' if sys.argv[4] == 'linearmx' else 'f32')
 else:
     pred = kom.MeanPredictor(p, ndim)
 if len(sys.argv) > 4 and sys.argv[4] == 'callback':  # the callback path: opaque predictions_fn

@@ -16,7 +16,7 @@ name, src, flags = sys.argv[1], sys.argv[2], sys.argv[3:]
 _build.build(verbose=False)
 objs = sorted(os.path.join(_build.BUILD, f) for f in os.listdir(_build.BUILD) if f.endswith('.o'))
 vobj = os.path.join('/tmp', f'variant_{name}_' + src.replace('.hip', '.o'))
-subprocess.run([_build.HIPCC, *_build.FLAGS, *flags, '-c', os.path.join(_build.CSRC, src), '-o', vobj], check=True)
+subprocess.run([_build.HIPCC, *_build.FLAGS, *_build.FILE_FLAGS.get(src, []), *flags, '-c', os.path.join(_build.CSRC, src), '-o', vobj], check=True)
 objs = [vobj if os.path.basename(o) == src.replace('.hip', '.o') else o for o in objs]
 out = os.path.join(PKG, f'libkompressor_hip_{name}.so')
 subprocess.run([_build.HIPCC, f'--offload-arch={_build.ARCH}', '-shared', '-fPIC', *objs, '-o', out], check=True)
