@@ -60,10 +60,8 @@ def all_gather_tiles(local, n_units, group=None):
     """Reassemble the full ``[n_units, ...]`` batch on every rank from each rank's
     :func:`shard_range` slice ``local``, as a new tensor (never an alias of ``local``).  Byte
     views travel, so any dtype does (RCCL has no uint16).  Equal shards: one
-    ``all_gather_into_tensor`` straight into the result.  Uneven shards over RCCL: the list form
-    with each rank's exact slice of the result as its receive buffer (torch issues it as coalesced
-    broadcasts), so no padding and no concatenation copy afterwards; over gloo (CPU tests) the
-    shards are padded to the largest and the padding dropped."""
+    ``all_gather_into_tensor`` straight into the result (the list form over gloo).  Uneven shards:
+    padded to the largest, gathered the same way, the padding dropped."""
     world, rank = world_and_rank(group)
     if world == 1:
         return local.clone()
@@ -76,22 +74,26 @@ def all_gather_tiles(local, n_units, group=None):
     send = local.contiguous()
     sb = send.view(torch.uint8).reshape(-1)
     nccl = dist.get_backend(group) == 'nccl'
-    if n_units == per * world or nccl:
+    if n_units == per * world:
         out = torch.empty((n_units, *row), dtype=local.dtype, device=local.device)
         ob = out.view(torch.uint8).reshape(-1)
-        if n_units == per * world and nccl:
+        if nccl:
             dist.all_gather_into_tensor(ob, sb, group=group)
         else:
-            unit = ob.numel() // max(n_units, 1)
-            views = [ob[unit * rb:unit * re_] for rb, re_ in (shard_range(n_units, r, world) for r in range(world))]
-            dist.all_gather(views, sb, group=group)
+            dist.all_gather(list(ob.chunk(world)), sb, group=group)
         return out
-    # gloo, uneven shards: equal-size padded slabs
+    # uneven shards (including ranks with none): equal-size padded slabs -- one
+    # all_gather_into_tensor over RCCL, the list form over gloo -- and the padding dropped.  (The
+    # RCCL list form with exact-size receive views would save the padding but has never run on a
+    # multi-GPU box here, so it is not used.)
     pad = torch.empty((per, *row), dtype=local.dtype, device=local.device)
     pad[:send.shape[0]].copy_(send)
     full = torch.empty((per * world, *row), dtype=local.dtype, device=local.device)
-    dist.all_gather(list(full.view(torch.uint8).reshape(-1).chunk(world)), pad.view(torch.uint8).reshape(-1),
-                    group=group)
+    fb, pb = full.view(torch.uint8).reshape(-1), pad.view(torch.uint8).reshape(-1)
+    if nccl:
+        dist.all_gather_into_tensor(fb, pb, group=group)
+    else:
+        dist.all_gather(list(fb.chunk(world)), pb, group=group)
     parts = []
     for r in range(world):
         rb, re_ = shard_range(n_units, r, world)
