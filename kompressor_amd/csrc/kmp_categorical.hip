@@ -201,8 +201,14 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_decode_select_kern
 //   over the bins to pick the one that holds rank k (its lane by one ballot, the bin inside the
 //   lane on the scalar unit), and a bitwise radix select inside that bin, stopping as soon as the
 //   key range [t, hi) that holds rank k contains one key.  Then the m-th highest class index with
-//   a key in [t, hi).
+//   a key in [t, hi) -- when the last bin holds one key, its class straight from the bin's
+//   owner slot (written beside the histogram), otherwise from ballots.  Ranks and ranges are 32-bit
+//   scalar arithmetic throughout (VALU issue is the bound: r3 SQ counters, 130 VALU per element).
 constexpr int kCatPF = 4;  // 8 measured no faster (r3s54: decode 394-397 vs 376-385 us)
+// Decode ranks below kCatPeel take k + 1 wave max-reductions (~20 VALU each) instead of the radix
+// select (a histogram round is ~35 VALU, one to three rounds per element): a good predictor's ranks
+// (bench_rows decode_small_ranks, ranks < 4) stay on the peel.
+constexpr int kCatPeel = 4;
 typedef float cat_f32x4 __attribute__((ext_vector_type(4)));
 
 template <int E4>
@@ -211,23 +217,24 @@ struct CatRow {
   uint32_t xv;  // the element's value (gt / enc), raw 32-bit pattern, in a VGPR
 };
 
-// The value is read as the aligned dword that holds it (cat_xval shifts it out when the element
-// is ranked), through an address with a divergent zero (zero0 below): a wave-uniform load, or a
-// sub-dword one, is moved to a scalar register or masked right at the load, which waits the load
-// out there instead of when the element is ranked PF elements later.
+// Rows and values are read through buffer resources over the wave's range (soffset = the element's
+// byte offset, on the scalar unit; voffset = the lane's constant offset), so no per-element
+// address arithmetic runs on the VALU, whose issue bounds this kernel.  The value is read as the
+// aligned dword that holds it (cat_xval shifts it out when the element is ranked), through a
+// divergent zero voffset (zero0 below): a wave-uniform load would be moved to a scalar register
+// and waited out right at the load instead of when the element is ranked PF elements later.
 template <typename T, int E4, bool FULL>
-__device__ __forceinline__ void cat_load(const cat_f32x4* __restrict__ row, const T* __restrict__ xe, int64_t L,
-                                         int lane, uint32_t zero0, CatRow<E4>& r) {
+__device__ __forceinline__ void cat_load(__amdgpu_buffer_rsrc_t rows, uint32_t roff, __amdgpu_buffer_rsrc_t xs,
+                                         uint32_t xoff, int64_t L, int lane, uint32_t zero0, CatRow<E4>& r) {
   const float qnan = __builtin_nanf("");
 #pragma unroll
   for (int s = 0; s < E4; ++s) {
     const int c4 = s * 64 + lane;
-    r.v[s] = FULL || 4 * c4 < L ? __builtin_nontemporal_load(row + c4) : (cat_f32x4){qnan, qnan, qnan, qnan};
+    r.v[s] = FULL || 4 * c4 < L
+                 ? __builtin_bit_cast(cat_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rows, (uint32_t)c4 * 16u, roff, 2))
+                 : (cat_f32x4){qnan, qnan, qnan, qnan};
   }
-  // the dword lies in the same page as the element: reading its other bytes cannot fault
-  const char* a = (const char*)xe;
-  a -= (uintptr_t)a & 3;  // scalar; pointer arithmetic keeps it a global (not flat) load
-  r.xv = *(const uint32_t*)(a + zero0);  // scalar base + 32-bit vector offset: no address VALU
+  r.xv = __builtin_amdgcn_raw_buffer_load_b32(xs, zero0, xoff, 0);
 }
 template <typename T>
 __device__ __forceinline__ int64_t cat_xval(const T* xe, uint32_t word) {  // xe: the element's value
@@ -267,12 +274,19 @@ __device__ __forceinline__ uint32_t order_key_fast(float f) {  // == order_key
   return z != z ? 0xffffffffu : k;
 }
 
+// max(a - b, 0) on the scalar unit (the compiler's form is a clamped VALU subtract and a readback)
+__device__ __forceinline__ int s_floor_sub(int a, int b) {
+  int r;
+  asm("s_sub_i32 %0, %1, %2\n\ts_max_i32 %0, %0, 0" : "=&s"(r) : "s"(a), "s"(b) : "scc");
+  return r;
+}
+
 __device__ __forceinline__ uint64_t lanes_below(int nl) {  // mask of lanes 0 .. nl-1
   return nl <= 0 ? 0ull : nl >= 64 ? ~0ull : ((1ull << nl) - 1);
 }
 
 template <typename T, int DIR, int E4, bool FULL>
-__device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins, int peel,
+__device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane, uint32_t* bins,
                                       int64_t xv) {  // the element's code (wave-uniform)
   if constexpr (DIR == KMP_ENCODE) {
     const int64_t g = xv;
@@ -321,9 +335,10 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
     uint32_t key[E4][4];
     bool ok[E4][4];
     // every logit in [+0, +inf] (softmax output, the reference's categorical predictor): the float
-    // bits are already order-preserving, and + 1 keeps key 0 for padding -- one add per key instead
-    // of order_key's six operations.  -0, negatives and NaN (bits above +inf) take order_key.
-    uint32_t mx = 0;
+    // bits are already order-preserving -- no work per key when every class exists (FULL), + 1 to
+    // keep key 0 for padding otherwise -- instead of order_key's six operations.  -0, negatives and
+    // NaN (bits above +inf) take order_key.  lmax: the lane's largest key.
+    uint32_t mx = 0, lmax;
 #pragma unroll
     for (int s = 0; s < E4; ++s)
 #pragma unroll
@@ -335,53 +350,66 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
 #pragma unroll
       for (int s = 0; s < E4; ++s)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) key[s][q] = ok[s][q] ? __float_as_uint(cur.v[s][q]) + 1u : 0u;
+        for (int q = 0; q < 4; ++q)
+          key[s][q] = FULL ? __float_as_uint(cur.v[s][q]) : ok[s][q] ? __float_as_uint(cur.v[s][q]) + 1u : 0u;
+      lmax = FULL ? mx : mx + 1u;  // (an empty lane's 1 is below the wave's largest valid key)
     } else {
+      lmax = 0;
 #pragma unroll
       for (int s = 0; s < E4; ++s)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) key[s][q] = ok[s][q] ? order_key_fast(cur.v[s][q]) : 0u;  // padding keys 0
+        for (int q = 0; q < 4; ++q) {
+          key[s][q] = ok[s][q] ? order_key_fast(cur.v[s][q]) : 0u;  // padding keys 0
+          lmax = max(lmax, key[s][q]);
+        }
     }
-    auto count = [&](auto pred) {  // wave-uniform #{classes j with pred(key_j)}; pred(0) is false
-      uint32_t c = 0;
-#pragma unroll
-      for (int s = 0; s < E4; ++s)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) c += __popcll(__ballot(pred(key[s][q])));
-      return c;
-    };
-    const int64_t kk = xv;
-    const uint32_t k = (uint32_t)(kk < 0 ? 0 : (kk >= L ? L - 1 : kk));
-    uint32_t t = 0, m = 0;
-    uint64_t hi = 1ull << 32;  // the answer's key lies in [t, hi); m = its rank among those keys
-    if ((int)k < peel) {
-      uint32_t taken = 0;
+    // the rank, clamped to [0, L) in 32-bit scalar arithmetic (xv holds a T value; L <= 512 here)
+    uint32_t k = std::is_signed<T>::value ? (uint32_t)max((int32_t)xv, 0) : (uint32_t)xv;
+    k = min(k, (uint32_t)L - 1u);
+    // The answer's key lies in [t, t | span] (t's low bits below span are zero); m = its rank among
+    // the keys there.  cls: the class itself once the range is known to hold one key.
+    uint32_t t = 0, span = 0, m = 0;
+    int cls = -1;
+    uint64_t w[E4][4];  // ballots of the keys in the range (the peel's last round)
+    bool have_w = false;
+    if (k < (uint32_t)kCatPeel) {
+      // the largest key, its ties; while those are all above rank k, the largest key below it.
+      // "Largest key below wmax" as one add and one max per key: key + c (c = -wmax) wraps the keys
+      // below wmax above every other (padding keys 0 included, which never win: k < L valid keys).
+      uint32_t taken = 0, wmax = wave_max_dpp(lmax);
       while (true) {
-        uint32_t best = 0;  // valid keys are > 0 (order_key of -inf is 0x007fffff; the bits + 1 >= 1)
+        uint32_t ties = 0;
 #pragma unroll
         for (int s = 0; s < E4; ++s)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if ((uint64_t)key[s][q] < hi) best = max(best, key[s][q]);
-        const uint32_t wmax = wave_max_dpp(best);
-        const uint32_t ties = count([&](uint32_t v) { return v == wmax; });
+          for (int q = 0; q < 4; ++q) {
+            w[s][q] = __ballot(key[s][q] == wmax);
+            ties += (uint32_t)__popcll(w[s][q]);
+          }
         if (taken + ties > k) {
           t = wmax;
           m = k - taken;
-          hi = (uint64_t)wmax + 1;
           break;
         }
         taken += ties;
-        hi = wmax;
+        const uint32_t c = 0u - wmax;
+        uint32_t best = 0;
+#pragma unroll
+        for (int s = 0; s < E4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) best = max(best, key[s][q] + c);
+        wmax = wave_max_dpp(best) - c;
       }
+      have_w = true;
     } else {
       // radix select on digits of up to 8 bits from the top of the bits in which the keys differ
       // (P of them below the common prefix): per round a 256-bin LDS histogram of the digit over
-      // the keys in the current range [t, hi) (bin = digit, one bit-field extract per key), a DPP
-      // scan over the bins in descending digit order, the bin that holds rank k; the range narrows
-      // to that bin.  Stops when
-      // the bin holds one key or the digits run out (ties).  Two rounds isolate the key for
-      // softmax rows, whose first digit is mostly exponent bits (up to half the keys in one bin)
+      // the keys in the current range (bin = digit, one bit-field extract per key), a DPP scan over
+      // the bins in descending digit order, the bin that holds rank k; the range narrows to that
+      // bin.  Stops when the bin holds one key or the digits run out (ties).  Every key also writes
+      // its class into the owner slot of its bin (own[d], same address register, immediate offset):
+      // when the final bin holds one key, that slot names the class -- one LDS read, no ballots.
+      uint32_t* own = bins + 256;
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[0][0]);  // class 0 exists
       uint32_t dif = 0;
 #pragma unroll
@@ -390,29 +418,11 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
         for (int q = 0; q < 4; ++q) dif |= ok[s][q] ? key[s][q] ^ k0 : 0u;
       dif = wave_or_dpp(dif);
       const int P = dif == 0 ? 0 : 32 - __clz((int)dif);
-      int sh = P > 8 ? P - 8 : 0, wd = P - sh;  // digit = bits [sh, sh + wd)
+      int sh = s_floor_sub(P, 8), wd = P - sh;  // digit = bits [sh, sh + wd)
       t = P >= 32 ? 0u : (k0 >> P) << P;
-      uint32_t c_hi = 0;  // keys above the range
-      for (int round = 0;; ++round) {
-        *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t dm = (1u << wd) - 1u;
-        if (round == 0) {
-#pragma unroll
-          for (int s = 0; s < E4; ++s)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (ok[s][q]) atomicAdd(bins + __builtin_amdgcn_ubfe(key[s][q], (uint32_t)sh, (uint32_t)wd), 1u);
-        } else {  // keys in the range [t, t + 2^(sh + wd)): (key >> sh) - (t >> sh) <= dm, and that is the digit
-          const uint32_t lo = t >> sh;
-#pragma unroll
-          for (int s = 0; s < E4; ++s)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const uint32_t d = (key[s][q] >> sh) - lo;
-              if (ok[s][q] && d <= dm) atomicAdd(bins + d, 1u);
-            }
-        }
+      uint32_t c_hi = 0, cnt, dig;  // c_hi: keys above the range
+      // the bin that holds rank k: its digit, its count; keys above it into c_hi
+      auto pick_bin = [&](uint32_t dm) {
         __builtin_amdgcn_wave_barrier();
         // bins in ascending digit order; lane l takes digits 255 - 4 l down to 252 - 4 l
         const uint4 bu = *(const uint4*)(bins + 4 * (63 - lane));
@@ -426,7 +436,8 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
         const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)bu.z, ls);
         const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)bu.y, ls);
         const uint32_t b3 = (uint32_t)__builtin_amdgcn_readlane((int)bu.x, ls);
-        uint32_t cnt = b0, q = 0;
+        uint32_t q = 0;
+        cnt = b0;
         if (r >= cb + b0) {
           cb += b0; cnt = b1; q = 1;
           if (r >= cb + b1) {
@@ -435,52 +446,93 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
           }
         }
         c_hi += cb;
-        const uint32_t digit = (255u - (uint32_t)(4 * ls + (int)q)) & dm;
-        t |= digit << sh;
-        if (cnt <= 1 || sh == 0) break;
-        const int nsh = sh > 8 ? sh - 8 : 0;
+        dig = (255u - (uint32_t)(4 * ls) - q) & dm;
+        t |= dig << sh;
+      };
+      *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (ok[s][q]) {
+            const uint32_t d = __builtin_amdgcn_ubfe(key[s][q], (uint32_t)sh, (uint32_t)wd);
+            atomicAdd(bins + d, 1u);
+            own[d] = (uint32_t)(s * 256 + 4 * lane + q);
+          }
+      pick_bin((1u << wd) - 1u);
+      while (cnt > 1u && sh != 0) {
+        const int nsh = s_floor_sub(sh, 8);
         wd = sh - nsh;
         sh = nsh;
-        __builtin_amdgcn_wave_barrier();  // the next round's zeroing must not overtake these reads
-      }
-      hi = (uint64_t)t + (1ull << sh);
-      m = k - c_hi;
-    }
-    // the m-th highest class index among the classes with key in [t, hi); padding keys (0) are
-    // below every valid key (>= 1), so the range starts at 1 at the least
-    const uint32_t tlo = t > 0 ? t : 1u;
-    // key in [tlo, hi) as one unsigned compare: key - tlo <= span (hi - 1 < tlo: no key, no class)
-    const bool none = hi - 1 < (uint64_t)tlo;
-    const uint32_t span = (uint32_t)(hi - 1 - tlo);
-    int64_t cls = 0;
-    for (int s = E4 - 1; s >= 0; --s) {
-      uint64_t w[4];
-      uint32_t tot = 0;
+        const uint32_t dm = (1u << wd) - 1u;
+        __builtin_amdgcn_wave_barrier();  // the zeroing must not overtake the last round's reads
+        *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_wave_barrier();
+        // keys in the range [t, t + 2^(sh + wd)): (key >> sh) - (t >> sh) <= dm, and that is the digit
+        const uint32_t lo = t >> sh;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        w[q] = none ? 0ull : __ballot(key[s][q] - tlo <= span);
-        tot += __popcll(w[q]);
-      }
-      if (m >= tot) {
-        m -= tot;
-        continue;
-      }
-      uint64_t lanes = w[0] | w[1] | w[2] | w[3];
-      while (true) {  // lanes from the highest; within a lane q from 3 down
-        const int l = 63 - __clzll(lanes);
-        int q = 3;
-        for (; q >= 0; --q)
-          if ((w[q] >> l) & 1) {
-            if (m == 0) break;
-            --m;
+        for (int s = 0; s < E4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t d = (key[s][q] >> sh) - lo;
+            if (ok[s][q] && d <= dm) {
+              atomicAdd(bins + d, 1u);
+              own[d] = (uint32_t)(s * 256 + 4 * lane + q);
+            }
           }
-        if (q >= 0) {
-          cls = s * 256 + 4 * l + q;
+        pick_bin(dm);
+      }
+      span = (1u << sh) - 1u;  // sh <= 24
+      m = k - c_hi;
+      // the final round's writes precede this read in the wave's LDS order
+      if (cnt == 1u) cls = __builtin_amdgcn_readfirstlane((int)own[dig]);
+    }
+    if (cls < 0) {
+      // the m-th highest class index among the classes with a key in [tlo, t | span]; padding keys
+      // (0) are below every valid key (>= 1), so without FULL the range starts at 1 at the least
+      if (!have_w) {
+        const uint32_t tlo = FULL || t > 0 ? t : 1u, ext = (t | span) - tlo;
+#pragma unroll
+        for (int s = 0; s < E4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[s][q] = __ballot(key[s][q] - tlo <= ext);
+      }
+      cls = 0;
+#pragma unroll
+      for (int s = E4 - 1; s >= 0; --s) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tot += (uint32_t)__popcll(w[s][q]);
+        if (m >= tot) {
+          m -= tot;
+          continue;
+        }
+        if (tot == 1u) {  // one key: its lane and slot, no walk
+          int c = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) c = w[s][q] ? 4 * __builtin_ctzll(w[s][q]) + q : c;
+          cls = s * 256 + c;
           break;
         }
-        lanes &= ~(1ull << l);
+        // ties: lanes from the highest; within a lane q from 3 down
+        uint64_t lanes = w[s][0] | w[s][1] | w[s][2] | w[s][3];
+        while (true) {
+          const int l = 63 - __clzll(lanes);
+          int q = 3;
+          for (; q >= 0; --q)
+            if ((w[s][q] >> l) & 1) {
+              if (m == 0) break;
+              --m;
+            }
+          if (q >= 0) {
+            cls = s * 256 + 4 * l + q;
+            break;
+          }
+          lanes &= ~(1ull << l);
+        }
+        break;
       }
-      break;
     }
     return (T)cls;
   }
@@ -489,8 +541,8 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
 template <typename T, int DIR, int E4, int PF, bool FULL>
 __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const float* __restrict__ logits, int64_t n,
                                                                           int64_t L, const T* __restrict__ x,
-                                                                          T* __restrict__ out, int peel) {
-  __shared__ __attribute__((aligned(16))) uint32_t bins_all[kCatWaves][256];
+                                                                          T* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t bins_all[kCatWaves][512];  // bins, owner slots
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
   uint32_t* bins = bins_all[wv];
@@ -505,28 +557,38 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
   // (the loop stops PF elements before the range's end) so the outstanding count at each use is
   // the same PF - 1.  Row, value and code pointers advance on the scalar unit.
   const uint32_t zero0 = (threadIdx.x >> 6) - (uint32_t)wv;  // 0, but not provably wave-uniform
-  const int64_t L4 = L / 4;
-  const cat_f32x4* rp = (const cat_f32x4*)logits + b * L4;
+  // the wave's rows and the dwords that hold its values (the host keeps a range's rows < 2^31 bytes)
+  const uint32_t rstride = (uint32_t)L * 4u;
+  const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(logits + b * L), (short)0, (int)((uint32_t)(end - b) * rstride), 0x00020000);
+  const uintptr_t xb = (uintptr_t)(x + b) & ~(uintptr_t)3;
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)xb, (short)0, (int)((((uintptr_t)(x + end - 1) & ~(uintptr_t)3) + 4) - xb), 0x00020000);
+  auto xoff = [&](const T* xe) { return (uint32_t)(((uintptr_t)xe & ~(uintptr_t)3) - xb); };
+  uint32_t ro = 0;
   const T* xp = x + b;
   T* op = out + b;
   int64_t e = b;
   CatRow<E4> ring[PF];
   auto rank = [&](int u, const T* xe) {
     const uint32_t xw = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[u].xv);
-    return cat_rank<T, DIR, E4, FULL>(ring[u], L, lane, bins, peel, cat_xval<T>(xe, xw));
+    return cat_rank<T, DIR, E4, FULL>(ring[u], L, lane, bins, cat_xval<T>(xe, xw));
+  };
+  auto load = [&](int u, int j) {  // element e + j into ring[u]
+    cat_load<T, E4, FULL>(rows, ro + (uint32_t)j * rstride, xs, xoff(xp + j), L, lane, zero0, ring[u]);
   };
   const bool main = b + 2 * PF <= end;
   if (main) {
 #pragma unroll
-    for (int u = 0; u < PF; ++u) cat_load<T, E4, FULL>(rp + u * L4, xp + u, L, lane, zero0, ring[u]);
+    for (int u = 0; u < PF; ++u) load(u, u);
     do {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const T code = rank(u, xp + u);
         if (lane == 0) op[u] = code;
-        cat_load<T, E4, FULL>(rp + (u + PF) * L4, xp + u + PF, L, lane, zero0, ring[u]);
+        load(u, u + PF);
       }
-      rp += PF * L4;
+      ro += PF * rstride;
       xp += PF;
       op += PF;
       e += PF;
@@ -534,7 +596,7 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
   } else {
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-      if (e + u < end) cat_load<T, E4, FULL>(rp + u * L4, xp + u, L, lane, zero0, ring[u]);
+      if (e + u < end) load(u, u);
   }
   // the range's last elements (PF to 2 PF - 1 after the main loop, fewer without it): ring[u]
   // holds element e + u; reload a slot only while elements remain
@@ -543,7 +605,7 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
     if (e + u < end) {
       const T code = rank(u, xp + u);
       if (lane == 0) op[u] = code;
-      if (e + u + PF < end) cat_load<T, E4, FULL>(rp + (u + PF) * L4, xp + u + PF, L, lane, zero0, ring[u]);
+      if (e + u + PF < end) load(u, u + PF);
     }
 #pragma unroll
   for (int u = 0; u < PF - 1; ++u)
@@ -567,16 +629,17 @@ extern "C" int kmp_categorical(int32_t direction, const float* logits, int64_t n
   const unsigned grid = (unsigned)(g > 65536 ? 65536 : g);
   // vector form: 8 waves per SIMD over the chip, each walking its elements one load ahead
   const bool vec = L % 4 == 0 && L <= 512 && ((uintptr_t)logits & 15) == 0;
-  const unsigned vgrid = (unsigned)(g > 2048 ? 2048 : g);
-  const char* pv = std::getenv("KMP_CAT_PEEL");  // decode ranks below this peel maxima
-  const int peel = pv ? std::atoi(pv) : 4;
+  // a wave's rows (buffer resource, 32-bit offsets) stay below 2^31 bytes: more waves for huge n
+  const int64_t per_max = ((int64_t)1 << 31) / (L * 4) - 1;
+  const int64_t g_min = (n + per_max * kCatWaves - 1) / (per_max * kCatWaves);
+  const unsigned vgrid = (unsigned)std::max<int64_t>(g > 2048 ? 2048 : g, g_min);
   return dispatch_int_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     if (vec) {
       constexpr int PF = kCatPF;
       hipStream_t st = (hipStream_t)stream;
       // FULL: L == 256 E4, no padding classes (no per-class masks)
-      auto go = [&](auto kern) { kern<<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out, peel); };
+      auto go = [&](auto kern) { kern<<<vgrid, 64 * kCatWaves, 0, st>>>(logits, n, L, (const T*)x, (T*)out); };
       if (direction == KMP_ENCODE && L <= 256)
         L == 256 ? go(categorical_vec_kernel<T, KMP_ENCODE, 1, PF, true>) : go(categorical_vec_kernel<T, KMP_ENCODE, 1, PF, false>);
       else if (direction == KMP_ENCODE)

@@ -421,6 +421,32 @@ def test_categorical_coder_vs_oracle(kom, vec):
                               oracle.common.decode_categorical(logits, x)), L
 
 
+@pytest.mark.parametrize('dt', [np.uint8, np.uint16])
+@pytest.mark.parametrize('off', [1, 2, 3])
+def test_categorical_value_offsets(kom, dt, off):
+    """Values (classes / ranks) that start off elements past an aligned address: the vector
+    kernels read each value as the aligned dword that holds it and shift it out (cat_xval), so
+    every byte position inside the dword is exercised, on both directions and on the peel and radix
+    paths of the decode."""
+    import oracle
+    n, L = 2053, 256
+    rng = np.random.default_rng(19 + off)
+    logits = rng.random((n, L)).astype(np.float32)
+    logits[::4] = rng.standard_normal((logits[::4].shape[0], L)).astype(np.float32)
+    x = rng.integers(0, L, n).astype(dt)
+    x[::2] = rng.integers(0, 4, x[::2].size)  # small ranks: the peel
+    lg = torch.from_numpy(logits).cuda()
+    buf = torch.zeros(n + 4, dtype=torch.uint8 if dt == np.uint8 else torch.int16, device='cuda')
+    xg = buf[off:off + n]
+    xg.copy_(torch.from_numpy(x.view(np.int16) if dt == np.uint16 else x))
+    if dt == np.uint16:
+        xg = xg.view(torch.uint16)
+    assert np.array_equal(kom.utils.encode_categorical(lg, xg).cpu().numpy().astype(dt),
+                          oracle.common.encode_categorical(logits, x))
+    assert np.array_equal(kom.utils.decode_categorical(lg, xg).cpu().numpy().astype(dt),
+                          oracle.common.decode_categorical(logits, x))
+
+
 @pytest.mark.parametrize('L,dt,rows', [(8, np.uint8, None), (8, np.uint16, None), (12, np.int32, None),
                                        (260, np.uint16, 3000), (256, np.uint8, 3000)])
 def test_categorical_long_ranges(kom, L, dt, rows):
