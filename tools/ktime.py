@@ -18,7 +18,8 @@ if wl == 'categorical':  # rank coder, 1M elements x 256 logits (tools/bench_row
     for _ in range(reps):
         enc = kom.volume.encode_categorical(logits, gt)
         dec = kom.volume.decode_categorical(logits, enc)
-        kom.volume.decode_categorical(logits, small)
+        if os.environ.get('KMP_CAT_SMALL', '1') != '0':  # 0: the uniform-rank decode only (counters)
+            kom.volume.decode_categorical(logits, small)
     torch.cuda.synchronize()
     assert torch.equal(dec, gt)
     print('ok', os.environ.get('KMP_TAG', ''))
