@@ -38,6 +38,7 @@ def _headers_mtime():
 # (-amdgpu-mfma-vgpr-form): with AGPRs every tile paid 4 accvgpr writes (the bias) and 4 reads
 # (the results) per MFMA, 256 VALU instructions per wave step of kmp_codec_linear3m.hip
 FILE_FLAGS = {'kmp_codec_linear3m.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form'],
+              'kmp_codec_linear3pm.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form'],
               'kmp_linear.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form']}
 
 

@@ -80,5 +80,24 @@ __device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, const f32x
                                                  0, 0);
 }
 
+// 4 MFMA results -> 4 samples of T (u8 / u16) packed little-endian in the low 4 * sizeof(T) bytes,
+// with the sample dtype's cast (XLA astype: truncate, NaN and negatives 0, saturate):
+// v_cvt_u32_f32 truncates with exactly that clamping at 0 and 2^32 - 1, v_cvt_pk_u16_u32
+// saturates a pair to 16 bits
+template <typename T>
+__device__ __forceinline__ uint2 cast_pack4(const f32x4& v) {
+  uint32_t u[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = (uint32_t)v[j];
+  if constexpr (sizeof(T) == 2) {
+    return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[0], u[1])),
+                      __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[2], u[3])));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) u[j] = u[j] < 255u ? u[j] : 255u;
+    return make_uint2(u[0] | (u[1] << 8) | (u[2] << 16) | (u[3] << 24), 0u);
+  }
+}
+
 }  // namespace bx
 }  // namespace kmp

@@ -29,6 +29,14 @@ template <typename T>
 int try_fast2d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
                       const kmp_predictor* pred, T* hi, const kmp_region* region, hipStream_t stream);
 template <typename T>
+int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                         const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+template <typename T>
+int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                         const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+template <typename T>
 int try_linear3m_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                         const MapPtrs& maps, const kmp_region* region, hipStream_t stream);
 template <typename T>

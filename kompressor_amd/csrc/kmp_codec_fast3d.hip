@@ -499,6 +499,8 @@ int try_fast_encode(int nsp, const T* hi, const Geo& g, int64_t B, int64_t C, co
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // linear p = 1
     if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3pm_encode<T>(hi, g, B, C, pred, lowres, maps, region, ws, ws_bytes, stream);  // matrix-core linear p = 1
+    if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     F3 a{};
@@ -534,6 +536,8 @@ int try_fast_decode(int nsp, const T* lowres, const CMapPtrs& maps, const Geo& g
     st = try_wave3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
     st = try_linear3dp_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
+    if (st != KMP_ERR_UNSUPPORTED) return st;
+    st = try_linear3pm_decode<T>(lowres, maps, g, B, C, pred, hi, region, ws, ws_bytes, stream);
     if (st != KMP_ERR_UNSUPPORTED) return st;
   }
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {

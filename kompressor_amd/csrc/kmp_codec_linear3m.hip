@@ -59,22 +59,6 @@ __device__ __forceinline__ uint2 node_words8(const uint4& v) {  // the even elem
   return make_uint2(__builtin_amdgcn_perm(v.y, v.x, sel), __builtin_amdgcn_perm(v.w, v.z, sel));
 }
 
-// 4 MFMA results -> 4 samples of T packed little-endian in the low 4 * sizeof(T) bytes
-template <typename T>
-__device__ __forceinline__ uint2 cast_pack4(const bx::f32x4& v) {
-  uint32_t u[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) u[j] = (uint32_t)v[j];
-  if constexpr (sizeof(T) == 2) {
-    return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[0], u[1])),
-                      __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[2], u[3])));
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) u[j] = u[j] < 255u ? u[j] : 255u;
-    return make_uint2(u[0] | (u[1] << 8) | (u[2] << 16) | (u[3] << 24), 0u);
-  }
-}
-
 template <typename T, bool DEC, int EX, int STEPS>
 __global__ void __launch_bounds__(64) linear3m_kernel(M3 a) {
   constexpr int VX = 8 / (int)sizeof(T);
@@ -256,7 +240,7 @@ __global__ void __launch_bounds__(64) linear3m_kernel(M3 a) {
         // at 0 and 2^32 - 1, v_cvt_pk_u16_u32 saturates a pair to 16 bits (1.5 instructions a value)
         const int cx = x0 + 4 * g;
         auto put = [&](int ch, const bx::f32x4& d) {
-          const uint2 v = cast_pack4<T>(d);
+          const uint2 v = bx::cast_pack4<T>(d);
           T* dst = ct + ch * (CSB / SZ) + ri * EX + cx;
           if constexpr (sizeof(T) == 2) *(uint2*)dst = v;
           else *(uint32_t*)dst = v.x;

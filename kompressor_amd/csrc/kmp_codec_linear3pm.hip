@@ -1,0 +1,532 @@
+// kmp_codec_linear3pm.hip -- one-pass volume encode / decode for the LinearPredictor with padding 1
+// on the matrix cores (KMP_PRED_LINEAR_MFMA; SURVEY.md §8a row a9', the north star's
+// "learned-predictor apply").
+//
+// pred[cell, k] = b[k] + sum_n f_n W[n, k] over the (2p+2)^3 = 64 features of the cell's node
+// neighbourhood (features_from_lowres, volume/utils.py:199-210), in the bf16x2 arithmetic of
+// kmp_bf16x2.h: 8 chunks of 8 features, one v_mfma_f32_16x16x32_bf16 each, accumulated from the
+// bias -- the same MFMAs on the same fragments as kmp_linear.hip's linear_bf16x2_kernel, so the
+// predictions are bit-identical to the callable / generic path of this predictor kind.  In the f32
+// form (kmp_codec_linear3dp.hip) these are 1216 FMAs per cell on the vector unit, which bound that
+// kernel at 510-560 us per C3 volume; as bf16 MFMAs they go to the matrix pipe (16 x 16 cells x
+// channels per MFMA, 16 cycles).
+//
+// A workgroup owns one output plane c of one tile; its waves own ROWS lowres rows each (the
+// lane layout, loads, staging and aggregation of kmp_codec_linear3dp.hip):
+//   1. every lane loads its 4 nodes of the 5 node planes c-2 .. c+2 and stages them in LDS as
+//      feature dwords (bf16 hi byte | bf16 lo byte) with the mirrored halo rows / columns of the
+//      symmetric neighbourhood pad over the even reflect pad (volume/utils.py:213-237); a barrier;
+//   2. per 16-cell tile (16 consecutive x of one row) two column tiles: cell plane c (node planes
+//      c-1 .. c+2, its 14 channels) and cell plane c-1 (node planes c-2 .. c+1, channels 5, 13, 14,
+//      17, 18), 8 MFMAs each.  Chunk q = 2 dz + h covers node rows dy = 2h, 2h+1 of plane dz: the
+//      A fragment of lane (g, m) is its cell's 4 consecutive nodes x-1 .. x+2 of node row 2h +
+//      (g & 1) -- so the plane-c tile's chunk (dz, h) and the plane-(c-1) tile's chunk (dz+1, h)
+//      read the same fragment, and row Y's h = 1 fragment is row Y+2's h = 0 one: the wave walks
+//      its rows by parity and reads 5 fragments per row instead of 16.  The weights' B fragments
+//      stay in registers for the whole plane.  Each MFMA leaves a lane one channel of 4 cells,
+//      cast to u16 and written to the wave's channel table [channel][row][x] in LDS; a barrier;
+//   3. each lane reads back its cells' channels (the row above from the same table, the wave
+//      above's last row included) and runs linear3dp's aggregation, coder and stores.
+#include <cstdlib>
+
+#include "kmp_bf16x2.h"
+#include "kmp_wave.h"
+
+namespace kmp {
+namespace l3q {
+
+using namespace wv;
+
+struct PM {
+  const bx::u32x4* frag;  // [3][8][64] B fragments (column tiles C, Q, zero), then [3][64] biases
+  const void* hi_in;
+  void* hi_out;
+  const void* lo_in;
+  void* lo_out;
+  MapPtrs maps;
+  const float* W;  // [64, 19] row-major
+  const float* b;  // [19]
+  int32_t D, H, W_;
+  int32_t Lz, Ly, Lx, Ez, Ey, Ex, Lcz, Lcy, Lcx;
+  int32_t zbegin, zend;
+  int32_t xcd_per;
+};
+
+constexpr int P = 1;         // padding
+constexpr int NPL = 2 * P + 3;  // staged node planes c-1-P .. c+1+P
+// column tiles: cell plane c (C) and c-1 (Q); -1 = unused column
+__constant__ int8_t kCch[16] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16, -1, -1};
+__constant__ int8_t kQch[16] = {5, 13, 14, 17, 18, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+
+// The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
+// biases, built once per call into the workspace instead of in every wave (64 bf16 splits a lane)
+__global__ void __launch_bounds__(64) fragments_kernel(const float* __restrict__ W, const float* __restrict__ bias,
+                                                       bx::u32x4* __restrict__ frag) {
+  const int lane = threadIdx.x, m = lane & 15, g = lane >> 4;
+  float* fb = (float*)(frag + 3 * 8 * 64);
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {  // C, Q, and a zero tile (the channels of a cell plane outside the tile)
+    const int ch = t == 0 ? kCch[m] : t == 1 ? kQch[m] : -1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) frag[(t * 8 + q) * 64 + lane] = bx::b_fragment(W + (ch >= 0 ? ch : 0), 19, 64, q, g, ch >= 0);
+    fb[t * 64 + lane] = ch >= 0 ? bias[ch] : 0.0f;
+  }
+}
+constexpr size_t kFragBytes = 3 * 8 * 64 * sizeof(bx::u32x4) + 3 * 64 * sizeof(float);
+
+template <bool DEC, int EX, int EY>
+__global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a) {
+  typedef uint16_t T;
+  constexpr int VX = 4;               // u16 cells per lane
+  constexpr int TXN = EX / VX;        // lanes per row
+  constexpr int ROWS = 64 / TXN;      // rows per wave
+  constexpr int NW = EY / ROWS;       // waves
+  constexpr int TPR = EX / 16;        // 16-cell tiles per row
+  constexpr int NR = EY + 2 * P + 1;  // staged node rows -P .. EY+P
+  constexpr int NHR = 4 * ((VX + 2 * P + 1 + 3) / 4) - VX - P;  // halo columns right of EX
+  constexpr int PITCH = EX + P + NHR;  // staged row: node columns -P .. EX-1+NHR (dwords)
+  // a wave's channel table (u16) [channel][row][x], the channel stride padded 8 banks past a
+  // multiple of 64 so that an MFMA's 16 channels x 4 cell groups write all 64 banks
+  constexpr int CS = ROWS * EX + 16;
+  constexpr int CT = 19 * CS;
+  constexpr uint32_t MASK = 0xffffu;
+  static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
+  using V = typename std::conditional<DEC, uint2, uint4>::type;
+
+  __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];
+  __shared__ __attribute__((aligned(16))) T ct[NW * CT];
+
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int tx = lane % TXN;
+  const int r = lane / TXN;
+  const int X = tx * VX;
+  const int m = lane & 15, g = lane >> 4;  // MFMA roles
+  int blk = (int)blockIdx.x;
+  if (a.xcd_per > 0) {
+    const int x = blk % 8, k = blk / 8;
+    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
+  }
+  const int nplanes = a.zend - a.zbegin;
+  const int c = a.zbegin + blk % nplanes;
+  const int64_t b = blk / nplanes;
+  const int Y0 = w * ROWS;
+  const int Y = Y0 + r;
+  const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+
+  const int hplane = a.H * a.W_;
+  const int lplane = EY * EX;
+  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
+  T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
+  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
+  const int hx = 2 * X;
+  const int ho_own = 2 * Y * a.W_ + hx;
+  const int lo_own = Y * EX + X;
+  T* mbase[7];
+  int mplane[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    int par[3];
+    map_parity(3, k, par);
+    const int ez = par[0] ? a.Lcz : a.Ez;
+    mplane[k] = lplane;  // FULL: Lcy == Ey
+    mbase[k] = (T*)a.maps.p[k] + b * (int64_t)ez * lplane + lo_own;
+  }
+
+  // ---- loads: the lane's node row of every staged plane, then the stream rows ----
+  V own[NPL];
+#pragma unroll
+  for (int t = 0; t < NPL; ++t) {
+    const int sz = lsrc1(c - 1 - P + t, a.Lz, a.Ez);
+    if constexpr (DEC) own[t] = ld8c(lin + sz * lplane + lo_own);
+    else own[t] = ld16c(hin + 2 * sz * hplane + ho_own);
+  }
+  uint4 e1 = make_uint4(0, 0, 0, 0), o0 = e1, o1 = e1;
+  uint2 mv[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
+  if constexpr (DEC) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int par[3];
+      map_parity(3, k, par);
+      if (!par[0] || vz1) mv[k] = ld8(mbase[k] + c * mplane[k]);
+    }
+  } else {
+    const T* p = hin + 2 * c * hplane;
+    e1 = ld16(p + ho_own + a.W_);
+    if (vz1) {
+      o0 = ld16(p + hplane + ho_own);
+      o1 = ld16(p + hplane + ho_own + a.W_);
+    }
+  }
+
+  // ---- the weights' B fragments and the bias (channel of column m); a cell plane outside the
+  // tile gets zero weights and bias: its channels are 0, what the aggregation's masks want ----
+  const int chC = kCch[m], chQ = kQch[m];
+  const int tC = vz1 ? 0 : 2, tQ = vz0 ? 1 : 2;  // uniform: the zero tile for a missing cell plane
+  bx::u32x4 bC[8], bQ[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bC[q] = a.frag[(tC * 8 + q) * 64 + lane];
+    bQ[q] = a.frag[(tQ * 8 + q) * 64 + lane];
+  }
+  const float* fb = (const float*)(a.frag + 3 * 8 * 64);
+  const float biasC = fb[tC * 64 + lane], biasQ = fb[tQ * 64 + lane];
+
+  // ---- 1. stage: every lane writes its 4 nodes of each plane as feature dwords, plus the
+  // mirrored halo columns / rows it is the source of (lsrc1), then one barrier ----
+  {
+    const bool xfirst = tx == 0, xlast = tx == TXN - 1;
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+      uint32_t v[VX];
+#pragma unroll
+      for (int i = 0; i < VX; ++i)
+        v[i] = bx::feature_dword(DEC ? el8<T>(*(const uint2*)&own[t], i) : el16<T>(*(const uint4*)&own[t], 2 * i));
+      auto put_row = [&](int ry) __attribute__((always_inline)) {
+        uint32_t* row = st + (t * NR + ry) * PITCH + P + X;
+#pragma unroll
+        for (int i = 0; i < VX; ++i) row[i] = v[i];
+        if (xfirst) {
+#pragma unroll
+          for (int k = 1; k <= P; ++k) row[-k] = v[k - 1];  // node column -k mirrors column k-1
+        }
+        if (xlast) {
+#pragma unroll
+          for (int j = 0; j < NHR; ++j) {
+            const int sx = lsrc1(EX + j, a.Lx, EX) - X;
+            uint32_t u = v[0];
+#pragma unroll
+            for (int i = 1; i < VX; ++i) u = sx == i ? v[i] : u;
+            row[VX + j] = u;
+          }
+        }
+      };
+      put_row(Y + P);
+#pragma unroll
+      for (int h = 0; h < 2 * P + 1; ++h) {  // node rows -P .. -1 and EY .. EY+P
+        const int rr = h < P ? h - P : EY + (h - P);
+        if (lsrc1(rr, a.Ly, EY) == Y) put_row(rr + P);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. the channels on the matrix cores ----
+  T* ctw = ct + w * CT;
+  {
+    // A fragment: staged plane t, node rows starting at staged row ry, cells x0 + m
+    auto frag = [&](int t, int ry, int x0) {
+      const uint32_t* p = st + (t * NR + ry + (g & 1)) * PITCH + x0 + m;
+      return (bx::u32x4){p[0], p[1], p[2], p[3]};
+    };
+    auto put = [&](int k, int row, int x0, const bx::f32x4& d) {
+      *(uint2*)(ctw + k * CS + row * EX + x0 + 4 * g) = bx::cast_pack4<T>(d);
+    };
+    // the wave's tile rows in order (x tile, row parity, row pair); the fragments a tile row reads
+    // beyond its predecessor's are loaded one tile row ahead, so an MFMA row (16 x 16 cycles)
+    // covers their LDS latency
+    constexpr int NTR = TPR * ROWS;  // tile rows
+    auto tr_row = [](int i) { return ((i / (ROWS / 2)) & 1) + 2 * (i % (ROWS / 2)); };  // row in the wave
+    auto tr_x0 = [](int i) { return 16 * (i / ROWS); };
+    auto tr_first = [](int i) { return i % (ROWS / 2) == 0; };  // a chain's first row: no pair-0 carry
+    bx::u32x4 F0[NPL], F1[NPL], N0[NPL], N1[NPL];
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+      F0[t] = frag(t, Y0 + tr_row(0), 0);
+      F1[t] = frag(t, Y0 + tr_row(0) + 2, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NTR; ++i) {
+      const int row = tr_row(i), x0 = tr_x0(i);
+      if (i + 1 < NTR) {
+        const int nrow = tr_row(i + 1), nx0 = tr_x0(i + 1);
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) {
+          if (tr_first(i + 1)) N0[t] = frag(t, Y0 + nrow, nx0);
+          N1[t] = frag(t, Y0 + nrow + 2, nx0);
+        }
+      }
+      bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // chunk q: plane offset dz = q / 2, node rows 2 (q & 1) + 0 / 1
+        const int dz = q >> 1;
+        dC = bx::mfma((q & 1) ? F1[1 + dz] : F0[1 + dz], bC[q], dC);
+        dQ = bx::mfma((q & 1) ? F1[dz] : F0[dz], bQ[q], dQ);
+      }
+      if (chC >= 0) put(chC, row, x0, dC);
+      if (chQ >= 0) put(chQ, row, x0, dQ);
+      if (i + 1 < NTR) {
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) {
+          F0[t] = tr_first(i + 1) ? N0[t] : F1[t];
+          F1[t] = N1[t];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. channel k of the lane's cells X .. X+3 at index 1 .. 4; the row above from the table
+  // (the wave above's last row for r = 0; none above row 0: zeros) ----
+  auto rd_at = [&](const T* tab, int k, int row, uint32_t (&v)[VX + 1]) {
+    const uint2 u = *(const uint2*)(tab + k * CS + row * EX + X);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
+  };
+  auto rd = [&](int k, uint32_t (&v)[VX + 1]) { rd_at(ctw, k, r, v); };
+  auto rd_up = [&](int k, uint32_t (&v)[VX + 1]) {
+    if (r > 0) rd_at(ctw, k, r - 1, v);
+    else if (w > 0) rd_at(ctw - CT, k, ROWS - 1, v);
+    else {
+#pragma unroll
+      for (int i = 1; i <= VX; ++i) v[i] = 0u;
+    }
+  };
+  uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
+  rd_up(3, A3);
+  rd_up(9, A9);
+  rd_up(10, A10);
+  rd_up(16, A16);
+  rd_up(17, QA17);
+  A9[0] = shup(A9[VX], 1);
+
+  const bool vy0 = Y >= 1;
+  bool vx[VX + 1];
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = q >= 1 || X >= 1;
+  const uint32_t ny = (uint32_t)vy0 + 1u;
+  const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+  auto mk = [&](const uint32_t (&v)[VX + 1], int q) { return vx[q] ? v[q] : 0u; };
+  auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };
+  auto put8 = [&](int k, const uint32_t (&res)[VX]) {
+    int par[3];
+    map_parity(3, k, par);
+    if (!par[0] || vz1) st8(mbase[k] + c * mplane[k], pack8<T, VX>(res));
+  };
+  constexpr int tc = 1 + P;  // staged plane index of node plane c
+  const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own[tc];
+  T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
+  uint32_t ownv[VX];
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own[tc], i);
+    else ownv[i] = el16<T>(e0, 2 * i);
+  }
+  auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      if constexpr (DEC) outv[i] = (pred[i] + el8<T>(mv[k], i)) & MASK;
+      else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+    }
+  };
+
+  // X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); with the lowres
+  {
+    uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
+    rd(15, P15);
+    rd(18, Q18);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) pred[i] = (P15[i + 1] + A16[i + 1] + QA17[i + 1] + Q18[i + 1]) >> ((nz * ny) >> 1);
+    code(6, pred, e0, 1, outv);
+    if constexpr (DEC) {
+      st16(h0, pack16<T, VX>(ownv, outv));
+    } else {
+      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(ownv));
+      put8(6, outv);
+    }
+  }
+  // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
+  {
+    uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
+    uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
+    rd(7, P7);
+    rd(8, P8);
+    rd(2, P2);
+    left(P8);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pZ[i] = (P7[i + 1] + mk(P8, i) + mk(A9, i) + A10[i + 1]) >> ((ny * nx) >> 1);
+      pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
+    }
+    code(4, pZ, o0, 0, oZ);
+    code(1, pU, o0, 1, oU);
+    if constexpr (DEC) {
+      if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
+    } else {
+      put8(4, oZ);
+      put8(1, oU);
+    }
+  }
+  // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
+  {
+    uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
+    uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
+    rd(11, P11);
+    rd(12, P12);
+    rd(13, Q13);
+    rd(14, Q14);
+    rd(4, P4);
+    rd(5, Q5);
+    left(P12);
+    left(Q13);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pY[i] = (P11[i + 1] + mk(P12, i) + mk(Q13, i) + Q14[i + 1]) >> ((nz * nx) >> 1);
+      pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
+    }
+    code(5, pY, e1, 0, oY);
+    code(2, pF, e1, 1, oF);
+    if constexpr (DEC) {
+      st16(h0 + a.W_, pack16<T, VX>(oY, oF));
+    } else {
+      put8(5, oY);
+      put8(2, oF);
+    }
+  }
+  // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
+  {
+    uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
+    uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
+    rd(0, P0);
+    rd(1, P1);
+    rd(6, P6);
+    left(P1);
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+      pL[i] = (P0[i + 1] + mk(P1, i)) >> (nx >> 1);
+      pC[i] = P6[i + 1];
+    }
+    code(0, pL, o1, 0, oL);
+    code(3, pC, o1, 1, oC);
+    if constexpr (DEC) {
+      if (vz1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
+    } else {
+      put8(0, oL);
+      put8(3, oC);
+    }
+  }
+}
+
+}  // namespace l3q
+
+static int l3q_env(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+// u16 FULL tiles (Lcy == Ey, Lcx == Ex) with Ex, Ey in {16, 32}; anything else is served by the
+// generic path with kmp_linear.hip's kernel of the same predictor kind (bit-identical arithmetic)
+template <typename T>
+static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
+                               const kmp_region* region, l3q::PM& a, dim3& grid, dim3& block) {
+  constexpr int P = l3q::P;
+  if (!std::is_same<T, uint16_t>::value) return false;
+  if (l3q_env("KMP_DISABLE_FAST", 0) || l3q_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (C != 1 || pred->kind != KMP_PRED_LINEAR_MFMA || pred->padding != P || !pred->weights || !pred->bias) return false;
+  if (g.E[2] != 16 && g.E[2] != 32) return false;
+  if (g.E[1] != 16 && g.E[1] != 32) return false;
+  if (g.Lc[1] != g.E[1] || g.Lc[2] != g.E[2] || g.Lc[0] < 1) return false;
+  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
+  // one reflection covers every halo index (lsrc1): L >= P + 2 on each axis
+  if (g.L[0] < P + 2 || g.L[1] < P + 2 || g.L[2] < P + 2) return false;
+  int64_t zb = 0, ze = g.E[0];
+  if (region) {
+    if (region->begin[1] > 0 || region->begin[2] > 0 || region->end[1] < g.E[1] || region->end[2] < g.E[2]) return false;
+    zb = region->begin[0] < 0 ? 0 : region->begin[0];
+    ze = region->end[0] > g.E[0] ? g.E[0] : region->end[0];
+    if (ze <= zb) return false;
+  }
+  a.D = (int)g.n[0]; a.H = (int)g.n[1]; a.W_ = (int)g.n[2];
+  a.Lz = (int)g.L[0]; a.Ly = (int)g.L[1]; a.Lx = (int)g.L[2];
+  a.Ez = (int)g.E[0]; a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
+  a.Lcz = (int)g.Lc[0]; a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
+  a.zbegin = (int)zb; a.zend = (int)ze;
+  const int64_t nblk = B * (ze - zb);
+  a.xcd_per = (l3q_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  const int rows = 64 / (a.Ex / 4);
+  grid = dim3((unsigned)nblk);
+  block = dim3((unsigned)(64 * (a.Ey / rows)));
+  return nblk < ((int64_t)1 << 31);
+}
+
+template <bool DEC>
+static void launch_linear3pm(const l3q::PM& a, dim3 grid, dim3 block, hipStream_t stream) {
+#define KMP_L3Q(EX, EY) l3q::linear3pm_kernel<DEC, EX, EY><<<grid, block, 0, stream>>>(a)
+  if (a.Ex == 32) {
+    if (a.Ey == 32) KMP_L3Q(32, 32);
+    else KMP_L3Q(32, 16);
+  } else {
+    if (a.Ey == 32) KMP_L3Q(16, 32);
+    else KMP_L3Q(16, 16);
+  }
+#undef KMP_L3Q
+}
+
+template <typename T>
+int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
+                         const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value) {
+    l3q::PM a{};
+    dim3 grid, block;
+    if (!linear3pm_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k)
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+    a.hi_in = hi;
+    a.lo_out = lowres;
+    a.maps = maps;
+    a.W = pred->weights;
+    a.b = pred->bias;
+    if (!ws || ws_bytes < l3q::kFragBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
+    a.frag = (const bx::u32x4*)ws;
+    l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
+    launch_linear3pm<false>(a, grid, block, stream);
+    return check_launch("linear3pm_encode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
+                         const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
+                         hipStream_t stream) {
+  if constexpr (std::is_same<T, uint16_t>::value) {
+    l3q::PM a{};
+    dim3 grid, block;
+    if (!linear3pm_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
+    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    for (int k = 0; k < 7; ++k) {
+      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      a.maps.p[k] = (void*)maps.p[k];
+    }
+    a.hi_out = hi;
+    a.lo_in = lowres;
+    a.W = pred->weights;
+    a.b = pred->bias;
+    if (!ws || ws_bytes < l3q::kFragBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
+    a.frag = (const bx::u32x4*)ws;
+    l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
+    launch_linear3pm<true>(a, grid, block, stream);
+    return check_launch("linear3pm_decode");
+  }
+  return KMP_ERR_UNSUPPORTED;
+}
+
+#define KMP_L3Q_INST(T)                                                                                   \
+  template int try_linear3pm_encode<T>(const T*, const Geo&, int64_t, int64_t, const kmp_predictor*, T*,  \
+                                       const MapPtrs&, const kmp_region*, void*, size_t, hipStream_t);    \
+  template int try_linear3pm_decode<T>(const T*, const CMapPtrs&, const Geo&, int64_t, int64_t,           \
+                                       const kmp_predictor*, T*, const kmp_region*, void*, size_t, hipStream_t);
+KMP_L3Q_INST(uint8_t)
+KMP_L3Q_INST(uint16_t)
+KMP_L3Q_INST(int32_t)
+KMP_L3Q_INST(uint32_t)
+
+}  // namespace kmp

@@ -153,7 +153,11 @@ def test_linear_fused_p0(kom, shape, dtype, kernel):
 BF_CASES = [(3, 0, (4, 64, 64, 64, 1), np.uint16), (3, 0, (2, 16, 32, 32, 1), np.uint16),
             (3, 0, (1, 7, 32, 64, 1), np.uint16), (3, 0, (2, 9, 10, 12, 1), np.uint16),
             (3, 0, (2, 8, 32, 64, 1), np.uint8), (3, 0, (1, 9, 64, 32, 1), np.uint8),
-            (3, 1, (2, 8, 9, 7, 1), np.uint16), (2, 0, (3, 33, 20, 1), np.uint8), (2, 1, (2, 30, 31, 2), np.uint16)]
+            (3, 1, (2, 8, 9, 7, 1), np.uint16), (2, 0, (3, 33, 20, 1), np.uint8), (2, 1, (2, 30, 31, 2), np.uint16),
+            # p = 1 on the fused matrix-core kernel (linear3pm): 32 / 16-wide rows and planes
+            (3, 1, (2, 12, 64, 64, 1), np.uint16), (3, 1, (1, 10, 32, 32, 1), np.uint16),
+            (3, 1, (1, 8, 32, 64, 1), np.uint16), (3, 1, (1, 7, 64, 32, 1), np.uint16),
+            (3, 1, (1, 8, 32, 64, 1), np.uint8)]
 
 
 @pytest.mark.parametrize('ndim,p,shape,dtype', BF_CASES)
@@ -193,7 +197,11 @@ def test_linear_bf16x2_codec_paths_agree(kom, ndim, p, shape, dtype):
     rows = 64 // max(1, ex // vx)
     fused = (ndim == 3 and p == 0 and shape[2] % 2 == 0 and shape[3] % 2 == 0 and ex in (16, 32)
              and ey % rows == 0 and ey // rows in (1, 2, 4))
-    assert kom._lib.lib.kmp_last_launch().decode() == ('linear3m_encode' if fused else 'encode_generic')
+    # p = 1: u16 FULL volumes with 16 / 32-wide rows and 16 / 32 rows a plane
+    fused1 = (ndim == 3 and p == 1 and dtype == np.uint16 and shape[2] % 2 == 0 and shape[3] % 2 == 0
+              and ex in (16, 32) and ey in (16, 32))
+    want_kernel = 'linear3m_encode' if fused else 'linear3pm_encode' if fused1 else 'encode_generic'
+    assert kom._lib.lib.kmp_last_launch().decode() == want_kernel
     # (3) residuals == the oracle's coder on the kernel's own predictions (the callable's maps)
     padded = ons.pad_highres(hi)[0]
     pmaps = pred(ons.pad_neighborhood(ons.lowres_from_highres(padded), p))
