@@ -11,8 +11,11 @@
 //   * features are taken in chunks of 8 in the reference's order (features_from_lowres,
 //     volume/utils.py:199-210); per chunk ONE v_mfma_f32_16x16x32_bf16 with
 //         K = 32 = [hi_0, lo_0, ..., hi_7, lo_7 | the same 16] x [u1 of the chunk | u2 of the chunk],
-//     accumulated from the bias: acc = b[k]; acc = mfma(A_0, B_0, acc); acc = mfma(A_1, B_1, acc) ...
-//     (features past N and padded columns are zeros);
+//     accumulated from the bias, the even chunks first, then the odd ones (chunk_at):
+//     acc = b[k]; acc = mfma(A_0, B_0, acc); acc = mfma(A_2, B_2, acc) ... acc = mfma(A_1, B_1, acc) ...
+//     (features past N and padded columns are zeros).  For the volume p = 1 neighbourhood the even
+//     chunks are node rows dy = 0, 1 of each plane and the odd ones dy = 2, 3, so a kernel walking
+//     cell rows can load the next row's fragments into the registers of this row's first half;
 //   * then the sample dtype's truncating, saturating cast (XLA astype).
 // Error: <= 2^-18 sum|f w| from the split plus the f32 accumulation inside the MFMA, well within
 // 1e-5 of sum|f w| + |b| (tests/test_gpu_linear.py).  An MFMA output element depends only on its
@@ -32,6 +35,11 @@ namespace bx {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// the i-th chunk (of nq) in accumulation order: 0, 2, 4, ..., then 1, 3, 5, ...
+__host__ __device__ constexpr int chunk_at(int i, int nq) {
+  return i < (nq + 1) / 2 ? 2 * i : 2 * (i - (nq + 1) / 2) + 1;
+}
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN)
 __host__ __device__ __forceinline__ uint32_t bf16_rne(float f) {

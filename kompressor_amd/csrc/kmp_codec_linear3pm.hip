@@ -5,7 +5,7 @@
 // pred[cell, k] = b[k] + sum_n f_n W[n, k] over the (2p+2)^3 = 64 features of the cell's node
 // neighbourhood (features_from_lowres, volume/utils.py:199-210), in the bf16x2 arithmetic of
 // kmp_bf16x2.h: 8 chunks of 8 features, one v_mfma_f32_16x16x32_bf16 each, accumulated from the
-// bias -- the same MFMAs on the same fragments as kmp_linear.hip's linear_bf16x2_kernel, so the
+// bias in chunk_at order -- the same MFMAs on the same fragments as kmp_linear.hip's linear_bf16x2_kernel, so the
 // predictions are bit-identical to the callable / generic path of this predictor kind.  In the f32
 // form (kmp_codec_linear3dp.hip) these are 1216 FMAs per cell on the vector unit, which bound that
 // kernel at 510-560 us per C3 volume; as bf16 MFMAs they go to the matrix pipe (16 x 16 cells x
@@ -49,6 +49,7 @@ struct PM {
   int32_t D, H, W_;
   int32_t Lz, Ly, Lx, Ez, Ey, Ex, Lcz, Lcy, Lcx;
   int32_t zbegin, zend;
+  int32_t nsplit, zper;  // runs of output planes per tile, planes per run
   int32_t xcd_per;
 };
 
@@ -84,16 +85,20 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   constexpr int TPR = EX / 16;        // 16-cell tiles per row
   constexpr int NR = EY + 2 * P + 1;  // staged node rows -P .. EY+P
   constexpr int NHR = 4 * ((VX + 2 * P + 1 + 3) / 4) - VX - P;  // halo columns right of EX
-  constexpr int PITCH = EX + P + NHR;  // staged row: node columns -P .. EX-1+NHR (dwords)
-  // a wave's channel table (u16) [channel][row][x], the channel stride padded 8 banks past a
-  // multiple of 64 so that an MFMA's 16 channels x 4 cell groups write all 64 banks
-  constexpr int CS = ROWS * EX + 16;
+  // staged row: node columns -P .. EX-1+NHR (dwords), the pitch padded to 16 banks past a multiple
+  // of 32 (ds_read2_b32 banks are (a/4) mod 32 per half wave): an A-fragment read's lane groups
+  // g = 0 / 1 (adjacent node rows) then take disjoint banks
+  constexpr int PITCH0 = EX + P + NHR;
+  constexpr int PITCH = PITCH0 + ((16 - PITCH0 % 32) + 32) % 32;
+  // a wave's channel table (u16) [channel][row][x], the channel stride padded 2 banks past a
+  // multiple of 32 so that an MFMA's 16 channels (one ds_write_b64 lane group) write 32 banks
+  constexpr int CS = ROWS * EX + 4;
   constexpr int CT = 19 * CS;
   constexpr uint32_t MASK = 0xffffu;
   static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
   using V = typename std::conditional<DEC, uint2, uint4>::type;
 
-  __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];
+  __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];  // ring of 5 node planes
   __shared__ __attribute__((aligned(16))) T ct[NW * CT];
 
   const int lane = threadIdx.x & 63;
@@ -107,309 +112,335 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     const int x = blk % 8, k = blk / 8;
     blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
   }
-  const int nplanes = a.zend - a.zbegin;
-  const int c = a.zbegin + blk % nplanes;
-  const int64_t b = blk / nplanes;
+  // the workgroup's tile and its run of output planes [cb, ce)
+  const int64_t b = blk / a.nsplit;
+  const int cb = a.zbegin + (blk % a.nsplit) * a.zper;
+  const int ce = min(cb + a.zper, a.zend);
   const int Y0 = w * ROWS;
   const int Y = Y0 + r;
-  const bool vz1 = c < a.Lcz, vz0 = c >= 1;
 
   const int hplane = a.H * a.W_;
   const int lplane = EY * EX;
   const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * (int64_t)a.D * hplane;
   T* hout = DEC ? (T*)a.hi_out + b * (int64_t)a.D * hplane : nullptr;
   const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ez * lplane : nullptr;
+  T* lout = DEC ? nullptr : (T*)a.lo_out + b * (int64_t)a.Ez * lplane;
   const int hx = 2 * X;
   const int ho_own = 2 * Y * a.W_ + hx;
   const int lo_own = Y * EX + X;
   T* mbase[7];
-  int mplane[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     int par[3];
     map_parity(3, k, par);
     const int ez = par[0] ? a.Lcz : a.Ez;
-    mplane[k] = lplane;  // FULL: Lcy == Ey
-    mbase[k] = (T*)a.maps.p[k] + b * (int64_t)ez * lplane + lo_own;
+    mbase[k] = (T*)a.maps.p[k] + b * (int64_t)ez * lplane + lo_own;  // FULL: Lcy == Ey
   }
 
-  // ---- loads: the lane's node row of every staged plane, then the stream rows ----
-  V own[NPL];
+  // the lane's node row of node plane q (any q within one reflection of the axis)
+  auto node_row = [&](int q) -> V {
+    const int sz = lsrc1(q, a.Lz, a.Ez);
+    if constexpr (DEC) return ld8c(lin + sz * lplane + lo_own);
+    else return ld16c(hin + 2 * sz * hplane + ho_own);
+  };
+  // the rows an output plane's coder reads besides its nodes: the maps (decode) / the highres
+  // rows of the odd positions (encode)
+  struct Streams {
+    uint2 mv[7];
+    uint4 e1, o0, o1;
+  };
+  auto load_streams = [&](int c, Streams& sv) {
+    const bool vz1 = c < a.Lcz;
+    if constexpr (DEC) {
 #pragma unroll
-  for (int t = 0; t < NPL; ++t) {
-    const int sz = lsrc1(c - 1 - P + t, a.Lz, a.Ez);
-    if constexpr (DEC) own[t] = ld8c(lin + sz * lplane + lo_own);
-    else own[t] = ld16c(hin + 2 * sz * hplane + ho_own);
-  }
-  uint4 e1 = make_uint4(0, 0, 0, 0), o0 = e1, o1 = e1;
-  uint2 mv[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
-  if constexpr (DEC) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int par[3];
-      map_parity(3, k, par);
-      if (!par[0] || vz1) mv[k] = ld8(mbase[k] + c * mplane[k]);
-    }
-  } else {
-    const T* p = hin + 2 * c * hplane;
-    e1 = ld16(p + ho_own + a.W_);
-    if (vz1) {
-      o0 = ld16(p + hplane + ho_own);
-      o1 = ld16(p + hplane + ho_own + a.W_);
-    }
-  }
-
-  // ---- the weights' B fragments and the bias (channel of column m); a cell plane outside the
-  // tile gets zero weights and bias: its channels are 0, what the aggregation's masks want ----
-  const int chC = kCch[m], chQ = kQch[m];
-  const int tC = vz1 ? 0 : 2, tQ = vz0 ? 1 : 2;  // uniform: the zero tile for a missing cell plane
-  bx::u32x4 bC[8], bQ[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    bC[q] = a.frag[(tC * 8 + q) * 64 + lane];
-    bQ[q] = a.frag[(tQ * 8 + q) * 64 + lane];
-  }
-  const float* fb = (const float*)(a.frag + 3 * 8 * 64);
-  const float biasC = fb[tC * 64 + lane], biasQ = fb[tQ * 64 + lane];
-
-  // ---- 1. stage: every lane writes its 4 nodes of each plane as feature dwords, plus the
-  // mirrored halo columns / rows it is the source of (lsrc1), then one barrier ----
-  {
-    const bool xfirst = tx == 0, xlast = tx == TXN - 1;
-#pragma unroll
-    for (int t = 0; t < NPL; ++t) {
-      uint32_t v[VX];
-#pragma unroll
-      for (int i = 0; i < VX; ++i)
-        v[i] = bx::feature_dword(DEC ? el8<T>(*(const uint2*)&own[t], i) : el16<T>(*(const uint4*)&own[t], 2 * i));
-      auto put_row = [&](int ry) __attribute__((always_inline)) {
-        uint32_t* row = st + (t * NR + ry) * PITCH + P + X;
-#pragma unroll
-        for (int i = 0; i < VX; ++i) row[i] = v[i];
-        if (xfirst) {
-#pragma unroll
-          for (int k = 1; k <= P; ++k) row[-k] = v[k - 1];  // node column -k mirrors column k-1
-        }
-        if (xlast) {
-#pragma unroll
-          for (int j = 0; j < NHR; ++j) {
-            const int sx = lsrc1(EX + j, a.Lx, EX) - X;
-            uint32_t u = v[0];
-#pragma unroll
-            for (int i = 1; i < VX; ++i) u = sx == i ? v[i] : u;
-            row[VX + j] = u;
-          }
-        }
-      };
-      put_row(Y + P);
-#pragma unroll
-      for (int h = 0; h < 2 * P + 1; ++h) {  // node rows -P .. -1 and EY .. EY+P
-        const int rr = h < P ? h - P : EY + (h - P);
-        if (lsrc1(rr, a.Ly, EY) == Y) put_row(rr + P);
+      for (int k = 0; k < 7; ++k) {
+        int par[3];
+        map_parity(3, k, par);
+        sv.mv[k] = (!par[0] || vz1) ? ld8(mbase[k] + c * lplane) : make_uint2(0, 0);
       }
+    } else {
+      const T* p = hin + 2 * c * hplane;
+      sv.e1 = ld16(p + ho_own + a.W_);
+      sv.o0 = vz1 ? ld16(p + hplane + ho_own) : make_uint4(0, 0, 0, 0);
+      sv.o1 = vz1 ? ld16(p + hplane + ho_own + a.W_) : make_uint4(0, 0, 0, 0);
     }
-  }
-  __syncthreads();
+  };
 
-  // ---- 2. the channels on the matrix cores ----
+  const int chC = kCch[m], chQ = kQch[m];
+
+  // ---- staging: the node row of node plane q as feature dwords into ring slot q mod 5, plus
+  // the mirrored halo columns / rows this lane is the source of (lsrc1) ----
+  auto stage = [&](const V& own, int q) {
+    const int slot = (q + 2 * NPL) % NPL;  // q >= -2
+    const bool xfirst = tx == 0, xlast = tx == TXN - 1;
+    uint32_t v[VX];
+#pragma unroll
+    for (int i = 0; i < VX; ++i)
+      v[i] = bx::feature_dword(DEC ? el8<T>(*(const uint2*)&own, i) : el16<T>(*(const uint4*)&own, 2 * i));
+    auto put_row = [&](int ry) __attribute__((always_inline)) {
+      uint32_t* row = st + (slot * NR + ry) * PITCH + P + X;
+#pragma unroll
+      for (int i = 0; i < VX; ++i) row[i] = v[i];
+      if (xfirst) {
+#pragma unroll
+        for (int k = 1; k <= P; ++k) row[-k] = v[k - 1];  // node column -k mirrors column k-1
+      }
+      if (xlast) {
+#pragma unroll
+        for (int j = 0; j < NHR; ++j) {
+          const int sx = lsrc1(EX + j, a.Lx, EX) - X;
+          uint32_t u = v[0];
+#pragma unroll
+          for (int i = 1; i < VX; ++i) u = sx == i ? v[i] : u;
+          row[VX + j] = u;
+        }
+      }
+    };
+    put_row(Y + P);
+#pragma unroll
+    for (int h = 0; h < 2 * P + 1; ++h) {  // node rows -P .. -1 and EY .. EY+P
+      const int rr = h < P ? h - P : EY + (h - P);
+      if (lsrc1(rr, a.Ly, EY) == Y) put_row(rr + P);
+    }
+  };
+
+  // ---- the channels of output plane c on the matrix cores, into the wave's channel table.  A
+  // cell plane outside the tile (c - 1 < 0: Q, c >= Lcz: C) has channels 0, what the
+  // aggregation's masks want ----
   T* ctw = ct + w * CT;
-  {
-    // A fragment: staged plane t, node rows starting at staged row ry, cells x0 + m
+  auto channels = [&](int c, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC, float biasQ) {
+    const bool doC = c < a.Lcz, doQ = c >= 1;
+    // A fragment: node plane q = c - 2 + t (ring slot), node rows from staged row ry, cells x0 + m
+    int sl[NPL];
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) sl[t] = (c - 2 + t + 2 * NPL) % NPL;
     auto frag = [&](int t, int ry, int x0) {
-      const uint32_t* p = st + (t * NR + ry + (g & 1)) * PITCH + x0 + m;
+#ifdef L3Q_NOFRAG
+      const uint32_t u = (uint32_t)(t * 977 + ry * 131 + x0 + lane);
+      return (bx::u32x4){bx::feature_dword(u & 0xffff), bx::feature_dword((u + 1) & 0xffff),
+                         bx::feature_dword((u + 2) & 0xffff), bx::feature_dword((u + 3) & 0xffff)};
+#else
+      const uint32_t* p = st + (sl[t] * NR + ry + (g & 1)) * PITCH + x0 + m;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
+#endif
     };
     auto put = [&](int k, int row, int x0, const bx::f32x4& d) {
       *(uint2*)(ctw + k * CS + row * EX + x0 + 4 * g) = bx::cast_pack4<T>(d);
     };
-    // the wave's tile rows in order (x tile, row parity, row pair); the fragments a tile row reads
-    // beyond its predecessor's are loaded one tile row ahead, so an MFMA row (16 x 16 cycles)
-    // covers their LDS latency
-    constexpr int NTR = TPR * ROWS;  // tile rows
-    auto tr_row = [](int i) { return ((i / (ROWS / 2)) & 1) + 2 * (i % (ROWS / 2)); };  // row in the wave
-    auto tr_x0 = [](int i) { return 16 * (i / ROWS); };
-    auto tr_first = [](int i) { return i % (ROWS / 2) == 0; };  // a chain's first row: no pair-0 carry
-    bx::u32x4 F0[NPL], F1[NPL], N0[NPL], N1[NPL];
+    const bx::f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+    // tile rows by x tile, row parity, row pair: row Y's node rows 2, 3 (F1) are row Y+2's 0, 1
 #pragma unroll
-    for (int t = 0; t < NPL; ++t) {
-      F0[t] = frag(t, Y0 + tr_row(0), 0);
-      F1[t] = frag(t, Y0 + tr_row(0) + 2, 0);
-    }
+    for (int xt = 0; xt < TPR; ++xt) {
 #pragma unroll
-    for (int i = 0; i < NTR; ++i) {
-      const int row = tr_row(i), x0 = tr_x0(i);
-      if (i + 1 < NTR) {
-        const int nrow = tr_row(i + 1), nx0 = tr_x0(i + 1);
+      for (int par = 0; par < 2; ++par) {
+        bx::u32x4 F0[NPL], F1[NPL];
 #pragma unroll
-        for (int t = 0; t < NPL; ++t) {
-          if (tr_first(i + 1)) N0[t] = frag(t, Y0 + nrow, nx0);
-          N1[t] = frag(t, Y0 + nrow + 2, nx0);
-        }
-      }
-      bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
+        for (int t = 0; t < NPL; ++t) F0[t] = frag(t, Y0 + par, 16 * xt);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {  // chunk q: plane offset dz = q / 2, node rows 2 (q & 1) + 0 / 1
-        const int dz = q >> 1;
-        dC = bx::mfma((q & 1) ? F1[1 + dz] : F0[1 + dz], bC[q], dC);
-        dQ = bx::mfma((q & 1) ? F1[dz] : F0[dz], bQ[q], dQ);
-      }
-      if (chC >= 0) put(chC, row, x0, dC);
-      if (chQ >= 0) put(chQ, row, x0, dQ);
-      if (i + 1 < NTR) {
+        for (int j = 0; j < ROWS / 2; ++j) {
+          const int row = par + 2 * j;
 #pragma unroll
-        for (int t = 0; t < NPL; ++t) {
-          F0[t] = tr_first(i + 1) ? N0[t] : F1[t];
-          F1[t] = N1[t];
+          for (int t = 0; t < NPL; ++t) F1[t] = frag(t, Y0 + row + 2, 16 * xt);
+          bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {  // chunk q (plane offset dz = q / 2, node rows 2 (q & 1) + 0 / 1)
+            const int q = bx::chunk_at(i, 8), dz = q >> 1;
+            dC = bx::mfma((q & 1) ? F1[1 + dz] : F0[1 + dz], bC[q], dC);
+            dQ = bx::mfma((q & 1) ? F1[dz] : F0[dz], bQ[q], dQ);
+          }
+          if (chC >= 0) put(chC, row, 16 * xt, doC ? dC : z4);
+          if (chQ >= 0) put(chQ, row, 16 * xt, doQ ? dQ : z4);
+#pragma unroll
+          for (int t = 0; t < NPL; ++t) F0[t] = F1[t];
         }
       }
     }
-  }
-  __syncthreads();
-
-  // ---- 3. channel k of the lane's cells X .. X+3 at index 1 .. 4; the row above from the table
-  // (the wave above's last row for r = 0; none above row 0: zeros) ----
-  auto rd_at = [&](const T* tab, int k, int row, uint32_t (&v)[VX + 1]) {
-    const uint2 u = *(const uint2*)(tab + k * CS + row * EX + X);
-#pragma unroll
-    for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
-  };
-  auto rd = [&](int k, uint32_t (&v)[VX + 1]) { rd_at(ctw, k, r, v); };
-  auto rd_up = [&](int k, uint32_t (&v)[VX + 1]) {
-    if (r > 0) rd_at(ctw, k, r - 1, v);
-    else if (w > 0) rd_at(ctw - CT, k, ROWS - 1, v);
-    else {
-#pragma unroll
-      for (int i = 1; i <= VX; ++i) v[i] = 0u;
-    }
-  };
-  uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
-  rd_up(3, A3);
-  rd_up(9, A9);
-  rd_up(10, A10);
-  rd_up(16, A16);
-  rd_up(17, QA17);
-  A9[0] = shup(A9[VX], 1);
-
-  const bool vy0 = Y >= 1;
-  bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = q >= 1 || X >= 1;
-  const uint32_t ny = (uint32_t)vy0 + 1u;
-  const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
-  auto mk = [&](const uint32_t (&v)[VX + 1], int q) { return vx[q] ? v[q] : 0u; };
-  auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };
-  auto put8 = [&](int k, const uint32_t (&res)[VX]) {
-    int par[3];
-    map_parity(3, k, par);
-    if (!par[0] || vz1) st8(mbase[k] + c * mplane[k], pack8<T, VX>(res));
-  };
-  constexpr int tc = 1 + P;  // staged plane index of node plane c
-  const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own[tc];
-  T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
-  uint32_t ownv[VX];
-#pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own[tc], i);
-    else ownv[i] = el16<T>(e0, 2 * i);
-  }
-  auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) outv[i] = (pred[i] + el8<T>(mv[k], i)) & MASK;
-      else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
-    }
   };
 
-  // X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); with the lowres
-  {
-    uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
-    rd(15, P15);
-    rd(18, Q18);
+  // ---- the maps / coder of output plane c from the channel table (linear3dp's aggregation):
+  // channel k of the lane's cells X .. X+3 at index 1 .. 4; the row above from the table (the
+  // wave above's last row for r = 0; none above row 0: zeros) ----
+  auto aggregate = [&](int c, const V& own, const Streams& sv) {
+    const bool vz1 = c < a.Lcz, vz0 = c >= 1;
+    auto rd_at = [&](const T* tab, int k, int row, uint32_t (&v)[VX + 1]) {
+      const uint2 u = *(const uint2*)(tab + k * CS + row * EX + X);
 #pragma unroll
-    for (int i = 0; i < VX; ++i) pred[i] = (P15[i + 1] + A16[i + 1] + QA17[i + 1] + Q18[i + 1]) >> ((nz * ny) >> 1);
-    code(6, pred, e0, 1, outv);
-    if constexpr (DEC) {
-      st16(h0, pack16<T, VX>(ownv, outv));
-    } else {
-      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(ownv));
-      put8(6, outv);
-    }
-  }
-  // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
-  {
-    uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
-    uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
-    rd(7, P7);
-    rd(8, P8);
-    rd(2, P2);
-    left(P8);
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
+    };
+    auto rd = [&](int k, uint32_t (&v)[VX + 1]) { rd_at(ctw, k, r, v); };
+    auto rd_up = [&](int k, uint32_t (&v)[VX + 1]) {
+      if (r > 0) rd_at(ctw, k, r - 1, v);
+      else if (w > 0) rd_at(ctw - CT, k, ROWS - 1, v);
+      else {
 #pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pZ[i] = (P7[i + 1] + mk(P8, i) + mk(A9, i) + A10[i + 1]) >> ((ny * nx) >> 1);
-      pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
-    }
-    code(4, pZ, o0, 0, oZ);
-    code(1, pU, o0, 1, oU);
-    if constexpr (DEC) {
-      if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
-    } else {
-      put8(4, oZ);
-      put8(1, oU);
-    }
-  }
-  // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
-  {
-    uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
-    uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
-    rd(11, P11);
-    rd(12, P12);
-    rd(13, Q13);
-    rd(14, Q14);
-    rd(4, P4);
-    rd(5, Q5);
-    left(P12);
-    left(Q13);
+        for (int i = 1; i <= VX; ++i) v[i] = 0u;
+      }
+    };
+    uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
+    rd_up(3, A3);
+    rd_up(9, A9);
+    rd_up(10, A10);
+    rd_up(16, A16);
+    rd_up(17, QA17);
+    A9[0] = shup(A9[VX], 1);
+
+    const bool vy0 = Y >= 1;
+    bool vx[VX + 1];
+#pragma unroll
+    for (int q = 0; q <= VX; ++q) vx[q] = q >= 1 || X >= 1;
+    const uint32_t ny = (uint32_t)vy0 + 1u;
+    const uint32_t nz = (uint32_t)vz0 + (uint32_t)vz1;
+    auto mk = [&](const uint32_t (&v)[VX + 1], int q) { return vx[q] ? v[q] : 0u; };
+    auto left = [&](uint32_t (&v)[VX + 1]) { v[0] = shup(v[VX], 1); };
+    auto put8 = [&](int k, const uint32_t (&res)[VX]) {
+      int par[3];
+      map_parity(3, k, par);
+      if (!par[0] || vz1) st8(mbase[k] + c * lplane, pack8<T, VX>(res));
+    };
+    const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own;
+    T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
+    uint32_t ownv[VX];
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pY[i] = (P11[i + 1] + mk(P12, i) + mk(Q13, i) + Q14[i + 1]) >> ((nz * nx) >> 1);
-      pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
+      if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own, i);
+      else ownv[i] = el16<T>(e0, 2 * i);
     }
-    code(5, pY, e1, 0, oY);
-    code(2, pF, e1, 1, oF);
-    if constexpr (DEC) {
-      st16(h0 + a.W_, pack16<T, VX>(oY, oF));
-    } else {
-      put8(5, oY);
-      put8(2, oF);
-    }
-  }
-  // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
-  {
-    uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
-    uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
-    rd(0, P0);
-    rd(1, P1);
-    rd(6, P6);
-    left(P1);
+    auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
 #pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-      pL[i] = (P0[i + 1] + mk(P1, i)) >> (nx >> 1);
-      pC[i] = P6[i + 1];
+      for (int i = 0; i < VX; ++i) {
+        if constexpr (DEC) outv[i] = (pred[i] + el8<T>(sv.mv[k], i)) & MASK;
+        else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+      }
+    };
+
+    // X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); with the lowres
+    {
+      uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
+      rd(15, P15);
+      rd(18, Q18);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) pred[i] = (P15[i + 1] + A16[i + 1] + QA17[i + 1] + Q18[i + 1]) >> ((nz * ny) >> 1);
+      code(6, pred, e0, 1, outv);
+      if constexpr (DEC) {
+        st16(h0, pack16<T, VX>(ownv, outv));
+      } else {
+        st8(lout + c * lplane + lo_own, pack8<T, VX>(ownv));
+        put8(6, outv);
+      }
     }
-    code(0, pL, o1, 0, oL);
-    code(3, pC, o1, 1, oC);
-    if constexpr (DEC) {
-      if (vz1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
-    } else {
-      put8(0, oL);
-      put8(3, oC);
+    // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
+    {
+      uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
+      uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
+      rd(7, P7);
+      rd(8, P8);
+      rd(2, P2);
+      left(P8);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pZ[i] = (P7[i + 1] + mk(P8, i) + mk(A9, i) + A10[i + 1]) >> ((ny * nx) >> 1);
+        pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
+      }
+      code(4, pZ, sv.o0, 0, oZ);
+      code(1, pU, sv.o0, 1, oU);
+      if constexpr (DEC) {
+        if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
+      } else {
+        put8(4, oZ);
+        put8(1, oU);
+      }
     }
+    // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
+    {
+      uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
+      uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
+      rd(11, P11);
+      rd(12, P12);
+      rd(13, Q13);
+      rd(14, Q14);
+      rd(4, P4);
+      rd(5, Q5);
+      left(P12);
+      left(Q13);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pY[i] = (P11[i + 1] + mk(P12, i) + mk(Q13, i) + Q14[i + 1]) >> ((nz * nx) >> 1);
+        pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
+      }
+      code(5, pY, sv.e1, 0, oY);
+      code(2, pF, sv.e1, 1, oF);
+      if constexpr (DEC) {
+        st16(h0 + a.W_, pack16<T, VX>(oY, oF));
+      } else {
+        put8(5, oY);
+        put8(2, oF);
+      }
+    }
+    // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
+    {
+      uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
+      uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
+      rd(0, P0);
+      rd(1, P1);
+      rd(6, P6);
+      left(P1);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) {
+        const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
+        pL[i] = (P0[i + 1] + mk(P1, i)) >> (nx >> 1);
+        pC[i] = P6[i + 1];
+      }
+      code(0, pL, sv.o1, 0, oL);
+      code(3, pC, sv.o1, 1, oC);
+      if constexpr (DEC) {
+        if (vz1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
+      } else {
+        put8(0, oL);
+        put8(3, oC);
+      }
+    }
+  };
+
+  // ---- the run: per output plane c, [code plane c-1 | stage node plane c+2 | load node plane
+  // c+3 and plane c's streams] barrier [channels of plane c] barrier.  Node planes c-1 .. c+3 stay
+  // in registers (R0 .. R4) until their coder step; each node plane is loaded and staged once
+  // per run.  Two workgroups share a CU (LDS), one in its channel phase while the other codes ----
+  bx::u32x4 bC[8], bQ[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bC[q] = a.frag[q * 64 + lane];
+    bQ[q] = a.frag[(8 + q) * 64 + lane];
   }
+  const float* fb = (const float*)(a.frag + 3 * 8 * 64);
+  const float biasC = fb[lane], biasQ = fb[64 + lane];
+  V R0 = node_row(cb - 1), R1 = node_row(cb), R2 = node_row(cb + 1), R3 = node_row(cb + 2);
+  stage(node_row(cb - 2), cb - 2);
+  stage(R0, cb - 1);
+  stage(R1, cb);
+  stage(R2, cb + 1);
+  Streams Sp, Sc;
+  for (int c = cb; c < ce; ++c) {
+#ifndef L3Q_NOAGG
+    if (c > cb) aggregate(c - 1, R0, Sp);
+#endif
+    stage(R3, c + 2);
+    V R4{};
+    if (c + 1 < ce) R4 = node_row(c + 3);
+    load_streams(c, Sc);
+    __syncthreads();
+    channels(c, bC, bQ, biasC, biasQ);
+    __syncthreads();
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    R3 = R4;
+    Sp = Sc;
+  }
+#ifndef L3Q_NOAGG
+  aggregate(ce - 1, R0, Sp);
+#endif
 }
 
 }  // namespace l3q
@@ -447,8 +478,15 @@ static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   a.Ez = (int)g.E[0]; a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
   a.Lcz = (int)g.Lc[0]; a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.zbegin = (int)zb; a.zend = (int)ze;
-  const int64_t nblk = B * (ze - zb);
-  a.xcd_per = (l3q_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  // each workgroup codes a run of output planes of one tile (node planes staged once per run):
+  // runs of >= 4 planes, enough of them for 2 workgroups per CU (the LDS holds 2)
+  const int64_t nz = ze - zb;
+  int64_t nsplit = std::min<int64_t>(ceil_div(512, B), ceil_div(nz, 4));
+  if (nsplit < 1) nsplit = 1;
+  a.zper = (int)ceil_div(nz, nsplit);
+  a.nsplit = (int)ceil_div(nz, a.zper);
+  const int64_t nblk = B * a.nsplit;
+  a.xcd_per = (l3q_env("KMP_W3_XCD", 1) && B % 8 == 0) ? a.nsplit : 0;
   const int rows = 64 / (a.Ex / 4);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * (a.Ey / rows)));

@@ -129,7 +129,8 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
       const bool col_ok = k < K;
       const float bk = col_ok ? bias[k] : 0.0f;
       bx::f32x4 acc = {bk, bk, bk, bk};
-      for (int q = 0; q < nq; ++q) {
+      for (int qi = 0; qi < nq; ++qi) {
+        const int q = bx::chunk_at(qi, nq);
         bx::u32x4 a;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

