@@ -11,22 +11,31 @@
 // kernel at 510-560 us per C3 volume; as bf16 MFMAs they go to the matrix pipe (16 x 16 cells x
 // channels per MFMA, 16 cycles).
 //
-// A workgroup owns one output plane c of one tile; its waves own ROWS lowres rows each (the
-// lane layout, loads, staging and aggregation of kmp_codec_linear3dp.hip):
-//   1. every lane loads its 4 nodes of the 5 node planes c-2 .. c+2 and stages them in LDS as
-//      feature dwords (bf16 hi byte | bf16 lo byte) with the mirrored halo rows / columns of the
-//      symmetric neighbourhood pad over the even reflect pad (volume/utils.py:213-237); a barrier;
-//   2. per 16-cell tile (16 consecutive x of one row) two column tiles: cell plane c (node planes
-//      c-1 .. c+2, its 14 channels) and cell plane c-1 (node planes c-2 .. c+1, channels 5, 13, 14,
-//      17, 18), 8 MFMAs each.  Chunk q = 2 dz + h covers node rows dy = 2h, 2h+1 of plane dz: the
-//      A fragment of lane (g, m) is its cell's 4 consecutive nodes x-1 .. x+2 of node row 2h +
-//      (g & 1) -- so the plane-c tile's chunk (dz, h) and the plane-(c-1) tile's chunk (dz+1, h)
-//      read the same fragment, and row Y's h = 1 fragment is row Y+2's h = 0 one: the wave walks
-//      its rows by parity and reads 5 fragments per row instead of 16.  The weights' B fragments
-//      stay in registers for the whole plane.  Each MFMA leaves a lane one channel of 4 cells,
-//      cast to u16 and written to the wave's channel table [channel][row][x] in LDS; a barrier;
-//   3. each lane reads back its cells' channels (the row above from the same table, the wave
-//      above's last row included) and runs linear3dp's aggregation, coder and stores.
+// A workgroup owns a run of output planes of one tile (all 32 at C3) and rolls along z; its waves own
+// ROWS lowres rows each (the lane layout, loads and aggregation of kmp_codec_linear3dp.hip).  Per
+// output plane c:
+//   1. the coder phase: plane c-1's maps and coder (below); node plane c+2's rows, loaded a step
+//      earlier, staged in LDS as feature dwords (bf16 hi byte | bf16 lo byte) with the mirrored
+//      halo rows / columns of the symmetric neighbourhood pad over the even reflect pad
+//      (volume/utils.py:213-237) into a 5-slot ring; node plane c+3 and plane c's streams loaded
+//      for the next step -- so each node plane is read from HBM and staged once per run; a barrier;
+//   2. the channel phase: per 16-cell tile (16 consecutive x of one row) two column tiles: cell plane
+//      c (node planes c-1 .. c+2, its 14 channels) and cell plane c-1 (node planes c-2 .. c+1,
+//      channels 5, 13, 14, 17, 18), 8 MFMAs each.  Chunk q = 2 dz + h covers node rows dy = 2h, 2h+1
+//      of plane dz: the A fragment of lane (g, m) is its cell's 4 consecutive nodes x-1 .. x+2 of
+//      node row 2h + (g & 1) -- so the plane-c tile's chunk (dz, h) and the plane-(c-1) tile's chunk
+//      (dz+1, h) read the same fragment, and row Y's h = 1 fragment is row Y+2's h = 0 one: the wave
+//      walks its rows by parity and reads 5 fragments per row instead of 16.  The weights' B
+//      fragments (built once per call, fragments_kernel) stay in registers for the whole run.  Each
+//      MFMA leaves a lane one channel of 4 cells, cast to u16 and written to the wave's channel table
+//      [channel][row][x] in LDS; a barrier;
+//   3. (in the next step's coder phase) each lane reads back its cells' channels (the row above from
+//      the same table, the wave above's last row included) and runs linear3dp's aggregation, coder
+//      and stores.
+// 75 KB of LDS a workgroup (ring 34 KB, channel tables 41 KB), 2 workgroups per CU,
+// so one workgroup's channel phase overlaps the other's coder phase.  LDS pitches are padded so the
+// fragment reads (ds_read2_b32: banks (a/4) mod 32 per half wave) and the channel-table writes are
+// conflict-free.
 #include <cstdlib>
 
 #include "kmp_bf16x2.h"
@@ -215,14 +224,8 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
 #pragma unroll
     for (int t = 0; t < NPL; ++t) sl[t] = (c - 2 + t + 2 * NPL) % NPL;
     auto frag = [&](int t, int ry, int x0) {
-#ifdef L3Q_NOFRAG
-      const uint32_t u = (uint32_t)(t * 977 + ry * 131 + x0 + lane);
-      return (bx::u32x4){bx::feature_dword(u & 0xffff), bx::feature_dword((u + 1) & 0xffff),
-                         bx::feature_dword((u + 2) & 0xffff), bx::feature_dword((u + 3) & 0xffff)};
-#else
       const uint32_t* p = st + (sl[t] * NR + ry + (g & 1)) * PITCH + x0 + m;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
-#endif
     };
     auto put = [&](int k, int row, int x0, const bx::f32x4& d) {
       *(uint2*)(ctw + k * CS + row * EX + x0 + 4 * g) = bx::cast_pack4<T>(d);
@@ -422,9 +425,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   stage(R2, cb + 1);
   Streams Sp, Sc;
   for (int c = cb; c < ce; ++c) {
-#ifndef L3Q_NOAGG
     if (c > cb) aggregate(c - 1, R0, Sp);
-#endif
     stage(R3, c + 2);
     V R4{};
     if (c + 1 < ce) R4 = node_row(c + 3);
@@ -438,9 +439,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     R3 = R4;
     Sp = Sc;
   }
-#ifndef L3Q_NOAGG
   aggregate(ce - 1, R0, Sp);
-#endif
 }
 
 }  // namespace l3q
