@@ -255,10 +255,11 @@ __device__ __forceinline__ void quotients(const uint32_t (&w)[Sw<W>::NW], int k,
   }
 }
 
-// 4 waves per SIMD (amdgpu_waves_per_eu: at most 128 VGPRs, 16-bit samples spill 28 bytes): 170 vs
-// 180 us per C3 bundle at 3 waves (137 VGPRs), profiles/round4/ab_rice_waves4_r4r1.log
+// 8- and 16-bit samples at 4 waves per SIMD (amdgpu_waves_per_eu: at most 128 VGPRs, 16-bit samples
+// spill 28 bytes): 170 vs 180 us per C3 bundle at 3 waves (137 VGPRs),
+// profiles/round4/ab_rice_waves4_r4r1.log; 32-bit samples need more registers than that
 template <int W>
-__global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_per_eu(4))) rice_bundle_encode_kernel(RArrs A, int64_t tile_begin, int64_t tiles_total,
+__global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_per_eu(W <= 16 ? 4 : 1))) rice_bundle_encode_kernel(RArrs A, int64_t tile_begin, int64_t tiles_total,
                                                                uint8_t* __restrict__ blob, int64_t payload_off,
                                                                uint64_t* __restrict__ state,
                                                                unsigned* __restrict__ ticket) {
