@@ -35,7 +35,8 @@ if wl == 'rice':  # Rice bundle encode + decode of 8 C3-sized u16 maps of N(0, s
         kpk._rice_encode_launch(arrays, (1, 1, 1))
         outs, _, bad = kpk._rice_decode_launch(blob, hb)
     torch.cuda.synchronize()
-    assert int(bad.item()) == 0 and all(torch.equal(a, b) for a, b in zip(outs, arrays))
+    if os.environ.get('KMP_NOCHECK', '0') == '0':
+        assert int(bad.item()) == 0 and all(torch.equal(a, b) for a, b in zip(outs, arrays))
     print('ok', os.environ.get('KMP_TAG', ''), 'bundle bytes', blob.numel())
     sys.exit(0)
 ndim = 3 if wl == 'volume' else 2
