@@ -424,10 +424,10 @@ def test_categorical_coder_vs_oracle(kom, vec):
 @pytest.mark.parametrize('dt', [np.uint8, np.uint16])
 @pytest.mark.parametrize('off', [1, 2, 3])
 def test_categorical_value_offsets(kom, dt, off):
-    """Values (classes / ranks) that start off elements past an aligned address: the vector
-    kernels read each value as the aligned dword that holds it and shift it out (cat_xval), so
-    every byte position inside the dword is exercised, on both directions and on the peel and radix
-    paths of the decode."""
+    """Values (classes / ranks) that start off elements past an aligned address and end at their
+    buffer's last element: the vector kernels read each value as the aligned dword that holds it
+    and shift it out (cat_xval), so every byte position inside the dword is exercised, on both
+    directions and on the peel and radix paths of the decode."""
     import oracle
     n, L = 2053, 256
     rng = np.random.default_rng(19 + off)
@@ -436,8 +436,9 @@ def test_categorical_value_offsets(kom, dt, off):
     x = rng.integers(0, L, n).astype(dt)
     x[::2] = rng.integers(0, 4, x[::2].size)  # small ranks: the peel
     lg = torch.from_numpy(logits).cuda()
-    buf = torch.zeros(n + 4, dtype=torch.uint8 if dt == np.uint8 else torch.int16, device='cuda')
-    xg = buf[off:off + n]
+    # the values end at the buffer's last element (the kernels read the aligned dword around each one)
+    buf = torch.zeros(off + n, dtype=torch.uint8 if dt == np.uint8 else torch.int16, device='cuda')
+    xg = buf[off:]
     xg.copy_(torch.from_numpy(x.view(np.int16) if dt == np.uint16 else x))
     if dt == np.uint16:
         xg = xg.view(torch.uint16)
