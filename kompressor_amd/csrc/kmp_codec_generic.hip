@@ -145,7 +145,9 @@ int64_t generic_workspace_bytes(int dtype, int nsp, const Geo& g, int64_t B, int
   int64_t need = B * g.Lc[0] * g.Lc[1] * g.Lc[2] * K * C * dtype_size(dtype);
   if (lin && B > 0) {  // the fused LinearPredictor kernels keep a reordered copy of W [N, K] there
     const int64_t nb = 2 * pred->padding + 2, N = nsp == 3 ? nb * nb * nb : nb * nb;
-    const int64_t wbytes = N * K * (int64_t)sizeof(float);
+    int64_t wbytes = N * K * (int64_t)sizeof(float);
+    // the matrix-core kernels' B fragments (3 column tiles x 8 chunks x 64 lanes x 16 B) + biases
+    if (pred->kind == KMP_PRED_LINEAR_MFMA) wbytes = wbytes > 3 * 8 * 64 * 16 + 3 * 64 * 4 ? wbytes : 3 * 8 * 64 * 16 + 3 * 64 * 4;
     need = need > wbytes ? need : wbytes;
   }
   return need;

@@ -157,7 +157,8 @@ BF_CASES = [(3, 0, (4, 64, 64, 64, 1), np.uint16), (3, 0, (2, 16, 32, 32, 1), np
             # p = 1 on the fused matrix-core kernel (linear3pm): 32 / 16-wide rows and planes
             (3, 1, (2, 12, 64, 64, 1), np.uint16), (3, 1, (1, 10, 32, 32, 1), np.uint16),
             (3, 1, (1, 8, 32, 64, 1), np.uint16), (3, 1, (1, 7, 64, 32, 1), np.uint16),
-            (3, 1, (1, 8, 32, 64, 1), np.uint8)]
+            (3, 1, (1, 8, 32, 64, 1), np.uint8),
+            (3, 1, (1, 6, 32, 32, 1), np.uint16)]  # a small volume: the workspace still holds the fragments
 
 
 @pytest.mark.parametrize('ndim,p,shape,dtype', BF_CASES)
