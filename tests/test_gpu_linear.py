@@ -227,3 +227,40 @@ def test_linear_bf16x2_rejects_32bit_samples(kom):
     pred = kom.LinearPredictor(w, b, 0, 3, arith='bf16x2')
     with pytest.raises(Exception):
         kom.volume.encode(pred, kom.volume.encode_values_raw, hi)
+
+
+def test_linear_bf16x2_p1_fused_sweep(kom, monkeypatch):
+    """Seeded sweep of fused-eligible p = 1 volumes (u16, 16 / 32-wide rows and planes, any depth,
+    batch sizes that do and do not take the XCD order, smooth and full-range data, chunked regions):
+    linear3pm's lowres + maps equal the generic bf16x2 path's bit for bit (KMP_DISABLE_LINEAR_FUSED),
+    and the round trip is lossless."""
+    V = kom.volume
+    rng = np.random.default_rng(2024)
+    for case in range(10):
+        B = int(rng.choice([1, 2, 3, 8]))
+        D = int(rng.integers(6, 24))
+        H, W = int(rng.choice([32, 64])), int(rng.choice([32, 64]))
+        hi = _data((B, D, H, W, 1), np.uint16, 100 + case)
+        if case % 2:  # smooth data: small residuals, the predictor's realistic regime
+            z, y, x = np.meshgrid(np.arange(D), np.arange(H), np.arange(W), indexing='ij')
+            hi = ((1000 + 40 * z + 25 * y + 10 * x)[None, ..., None] + rng.integers(0, 9, (B, D, H, W, 1))).astype(np.uint16)
+        w, b = _weights(3, 1, 200 + case, np.uint16)
+        pred = kom.LinearPredictor(w, b, 1, 3, arith='bf16x2')
+        hi_t = torch.from_numpy(hi).cuda()
+        lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, hi_t, padding=1)
+        assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_encode', (B, D, H, W)
+        chunk = int(rng.integers(4, 12))
+        lo_c, (maps_c, _) = V.encode_chunks(pred, V.encode_values_uint16, hi_t, chunk=chunk, padding=1)
+        with monkeypatch.context() as mp:
+            mp.setenv('KMP_DISABLE_LINEAR_FUSED', '1')
+            lo_g, (maps_g, _) = V.encode(pred, V.encode_values_uint16, hi_t, padding=1)
+            assert kom._lib.lib.kmp_last_launch().decode() == 'encode_generic'
+        assert torch.equal(lo, lo_g) and torch.equal(lo_c, lo_g)
+        for i, (a, c, g) in enumerate(zip(maps, maps_c, maps_g)):
+            assert torch.equal(a, g), f'case {case} map {i}: {int((a != g).sum())} mismatches'
+            assert torch.equal(c, g), f'case {case} chunked map {i}'
+        rec = V.decode(pred, V.decode_values_uint16, lo, (maps, dims), padding=1)
+        assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_decode'
+        assert torch.equal(rec, hi_t)
+        rec_c = V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=chunk, padding=1)
+        assert torch.equal(rec_c, hi_t)
