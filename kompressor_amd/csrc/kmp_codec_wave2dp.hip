@@ -231,7 +231,11 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
 // p+1 rows below).  So a step loads one node row and its output rows per lane, against the
 // plane-group kernel's node row + up to two halo rows; the node rows of step s+2 and the output
 // rows of step s+1 are in flight while step s computes.
-template <typename T, bool DEC, int P, bool STC = false>
+// STEPS > 0: the run is STEPS steps (rrun == STEPS * rows), fully unrolled, so the pipeline's
+// register ring is renamed rather than moved (the moves made every step wait for all its loads,
+// vmcnt(0), including the next step's just issued), and the output rows load unconditionally from
+// clamped rows (needs Lcy >= 1), so the waits stay counted
+template <typename T, bool DEC, int P, bool STC = false, int STEPS = 0>
 __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
   constexpr int VX = 8 / (int)sizeof(T);
   constexpr int NB = 2 * P + 2;
@@ -279,6 +283,17 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
     const int Y = y0 + r;
     const bool live = Y < a.Ey && Y < Ye, vy1 = Y < a.Lcy;
     const int Yc = live ? Y : 0;
+    if constexpr (STEPS > 0) {  // unconditional: lanes without the row read row 0 (unused)
+      const int Yl = live && vy1 ? Y : 0;
+      if constexpr (DEC) {
+        O.mv[0] = ld8((const T*)a.maps.p[0] + (b * a.Lcy + Yl) * a.Ex + X);
+        O.mv[1] = ld8((const T*)a.maps.p[1] + (b * a.Ey + Yc) * a.Ex + X);
+        O.mv[2] = ld8((const T*)a.maps.p[2] + (b * a.Lcy + Yl) * a.Ex + X);
+      } else {
+        O.o0 = ld16(hin + (live && vy1 ? 2 * Y + 1 : 0) * a.W + hx);
+      }
+      return;
+    }
     O.o0 = make_uint4(0, 0, 0, 0);
     O.mv[0] = O.mv[1] = O.mv[2] = make_uint2(0, 0);
     if constexpr (DEC) {
@@ -333,10 +348,8 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
   xpack(load_node(Ys - rows), pprev);
   xpack(own, pcur);
 
-#pragma unroll 1
-  for (int Y0 = Ys; Y0 < Ye; Y0 += rows) {
-    const bool more = Y0 + rows < Ye;
-    const V vnn = more ? load_node(Y0 + 2 * rows) : V{};  // step s+2's node rows
+  auto step = [&](const int Y0, const bool more, const bool more2) __attribute__((always_inline)) {
+    const V vnn = more2 ? load_node(Y0 + 2 * rows) : V{};  // step s+2's node rows
     if (more) load_out(Y0 + rows, Onext);
     uint32_t pnext[VW];
     xpack(vnext, pnext);
@@ -433,6 +446,13 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
     own = vnext;
     vnext = vnn;
     Ocur = Onext;
+  };
+  if constexpr (STEPS > 0) {
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) step(Ys + s * rows, s + 1 < STEPS, s + 2 <= STEPS);
+  } else {
+#pragma unroll 1
+    for (int Y0 = Ys; Y0 < Ye; Y0 += rows) step(Y0, Y0 + rows < Ye, Y0 + rows < Ye);
   }
 }
 
@@ -445,7 +465,9 @@ static int w2p_env(const char* name, int dflt) {
 
 // y-rolling kernel (wave2dr_kernel): output rows per wave, 0 = the row-group kernel; rounded up to
 // a multiple of the wave's rows.  Default 32 (C2 p = 1: 33.5 / 31.4 -> 28.4 / 28.1 us per
-// direction, profiles/round2/ab_wave2dr.log).  KMP_W2R_RUN overrides.
+// direction, profiles/round2/ab_wave2dr.log); runs of 8 steps take the unrolled form (C2 p = 1
+// 28.5 / 26.0 -> 27.0-28.2 / 24.7-25.7 us, p = 2 32.2 / 29.5 -> 31.3-31.7 / 27.8-28.8 us by
+// rocprofv3, profiles/round4/ab_wave2dr_unroll_r4w.log).  KMP_W2R_RUN overrides.
 static int w2p_run(int P, int bytes) {
   (void)P;
   (void)bytes;
@@ -502,6 +524,11 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
 template <typename T, bool DEC, bool STC>
 static void launch_wave2dp_s(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
   if (a.rrun > 0) {
+    if (a.rrun == 8 * a.rows && a.Lcy >= 1) {  // C2: runs of 32 rows, 4 per step
+      if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC, 8><<<grid, block, 0, s>>>(a);
+      else w2p::wave2dr_kernel<T, DEC, 2, STC, 8><<<grid, block, 0, s>>>(a);
+      return;
+    }
     if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
     else w2p::wave2dr_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
     return;
