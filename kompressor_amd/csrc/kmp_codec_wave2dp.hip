@@ -269,11 +269,18 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
   const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * himg;
   T* hout = DEC ? (T*)a.hi_out + b * himg : nullptr;
   const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
+  // the image's row arrays: a uniform base plus a 32-bit lane offset per access (an image holds
+  // < 2^31 samples), not 64-bit products per lane and step
+  T* const mlo = (T*)(DEC ? nullptr : a.lo_out) + b * (int64_t)a.Ey * a.Ex;
+  T* const mb[3] = {(T*)a.maps.p[0] + b * (int64_t)a.Lcy * a.Ex, (T*)a.maps.p[1] + b * (int64_t)a.Ey * a.Ex,
+                    (T*)a.maps.p[2] + b * (int64_t)a.Lcy * a.Ex};
 
   auto load_node = [&](int y0) __attribute__((always_inline)) {  // node row y0 + r (mirrored past the ends)
-    const int y = lsrc(y0 + r, a.Ly, a.Ey);
-    if constexpr (DEC) return (V)ld8c(lin + y * a.Ex + X);
-    else return (V)ld16c(hin + 2 * y * a.W + hx);
+    // STEPS > 0: the host guarantees Ly >= rrun + rows, so every row read lies in [-Ly, 2 Ly) and one
+    // reflection (lsrc1) equals the general lsrc, without its divisions
+    const int y = STEPS > 0 ? lsrc1(y0 + r, a.Ly, a.Ey) : lsrc(y0 + r, a.Ly, a.Ey);
+    if constexpr (DEC) return (V)ld8c(lin + (uint32_t)(y * a.Ex + X));
+    else return (V)ld16c(hin + (uint32_t)(2 * y * a.W + hx));
   };
   struct Out {
     uint4 o0;
@@ -286,11 +293,11 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
     if constexpr (STEPS > 0) {  // unconditional: lanes without the row read row 0 (unused)
       const int Yl = live && vy1 ? Y : 0;
       if constexpr (DEC) {
-        O.mv[0] = ld8((const T*)a.maps.p[0] + (b * a.Lcy + Yl) * a.Ex + X);
-        O.mv[1] = ld8((const T*)a.maps.p[1] + (b * a.Ey + Yc) * a.Ex + X);
-        O.mv[2] = ld8((const T*)a.maps.p[2] + (b * a.Lcy + Yl) * a.Ex + X);
+        O.mv[0] = ld8(mb[0] + (uint32_t)(Yl * a.Ex + X));
+        O.mv[1] = ld8(mb[1] + (uint32_t)(Yc * a.Ex + X));
+        O.mv[2] = ld8(mb[2] + (uint32_t)(Yl * a.Ex + X));
       } else {
-        O.o0 = ld16(hin + (live && vy1 ? 2 * Y + 1 : 0) * a.W + hx);
+        O.o0 = ld16(hin + (uint32_t)((live && vy1 ? 2 * Y + 1 : 0) * a.W + hx));
       }
       return;
     }
@@ -413,7 +420,7 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
       }
       uint32_t n[VX];
       nodes(own, n);
-      const int64_t m_lr = (b * a.Lcy + Y) * a.Ex + X, m_ud = (b * a.Ey + Y) * a.Ex + X;
+      const uint32_t m_row = (uint32_t)(Y * a.Ex + X);  // in the lowres and every map (rows Y < Lcy)
       if constexpr (!DEC) {
         uint32_t res[3][VX];
 #pragma unroll
@@ -422,17 +429,17 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
           res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;      // UD (0,1)
           res[2][i] = (el16<T>(Ocur.o0, 2 * i + 1) - pred[2][i]) & MASK;  // C  (1,1)
         }
-        stp8<STC>((T*)a.lo_out + m_ud, pack8<T, VX>(n));
-        if (vy1) stp8<STC>((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
-        stp8<STC>((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
-        if (vy1) stp8<STC>((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
+        stp8<STC>(mlo + m_row, pack8<T, VX>(n));
+        if (vy1) stp8<STC>(mb[0] + m_row, pack8<T, VX>(res[0]));
+        stp8<STC>(mb[1] + m_row, pack8<T, VX>(res[1]));
+        if (vy1) stp8<STC>(mb[2] + m_row, pack8<T, VX>(res[2]));
       } else {
         uint32_t dv[3][VX];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
 #pragma unroll
           for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(Ocur.mv[k], i)) & MASK;
-        T* h0 = hout + 2 * Y * a.W + hx;
+        T* h0 = hout + (uint32_t)(2 * Y * a.W + hx);
         st16(h0, pack16<T, VX>(n, dv[1]));
         if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[0], dv[2]));
       }
@@ -524,7 +531,7 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
 template <typename T, bool DEC, bool STC>
 static void launch_wave2dp_s(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
   if (a.rrun > 0) {
-    if (a.rrun == 8 * a.rows && a.Lcy >= 1) {  // C2: runs of 32 rows, 4 per step
+    if (a.rrun == 8 * a.rows && a.Lcy >= 1 && a.Ly >= a.rrun + a.rows) {  // C2: runs of 32 rows, 4 per step
       if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC, 8><<<grid, block, 0, s>>>(a);
       else w2p::wave2dr_kernel<T, DEC, 2, STC, 8><<<grid, block, 0, s>>>(a);
       return;

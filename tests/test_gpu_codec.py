@@ -595,9 +595,12 @@ def _W2P_DEFAULT(p, dtype):
     ((2, 31, 48, 1), np.uint16, 2),      # 6 lanes per row is not a power of two: the LDS kernel
     ((1, 20, 256, 1), np.uint16, 1),     # 2 rows per wave
     ((2, 9, 16, 1), np.uint8, 2),        # one lane per row, Ey = 5 < rows
-    ((2, 67, 256, 1), np.uint8, 1),      # default runs of 8 unrolled steps, the last one partial, odd height
+    ((2, 67, 256, 1), np.uint8, 1),      # odd height, a partial last run; Ly < run + rows: the step loop
     ((2, 67, 256, 1), np.uint8, 2),
-    ((2, 70, 128, 1), np.uint16, 2),     # 16-bit, 4 rows per wave: the unrolled steps, a partial last run
+    ((2, 70, 128, 1), np.uint16, 2),
+    ((2, 141, 256, 1), np.uint8, 1),     # runs of 8 unrolled steps (Ly >= run + rows), the last one partial
+    ((2, 141, 256, 1), np.uint8, 2),
+    ((2, 142, 128, 1), np.uint16, 1),    # 16-bit, 4 rows per wave, unrolled, partial last run
 ])
 @pytest.mark.parametrize('run', [None, '0', '8', '12', '64'])
 def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
