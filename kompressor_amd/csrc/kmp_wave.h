@@ -75,8 +75,14 @@ __device__ __forceinline__ uint4 pack16(const uint32_t (&ev)[VX], const uint32_t
   }
 }
 
+__device__ __forceinline__ int lsrc1(int r, int L, int E);
+
 __device__ __forceinline__ int lsrc(int r, int L, int E) {
-  // stored node index of padded node r along an axis (even reflect pad: node E -> E - 1)
+  // stored node index of padded node r along an axis (even reflect pad: node E -> E - 1).  Within one
+  // reflection of the axis (-L <= r < 2L, and L <= 2E: m < L <= 2E below) that is lsrc1's
+  // division-free form; the integer divisions (VALU reciprocal sequences with quarter-rate multiplies,
+  // even for uniform r) run only for indices further out
+  if (r >= -L && r < 2 * L && L <= 2 * E) return lsrc1(r, L, E);
   int m = r % (2 * L);
   if (m < 0) m += 2 * L;
   m = m < L ? m : 2 * L - 1 - m;
