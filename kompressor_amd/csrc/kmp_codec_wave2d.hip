@@ -55,8 +55,8 @@ __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
+  const int tx = lane & (a.txn - 1);          // txn: a power of two (host)
+  const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
   int blk = vblk;
   if (a.xcd_per > 0) {
@@ -271,8 +271,8 @@ __device__ __forceinline__ void wave2d_u8_dec_body(const W2& a, int vblk) {
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
+  const int tx = lane & (a.txn - 1);          // txn: a power of two (host)
+  const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
   int blk = vblk;
   if (a.xcd_per > 0) {

@@ -82,8 +82,8 @@ __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
+  const int tx = lane & (a.txn - 1);          // txn: a power of two (host)
+  const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
   // a.xcd_per > 0: tile-per-XCD order -- XCD x = blockIdx % 8 codes whole tiles, its k-th block
   // is block (k % per_tile) of tile (k / per_tile) * 8 + x, so the z-halo neighbours share an L2

@@ -83,11 +83,14 @@ __device__ __forceinline__ int lsrc(int r, int L, int E) {
   // division-free form; the integer divisions (VALU reciprocal sequences with quarter-rate multiplies,
   // even for uniform r) run only for indices further out
   if (r >= -L && r < 2 * L && L <= 2 * E) return lsrc1(r, L, E);
-  int m = r % (2 * L);
-  if (m < 0) m += 2 * L;
+  // periodic folds by subtraction, not %: a division's reciprocal setup depends only on L / E, so
+  // the compiler hoists it out of this rare branch into every kernel's prologue
+  int m = r;
+  while (m < 0) m += 2 * L;
+  while (m >= 2 * L) m -= 2 * L;
   m = m < L ? m : 2 * L - 1 - m;
-  int m2 = m % (2 * E);
-  return m2 < E ? m2 : 2 * E - 1 - m2;
+  while (m >= 2 * E) m -= 2 * E;
+  return m < E ? m : 2 * E - 1 - m;
 }
 
 // lsrc for indices within one reflection of the axis (-L <= r < 2L): no integer division
