@@ -129,8 +129,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 
   const int lane = threadIdx.x & 63;
   const int wv_ = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
+  const int tx = lane & (a.txn - 1);
+  const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
   int blk = (int)blockIdx.x;
   if (a.xcd_per > 0) {
@@ -495,7 +495,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
   const int lane = threadIdx.x;
   const int tx = lane & (a.txn - 1);
-  const int r = lane / a.txn;
+  const int r = lane >> __builtin_ctz(a.txn);
   const int rows = a.rows;
   const int X = tx * VX;
   int blk = (int)blockIdx.x;

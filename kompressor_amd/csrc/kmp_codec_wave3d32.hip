@@ -75,8 +75,8 @@ __global__ void __launch_bounds__(256) wave3d32_kernel(W32 a) {
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int tx = lane % a.txn;
-  const int r = lane / a.txn;
+  const int tx = lane & (a.txn - 1);
+  const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
   int blk = (int)blockIdx.x;
   if (a.xcd_per > 0) {
