@@ -190,8 +190,7 @@ __device__ __forceinline__ void wave2d_body(const W2& a, int vblk) {
   if (!live || Y < a.ybeg || Y >= a.yend) return;
 
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
   uint32_t pred[3][VX];  // LR, UD, C
   if constexpr (!LIN) {
@@ -333,8 +332,7 @@ __device__ __forceinline__ void wave2d_u8_dec_body(const W2& a, int vblk) {
 
   // validity of cells X-1 .. X+7 (vx[q] = cell X-1+q) as per-half masks
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
   uint32_t VM[4], BM[4];  // VM: cells X+2k, X+2k+1 valid; BM: both neighbours of the LR pair valid
 #pragma unroll
   for (int k = 0; k < 4; ++k) {

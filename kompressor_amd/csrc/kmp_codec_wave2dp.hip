@@ -183,8 +183,7 @@ __global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
   if (!live || Y < a.ybeg || Y >= a.yend) return;
 
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
 #pragma unroll
   for (int q = 0; q <= VX; ++q) {
@@ -402,8 +401,7 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
     if (Y < a.Ey && Y < Ye) {
       const bool vy1 = Y < a.Lcy, vy0 = Y >= 1;
       bool vx[VX + 1];
-#pragma unroll
-      for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+      cells_valid<VX>(vx, X, a.Lcx);
       const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
 #pragma unroll
       for (int q = 0; q <= VX; ++q) {

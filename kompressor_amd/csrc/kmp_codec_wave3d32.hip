@@ -208,8 +208,7 @@ __global__ void __launch_bounds__(256) wave3d32_kernel(W32 a) {
   cell_means(0);
 
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
 
 #pragma unroll
   for (int u = 0; u < PL; ++u) {

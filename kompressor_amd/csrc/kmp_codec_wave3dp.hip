@@ -240,8 +240,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   cell_means(0);
 
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
 
 #pragma unroll
@@ -512,8 +511,7 @@ wave3dr_kernel(W3P a) {
   cell_means(Mo[0], Ma[0]);
 
   bool vx[VX + 1];
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) vx[q] = (X - 1 + q) >= 0 && (X - 1 + q) < a.Lcx;
+  cells_valid<VX>(vx, X, a.Lcx);
   const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
 
   // one output plane: Sc holds its loads; plane c+PD's loads go into Sn first

@@ -93,6 +93,16 @@ __device__ __forceinline__ int lsrc(int r, int L, int E) {
   return m < E ? m : 2 * E - 1 - m;
 }
 
+// validity of cells X-1+q (q = 0..VX) for a lane whose VX nodes X..X+VX-1 lie inside the stored
+// row (the wave kernels' geometry: Ex = txn * VX).  Since Lc = L - 1 >= E - 1, cells X .. X+VX-2
+// always exist: only q = 0 (X = 0) and q = VX (the row's last cell) can be missing -- stated so
+// that the compiler keeps 2 lane masks, not VX + 1 (the C3 kernel spilled them to VGPR lanes)
+template <int VX>
+__device__ __forceinline__ void cells_valid(bool (&vx)[VX + 1], int X, int Lcx) {
+#pragma unroll
+  for (int q = 0; q <= VX; ++q) vx[q] = q == 0 ? X >= 1 : (q == VX ? X + VX - 1 < Lcx : true);
+}
+
 // lsrc for indices within one reflection of the axis (-L <= r < 2L): no integer division
 __device__ __forceinline__ int lsrc1(int r, int L, int E) {
   int m = r < 0 ? -1 - r : r;
