@@ -35,6 +35,7 @@ struct W2 {
   int32_t xcd_per;               // > 0: image-per-XCD block order (workgroups per image)
   int32_t ybeg, yend;            // output rows written (a chunked-driver region; all rows otherwise)
   int32_t nvblk;                 // virtual blocks (B * ngrp), grid-strided over the workgroups
+  UDiv ngrp_div;                 // n / ngrp (host-computed multiplier)
   const float* wt;               // LIN: LinearPredictor weights [4, 5] row-major and bias [5]
   const float* bias;
 };
@@ -273,13 +274,15 @@ __device__ __forceinline__ void wave2d_u8_dec_body(const W2& a, int vblk) {
   const int tx = lane & (a.txn - 1);          // txn: a power of two (host)
   const int r = lane >> __builtin_ctz(a.txn);
   const int X = tx * VX;
-  int blk = vblk;
-  if (a.xcd_per > 0) {
-    const int x = blk % 8, k = blk / 8;
-    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
-  }
-  const int grp = blk % a.ngrp;
-  const int64_t b = blk / a.ngrp;
+  // (the u8 decode: 22.0 -> 21.7 us; the encode body keeps % and /, 24.1 vs 24.6 us with this form,
+  // profiles/round4/ab_udiv_r4l5.log)
+  // virtual block -> (image b, row group grp); image-per-XCD order (xcd_per == ngrp): XCD x = vblk % 8
+  // codes whole images, its k-th block is group k % ngrp of image (k / ngrp) * 8 + x
+  const bool xcd = a.xcd_per > 0;
+  const uint32_t kk = xcd ? (uint32_t)vblk >> 3 : (uint32_t)vblk;
+  const uint32_t qq = udiv(kk, a.ngrp_div);
+  const int grp = (int)(kk - qq * (uint32_t)a.ngrp);
+  const int64_t b = xcd ? (int64_t)qq * 8 + (vblk & 7) : (int64_t)qq;
   const int Y0 = (grp * a.nwv + wv_) * a.rows;
   if (Y0 >= a.Ey) return;  // whole idle wave
   const int Y = Y0 + r;
@@ -414,6 +417,7 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)nwv; a.ngrp = (int)ngrp;
   a.xcd_per = (w2_env("KMP_W2_XCD", 1) && B % 8 == 0) ? (int)ngrp : 0;
+  a.ngrp_div = make_udiv((uint32_t)ngrp);
   a.ybeg = (int)yb;
   a.yend = (int)ye;
   const int64_t nblk = B * ngrp;

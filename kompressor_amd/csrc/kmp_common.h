@@ -214,6 +214,24 @@ struct CMapPtrs {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// n / d for a wave-uniform 0 <= n < 2^31 and a launch-constant d >= 1 as q = mulhi(n, m) >> s (s < 0:
+// d == 1, q = n), m = floor(2^(31+l) / d) + 1 with l = ceil(log2 d): exact on 31-bit n (error m d - 2^(31+l)
+// is in (0, d] and n d < 2^(31+l)).  Computed on the host, so the kernel divides with two scalar
+// instructions instead of a VALU reciprocal sequence with quarter-rate multiplies.
+struct UDiv {
+  uint32_t m;
+  int32_t s;
+};
+inline UDiv make_udiv(uint32_t d) {
+  if (d <= 1) return UDiv{0u, -1};
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  return UDiv{(uint32_t)(((uint64_t)1 << (31 + l)) / d + 1), l - 1};
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, UDiv f) {
+  return f.s < 0 ? n : __umulhi(n, f.m) >> f.s;
+}
+
 // 16-byte vectors: aligned, and any-alignment (gfx950 serves unaligned dwordx4 global accesses;
 // rows of odd length are only element-aligned)
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
