@@ -359,28 +359,23 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
     if (more) load_out(Y0 + rows, Onext);
     uint32_t pnext[VW];
     xpack(vnext, pnext);
-    // the p+1 rows above / below the step: previous step's last rows, next step's first rows
-    uint32_t pu[VW], pd[VW];
-#pragma unroll
-    for (int w = 0; w < VW; ++w) {
-      pu[w] = shdn(pprev[w], (rows - P - 1) * a.txn);
-      pd[w] = shup(pnext[w], (rows - P - 1) * a.txn);
-    }
+    // the y box: row r + d for |d| <= p+1, from this step's rows or, past the step's ends, the previous
+    // step's last / the next step's first rows.  One rotation by d rows per d (rows * txn = 64 lanes):
+    // the SOURCE lane picks what it sends -- for a given d, each source row feeds exactly one target row,
+    // which needs either its current row or (wrapped) the previous / next step's -- so a row shift is one
+    // ds_bpermute, not two plus a halo pre-shift
     uint32_t so[VW], su[VW];
 #pragma unroll
     for (int w = 0; w < VW; ++w) so[w] = su[w] = 0;
 #pragma unroll
     for (int d = -P - 1; d <= P + 1; ++d) {
-      const int j = r + d;
+      const int src = ((lane + d * a.txn) & 63) << 2;  // lane L reads lane L + d rows (mod 64)
 #pragma unroll
       for (int w = 0; w < VW; ++w) {
-        uint32_t v = d == 0 ? pcur[w] : (d < 0 ? shup(pcur[w], -d * a.txn) : shdn(pcur[w], d * a.txn));
-        if (d < 0) {
-          const uint32_t h = d == -P - 1 ? pu[w] : shdn(pu[w], (d + P + 1) * a.txn);
-          v = j < 0 ? h : v;
-        } else if (d > 0) {
-          const uint32_t h = d == P + 1 ? pd[w] : shup(pd[w], (P + 1 - d) * a.txn);
-          v = j >= rows ? h : v;
+        uint32_t v = pcur[w];
+        if (d != 0) {
+          const uint32_t send = d < 0 ? (r >= rows + d ? pprev[w] : pcur[w]) : (r < d ? pnext[w] : pcur[w]);
+          v = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)send);
         }
         if (d >= -P) so[w] += v;
         if (d <= P) su[w] += v;
