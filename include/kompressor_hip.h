@@ -81,6 +81,17 @@ const char* kmp_last_launch(void);
 /* 1 if the kernels were built for the device's ISA (gfx950) and a device is visible. */
 int kmp_device_ok(void);
 
+/* Process-wide dispatch options: switches to a fallback kernel family, the
+   encode store policy, the block order.  Each starts from the environment variable of the same
+   name, read once when the library loads; launches read the table, never the environment.
+   ``kmp_set_option(name, value)`` sets one (KMP_ERR_ARG for an unknown name);
+   ``kmp_clear_option`` returns it to the kernel's own default; ``kmp_get_option`` returns 1 and
+   the value when set, 0 when unset, KMP_ERR_ARG for an unknown name.  Not part of the
+   reference (which has no such switches); no production use needs them. */
+int kmp_set_option(const char* name, int value);
+int kmp_clear_option(const char* name);
+int kmp_get_option(const char* name, int* value);
+
 /* Device address of pinned (page-locked, device-mapped) host memory, for zero-copy streaming:
    the fused kernels then read the input from / write the outputs to host memory over the host
    link directly (kompressor_amd.stream, the reference's host-resident arrays,

@@ -77,6 +77,9 @@ def from_device(t, kind):
 # Host copies.  A pageable ``.cpu()`` of a large tensor runs at ~8 GB/s on the MI355X box (the
 # driver stages it); a copy into pinned memory runs at the link rate (~57 GB/s) and a parallel
 # memcpy from there into the numpy result at ~100 GB/s (profiles/round4/file_probe_r4s2.log).
+# Large transfers stream through a small ring of pinned chunks (``PinnedRing``): the link moves
+# chunk i+1 while the host copies chunk i, and the pinned memory a thread keeps is bounded
+# (``RING_CHUNK * RING_SLOTS`` per ring, whatever the transfer size).
 # ---------------------------------------------------------------------------------------------
 
 _TLS = threading.local()
@@ -84,15 +87,133 @@ _POOL = None
 _POOL_LOCK = threading.Lock()
 _COPY_THREADS = 8
 _SMALL = 4 << 20  # below this a plain .cpu() costs less than the hand-off
+RING_CHUNK = 16 << 20
+RING_SLOTS = 4
+_STAGING_CAP = 64 << 20  # pinned_staging buffers above this are not kept
 
 
 def pinned_staging(nbytes, slot='stage'):
-    """A reused pinned host byte buffer of at least ``nbytes`` (one per thread and ``slot``)."""
+    """A pinned host byte buffer of at least ``nbytes``: reused per thread and ``slot`` up to
+    ``_STAGING_CAP`` bytes; a larger request gets a buffer of its own, freed with its last reference
+    (so no thread keeps more than the cap pinned for the life of the process)."""
+    nbytes = int(nbytes)
+    if nbytes > _STAGING_CAP:
+        return torch.empty((nbytes,), dtype=torch.uint8, pin_memory=True)
     buf = getattr(_TLS, slot, None)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty((max(int(nbytes), 1 << 20),), dtype=torch.uint8, pin_memory=True)
+        buf = torch.empty((max(nbytes, 1 << 20),), dtype=torch.uint8, pin_memory=True)
         setattr(_TLS, slot, buf)
     return buf
+
+
+def release_pinned():
+    """Free this thread's cached pinned buffers (staging slots and chunk rings)."""
+    for k in list(vars(_TLS)):
+        delattr(_TLS, k)
+
+
+class PinnedRing:
+    """``RING_SLOTS`` pinned chunks of ``RING_CHUNK`` bytes with one event each, reused per thread
+    (``ring()``).  ``slot(i)`` is chunk i's buffer; ``done(i)`` records chunk i's transfer on
+    ``stream``; ``wait(i)`` blocks until it landed."""
+
+    def __init__(self):
+        self.chunk = RING_CHUNK
+        self.bufs = [torch.empty((RING_CHUNK,), dtype=torch.uint8, pin_memory=True) for _ in range(RING_SLOTS)]
+        self.events = [torch.cuda.Event() for _ in range(RING_SLOTS)]
+
+    def slot(self, i):
+        return self.bufs[i % RING_SLOTS]
+
+    def done(self, i, stream):
+        self.events[i % RING_SLOTS].record(stream)
+
+    def wait(self, i):
+        self.events[i % RING_SLOTS].synchronize()
+
+
+def ring(name='d2h'):
+    r = getattr(_TLS, 'ring_' + name, None)
+    if r is None or r.chunk != RING_CHUNK:
+        r = PinnedRing()
+        setattr(_TLS, 'ring_' + name, r)
+    return r
+
+
+def d2h_stream(src, sink, stream=None):
+    """Stream the device byte tensor ``src`` to the host in ``RING_CHUNK`` pieces:
+    ``sink(offset, pinned uint8 numpy view)`` is called for each piece in order, while the next
+    pieces are in flight on ``stream`` (default: the current stream of ``src``'s device)."""
+    n = src.numel()
+    s = stream or torch.cuda.current_stream(src.device)
+    r = ring('d2h')
+    nch = -(-n // RING_CHUNK)
+
+    def issue(i):
+        lo = i * RING_CHUNK
+        hi = min(n, lo + RING_CHUNK)
+        with torch.cuda.stream(s):
+            r.slot(i)[:hi - lo].copy_(src[lo:hi], non_blocking=True)
+        r.done(i, s)
+
+    for i in range(min(RING_SLOTS - 1, nch)):
+        issue(i)
+    for i in range(nch):
+        if i + RING_SLOTS - 1 < nch:
+            issue(i + RING_SLOTS - 1)  # its slot's previous chunk (i - 1) was consumed last step
+        r.wait(i)
+        lo = i * RING_CHUNK
+        sink(lo, r.slot(i)[:min(n, lo + RING_CHUNK) - lo].numpy())
+
+
+def h2d_stream(dst, source, stream=None):
+    """Fill the device byte tensor ``dst`` from the host in ``RING_CHUNK`` pieces:
+    ``source(offset, pinned uint8 numpy view)`` fills each piece and returns the bytes it wrote;
+    the piece's upload is queued on ``stream`` while the next piece is filled.  Returns the bytes
+    filled (short when ``source`` came up short)."""
+    n = dst.numel()
+    s = stream or torch.cuda.current_stream(dst.device)
+    r = ring('h2d')
+    for i in range(-(-n // RING_CHUNK)):
+        r.wait(i)  # the slot's previous upload (this call's chunk i - RING_SLOTS, or an earlier call's) landed
+        lo = i * RING_CHUNK
+        hi = min(n, lo + RING_CHUNK)
+        buf = r.slot(i)[:hi - lo]
+        got = source(lo, buf.numpy())
+        if got:
+            with torch.cuda.stream(s):
+                dst[lo:lo + got].copy_(buf[:got], non_blocking=True)
+            r.done(i, s)
+        if got != hi - lo:
+            return lo + got
+    return n
+
+
+def pread_into(fd, view, offset):
+    """``os.preadv`` of ``view.size`` bytes at ``offset`` into the numpy uint8 ``view``, split over
+    the copy threads for large views (page-cache reads of one file run in parallel); returns the
+    bytes read."""
+    n = view.size
+    k = copy_pool()._max_workers if n >= (8 << 20) else 1
+    step = -(-n // k)
+
+    def part(i):
+        lo, hi = i * step, min(n, (i + 1) * step)
+        got = 0
+        while lo + got < hi:
+            r = os.preadv(fd, [memoryview(view[lo + got:hi])], offset + lo + got)
+            if r <= 0:
+                break
+            got += r
+        return got, hi - lo
+
+    parts = list(copy_pool().map(part, range(k))) if k > 1 else [part(0)]
+    total = 0
+    for got, want in parts:
+        total += got
+        if got != want:
+            break
+    return total
 
 
 def copy_pool():
@@ -119,17 +240,18 @@ def parallel_copy(dst, src):
 
 
 def to_host(t):
-    """A device tensor as a new numpy array: pinned D2H at the link rate, then a parallel copy out of
-    the staging buffer (the result is ordinary pageable memory the caller owns)."""
+    """A device tensor as a new numpy array: pinned D2H at the link rate in ``RING_CHUNK`` pieces,
+    each copied out of its pinned chunk (in parallel) while the next pieces cross the link; the
+    result is ordinary pageable memory the caller owns.  Ordered after the work queued on the
+    current stream of ``t``'s device."""
     nbytes = t.numel() * t.element_size()
     if nbytes < _SMALL:
         return t.cpu().numpy()
     t = t.contiguous()
-    stage = pinned_staging(nbytes)
-    stage[:nbytes].copy_(t.view(-1).view(torch.uint8), non_blocking=True)
-    torch.cuda.current_stream().synchronize()
     out = np.empty(tuple(t.shape), dtype=torch.empty(0, dtype=t.dtype).numpy().dtype)
-    parallel_copy(out.reshape(-1).view(np.uint8), stage[:nbytes].numpy())
+    dst = out.reshape(-1).view(np.uint8)
+    with torch.cuda.device(t.device):
+        d2h_stream(t.view(-1).view(torch.uint8), lambda lo, piece: parallel_copy(dst[lo:lo + piece.size], piece))
     return out
 
 

@@ -62,6 +62,9 @@ _PROTOS = {
     'kmp_last_error': (ctypes.c_char_p, []),
     'kmp_last_launch': (ctypes.c_char_p, []),
     'kmp_device_ok': (ctypes.c_int, []),
+    'kmp_set_option': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    'kmp_clear_option': (ctypes.c_int, [ctypes.c_char_p]),
+    'kmp_get_option': (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     'kmp_host_device_pointer': (ctypes.c_int, [_vp, _vpp]),
     'kmp_volume_encode': (ctypes.c_int, [_i32, _vp, _i64, _i64, _i64, _i64, _i64, ctypes.POINTER(Predictor), _i32,
                                          _vp, _vpp, _i32p, ctypes.POINTER(Region), _vp, ctypes.c_size_t, _vp]),
@@ -137,6 +140,40 @@ def check(status, what):
 
 def version():
     return lib.kmp_version().decode()
+
+
+def get_option(name):
+    """A dispatch option's value, or None while it is unset."""
+    v = ctypes.c_int()
+    r = lib.kmp_get_option(name.encode(), ctypes.byref(v))
+    if r < 0:
+        check(r, 'kmp_get_option')
+    return v.value if r == 1 else None
+
+
+def set_option(name, value):
+    """Set a dispatch option (``None`` returns it to the kernel's own default)."""
+    if value is None:
+        check(lib.kmp_clear_option(name.encode()), 'kmp_clear_option')
+    else:
+        check(lib.kmp_set_option(name.encode(), int(value)), 'kmp_set_option')
+
+
+class option:
+    """``with option('KMP_DISABLE_FAST', 1): ...`` -- set a dispatch option for a block, restoring
+    its previous state after (the library reads its environment variable only once, at load)."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.prev = get_option(self.name)
+        set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.prev)
+        return False
 
 
 # ---------------------------------------------------------------------------------------------

@@ -107,14 +107,10 @@ def _bundle(x, arrays, dims, method):
 
 
 def _write(path, meta, blob, total, crc, t0):
-    """Header, metadata and the first ``total`` device bytes of ``blob`` to ``path``: one D2H into
-    the pinned staging buffer, then the file write from it."""
+    """Header, metadata and the first ``total`` device bytes of ``blob`` to ``path``: the bundle
+    crosses the link in pinned chunks (``_device.d2h_stream``), each written to the file while the
+    next ones are in flight."""
     t1 = time.perf_counter()
-    stage = dev.pinned_staging(total, 'file')
-    if total:
-        stage[:total].copy_(blob[:total], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-    t2 = time.perf_counter()
     meta = dict(meta, bundle_bytes=int(total), crc32=int(crc) & 0xffffffff)
     js = json.dumps(meta, separators=(',', ':')).encode()
     js += b' ' * (-len(js) % 8)
@@ -122,11 +118,12 @@ def _write(path, meta, blob, total, crc, t0):
     with open(tmp, 'wb') as f:
         f.write(_HEAD.pack(MAGIC, VERSION, 0, len(js)))
         f.write(js)
-        f.write(memoryview(stage[:total].numpy()))
+        if total:
+            dev.d2h_stream(blob[:total], lambda lo, piece: f.write(memoryview(piece)))
     os.replace(tmp, path)  # a reader never sees a half-written file
-    t3 = time.perf_counter()
+    t2 = time.perf_counter()
     last_timing.clear()
-    last_timing.update(device=t1 - t0, d2h=t2 - t1, write=t3 - t2, total=t3 - t0)
+    last_timing.update(device=t1 - t0, d2h_write=t2 - t1, total=t2 - t0)
     return _HEAD.size + len(js) + total
 
 
@@ -172,22 +169,28 @@ def _read(path):
         magic, version, _, mlen = _HEAD.unpack(head)
         if magic != MAGIC or version not in (1, VERSION) or mlen > (1 << 26):
             raise ValueError(f'{path}: not a kompressor_amd file (magic {magic!r}, version {version})')
-        meta = json.loads(f.read(mlen).decode())
+        try:
+            meta = json.loads(f.read(mlen).decode())
+            n = int(meta['bundle_bytes'])
+        except (ValueError, KeyError, TypeError) as e:
+            raise ValueError(f'{path}: corrupt metadata ({e})') from None
         if version == 1 and meta.get('method') != 'planes':
             # version-1 'rice' payloads were the per-array KMPR format, replaced by the v2 bundle;
             # version-1 'planes' payloads are unchanged and still read
             raise ValueError(f'{path}: a version-1 rice file (the retired per-array KMPR format): re-compress it')
-        n = int(meta['bundle_bytes'])
-        stage = dev.pinned_staging(n, 'file')
-        got = f.readinto(memoryview(stage[:n].numpy())) if n else 0
+        # the payload length is checked against the file before anything is allocated for it
+        avail = os.fstat(f.fileno()).st_size - (_HEAD.size + mlen)
+        if not 0 <= n <= avail:
+            raise ValueError(f'{path}: truncated or corrupt ({n} payload bytes recorded, {max(avail, 0)} present)')
+        # the payload: parallel page-cache reads into pinned chunks, each uploaded while the next is read
+        blob = torch.empty((max(n, 1),), dtype=torch.uint8, device='cuda')[:n]
+        fd, base = f.fileno(), _HEAD.size + mlen
+        got = dev.h2d_stream(blob, lambda lo, piece: dev.pread_into(fd, piece, base + lo)) if n else 0
     if got != n:
         raise ValueError(f'{path}: truncated ({got} of {n} payload bytes)')
     t1 = time.perf_counter()
-    blob = torch.empty((max(n, 1),), dtype=torch.uint8, device='cuda')[:n]
-    if n:
-        blob.copy_(stage[:n], non_blocking=True)
     crc = _device_crc(blob, n) if n else torch.zeros((1,), dtype=torch.int32, device='cuda')
-    return meta, blob, crc, {'read': t1 - t0, 't_upload': t1}
+    return meta, blob, crc, {'read_upload': t1 - t0, 't_upload': t1}
 
 
 def _check_crc(path, meta, crc):
@@ -273,6 +276,11 @@ def decompress(path, predictor=None, as_numpy=True):
     ndim, padding = meta['ndim'], meta['padding']
     if isinstance(pred, (MeanPredictor, LinearPredictor)) and pred.padding != padding:
         raise AssertionError(f'{path} was coded with padding {padding}; the predictor passed has {pred.padding}')
+    if isinstance(pred, LinearPredictor) and meta['predictor'] and meta['predictor'].get('kind') == 'linear':
+        # the two arithmetics are not bit-equal: decoding with the other one returns wrong samples
+        arith = meta['predictor'].get('arith', 'f32')
+        if pred.arith != arith:
+            raise AssertionError(f"{path} was coded with arith='{arith}'; the predictor passed has arith='{pred.arith}'")
     nmaps = _nd.NMAPS[ndim]
     levels = meta.get('levels') or [{'dims': list(bundle_dims)}]  # save(): one level, dims in the bundle
     if len(arrays) != nmaps * len(levels):
@@ -297,7 +305,8 @@ def decompress(path, predictor=None, as_numpy=True):
     out = dev.to_host(x) if as_numpy else x
     t3 = time.perf_counter()
     last_timing.clear()
-    last_timing.update(read=tm['read'], upload_crc=t1 - tm['t_upload'], device=t2 - t1, d2h=t3 - t2, total=t3 - t0)
+    last_timing.update(read_upload=tm['read_upload'], crc=t1 - tm['t_upload'], device=t2 - t1, d2h=t3 - t2,
+                       total=t3 - t0)
     return out
 
 

@@ -89,20 +89,18 @@ __device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, const f32x
 }
 
 // 4 MFMA results -> 4 samples of T (u8 / u16) packed little-endian in the low 4 * sizeof(T) bytes,
-// with the sample dtype's cast (XLA astype: truncate, NaN and negatives 0, saturate):
-// v_cvt_u32_f32 truncates with exactly that clamping at 0 and 2^32 - 1, v_cvt_pk_u16_u32
-// saturates a pair to 16 bits
+// with the sample dtype's cast (XLA astype: truncate, NaN and negatives 0, saturate), clamped to
+// [0, hi] first (hi = the dtype's maximum, or 0 for a result the caller wants zeroed): v_med3_f32
+// takes NaN to min3 = 0, so the float -> u32 conversion only ever sees in-range values (defined
+// C++; the same values as cast_f32 in kmp_common.h)
 template <typename T>
-__device__ __forceinline__ uint2 cast_pack4(const f32x4& v) {
+__device__ __forceinline__ uint2 cast_pack4(const f32x4& v, float hi) {
   uint32_t u[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) u[j] = (uint32_t)v[j];
+  for (int j = 0; j < 4; ++j) u[j] = (uint32_t)__builtin_amdgcn_fmed3f(v[j], 0.0f, hi);
   if constexpr (sizeof(T) == 2) {
-    return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[0], u[1])),
-                      __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u[2], u[3])));
+    return make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
   } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) u[j] = u[j] < 255u ? u[j] : 255u;
     return make_uint2(u[0] | (u[1] << 8) | (u[2] << 16) | (u[3] << 24), 0u);
   }
 }

@@ -520,7 +520,7 @@ static int window_launch(int nsp, int dtype, const void* src, int mult, const in
   return dispatch_any_dtype(dtype, [&](auto tag) {
     using T = decltype(tag);
     const int64_t src_n = B * S[0] * S[1] * S[2] * C;
-    if (C == 1 && total < ((int64_t)1 << 30) && src_n < ((int64_t)1 << 30) && !std::getenv("KMP_DISABLE_ROWS")) {
+    if (C == 1 && total < ((int64_t)1 << 30) && src_n < ((int64_t)1 << 30) && !opt(OPT_DISABLE_ROWS, 0)) {
       const int64_t nch = ceil_div(W[2], Vec16<T>::V), items = B * W[0] * W[1] * nch;
       rows_window_kernel<T><<<grid_for(items), kThreads, 0, stream>>>(
           (const T*)src, (int32_t)S[0], (int32_t)S[1], (int32_t)S[2], g, mult, nsp == 3 ? p : 0, p, (int32_t)W[0],
@@ -596,7 +596,7 @@ int kmp_encode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder,
    constexpr int CODER = decltype(coder_c)::value;
    return cb::dispatch_pred<T>(dtype, pred_dtype, [&](auto ptag) {
     using P = decltype(ptag);
-    if (small && !std::getenv("KMP_DISABLE_ROWS")) {
+    if (small && !opt(OPT_DISABLE_ROWS, 0)) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
       auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, false, 3, P> : cb::rows_code_preds_kernel<T, CODER, false, 2, P>;
@@ -652,7 +652,7 @@ int kmp_decode_with_predictions_typed(int32_t nsp, int32_t dtype, int32_t coder,
    constexpr int CODER = decltype(coder_c)::value;
    return cb::dispatch_pred<T>(dtype, pred_dtype, [&](auto ptag) {
     using P = decltype(ptag);
-    if (small && !std::getenv("KMP_DISABLE_ROWS")) {
+    if (small && !opt(OPT_DISABLE_ROWS, 0)) {
       const cb::MapExt me = cb::map_exts(g, nsp);
       const int64_t nch = ceil_div(g.E[2], Vec16<T>::V), items = B * g.E[0] * g.E[1] * nch;
       auto k = nsp == 3 ? cb::rows_code_preds_kernel<T, CODER, true, 3, P> : cb::rows_code_preds_kernel<T, CODER, true, 2, P>;

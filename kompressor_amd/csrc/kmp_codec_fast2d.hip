@@ -315,16 +315,11 @@ __global__ void __launch_bounds__(256) fast2d_kernel(F2 a) {
   }
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 template <typename T>
 static bool geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region, F2& a,
                      dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 8 / (int)sizeof(T);
-  if (env_int("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding > 2 || region) return false;
   const int P = pred->padding;
   const int64_t H = g.n[1], W = g.n[2];

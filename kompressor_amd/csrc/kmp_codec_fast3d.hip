@@ -413,17 +413,12 @@ __global__ void __launch_bounds__(1024) fast3d_kernel(F3 a) {
 // ------------------------------------------------------------------------------------------
 // Host: eligibility + launch geometry
 // ------------------------------------------------------------------------------------------
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 template <typename T>
 static bool fast3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
                             F3& a, dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (env_int("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding > 2) return false;
   const int P = pred->padding;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;

@@ -806,11 +806,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
 }  // namespace l3
 
-static int l3_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 // the y-rolling kernel serves FULL tiles whose rows split into 1, 2, 4 or 8 whole wave steps
 // (KMP_L3Y=0: the plane-block kernel, for A/B)
 // waves per SIMD: 16-bit samples 127 / 123 VGPRs (encode / decode, 4 steps fully unrolled; 8 steps
@@ -820,7 +815,7 @@ static int l3_env(const char* name, int dflt) {
 #define L3Y_W16 4
 #endif
 static int l3y_steps(const l3::L3& a) {
-  if (!a.full || a.Lcz < 1 || !l3_env("KMP_L3Y", 1)) return 0;
+  if (!a.full || a.Lcz < 1 || !opt(OPT_L3Y, 1)) return 0;
   if (a.Ey % a.rows != 0) return 0;
   const int steps = a.Ey / a.rows;
   return (steps == 1 || steps == 2 || steps == 4 || steps == 8) ? steps : 0;
@@ -831,7 +826,7 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
                               const kmp_region* region, l3::L3& a, dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (l3_env("KMP_DISABLE_FAST", 0) || l3_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR || pred->padding != 0) return false;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
@@ -854,7 +849,7 @@ static bool linear3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   a.zbegin = (int)zb; a.zend = (int)ze;
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)waves;
   const int64_t nblk = B * (ze - zb);
-  a.xcd_per = (l3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
   a.full = g.Lc[1] == g.E[1] && g.Lc[2] == g.E[2];
   lds = (size_t)(waves * l3::kXch * g.E[2]) * sizeof(uint32_t);
   grid = dim3((unsigned)nblk);

@@ -427,17 +427,12 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
 // linear predictor's generic workspace is B * cells * 19 samples)
 constexpr size_t kL3pWsBytes = 64 * 19 * sizeof(float);
 
-static int l3p_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 template <typename T>
 static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
                                const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 4;
   if (!std::is_same<T, uint16_t>::value) return false;
-  if (l3p_env("KMP_DISABLE_FAST", 0) || l3p_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR || pred->padding != 1 || !pred->weights || !pred->bias) return false;
   const int P = pred->padding;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
@@ -470,7 +465,7 @@ static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   lds = (size_t)(npl * a.nr * a.pitch + waves * l3p::kXch * g.E[2]) * sizeof(uint32_t);
   if (lds > 64 * 1024) return false;
   const int64_t nblk = B * (ze - zb);
-  a.xcd_per = (l3p_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * waves));
   return nblk < ((int64_t)1 << 31);

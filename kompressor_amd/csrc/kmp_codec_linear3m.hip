@@ -236,11 +236,10 @@ __global__ void __launch_bounds__(64) linear3m_kernel(M3 a) {
         const int i = i0 + u;
         const int ri = i / TPR, x0 = 16 * (i % TPR);
         // lane (g, m): cells x0 + 4g .. + 3 of channel chP / chQ, cast (XLA astype: truncate, NaN
-        // and negatives 0, saturate) and packed: v_cvt_u32_f32 truncates with exactly that clamping
-        // at 0 and 2^32 - 1, v_cvt_pk_u16_u32 saturates a pair to 16 bits (1.5 instructions a value)
+        // and negatives 0, saturate; bx::cast_pack4) and packed
         const int cx = x0 + 4 * g;
         auto put = [&](int ch, const bx::f32x4& d) {
-          const uint2 v = bx::cast_pack4<T>(d);
+          const uint2 v = bx::cast_pack4<T>(d, (float)std::numeric_limits<T>::max());
           T* dst = ct + ch * (CSB / SZ) + ri * EX + cx;
           if constexpr (sizeof(T) == 2) *(uint2*)dst = v;
           else *(uint32_t*)dst = v.x;
@@ -408,11 +407,6 @@ __global__ void __launch_bounds__(64) linear3m_kernel(M3 a) {
 
 }  // namespace l3m
 
-static int l3m_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 // FULL tiles (even y / x: Lcy == Ey, Lcx == Ex) with Ex in {16, 32} whose rows split into 1, 2 or 4
 // wave steps; anything else is served by the generic path with kmp_linear.hip's kernel of the same
 // predictor kind (bit-identical arithmetic)
@@ -421,7 +415,7 @@ static bool linear3m_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
                               l3m::M3& a, int& steps, dim3& grid) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (l3m_env("KMP_DISABLE_FAST", 0) || l3m_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR_MFMA || pred->padding != 0 || !pred->weights || !pred->bias) return false;
   if (g.Lc[1] != g.E[1] || g.Lc[2] != g.E[2] || g.Lc[0] < 1) return false;
   const int64_t ex = g.E[2];
@@ -445,7 +439,7 @@ static bool linear3m_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   a.Lcz = (int)g.Lc[0]; a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.zbegin = (int)zb; a.zend = (int)ze;
   const int64_t nblk = B * (ze - zb);
-  a.xcd_per = (l3m_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(ze - zb) : 0;
   grid = dim3((unsigned)nblk);
   return nblk < ((int64_t)1 << 31);
 }

@@ -100,9 +100,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   constexpr int PITCH0 = EX + P + NHR;
   constexpr int PITCH = PITCH0 + ((16 - PITCH0 % 32) + 32) % 32;
   // a wave's channel table (u16) [channel][row][x], the channel stride padded 2 banks past a
-  // multiple of 32 so that an MFMA's 16 channels (one ds_write_b64 lane group) write 32 banks
+  // multiple of 32 so that an MFMA's 16 channels (one ds_write_b64 lane group) write 32 banks, then
+  // DMY u16 where the MFMA columns that carry no channel write (each lane its own 8 bytes: no
+  // exec-mask branch around the table stores)
   constexpr int CS = ROWS * EX + 4;
-  constexpr int CT = 19 * CS;
+  constexpr int DMY = 64 * 4 + (ROWS - 1) * EX + EX / 2;
+  constexpr int CT = 19 * CS + DMY;
   constexpr uint32_t MASK = 0xffffu;
   static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
   using V = typename std::conditional<DEC, uint2, uint4>::type;
@@ -176,6 +179,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   };
 
   const int chC = kCch[m], chQ = kQch[m];
+  T* const ctw = ct + w * CT;
+  // the lane's column of the channel table (its C / Q channel, 4 cells from x0 + 4g), or its dummy slot
+  T* const ctC = chC >= 0 ? ctw + chC * CS + 4 * g : ctw + 19 * CS + 4 * lane;
+  T* const ctQ = chQ >= 0 ? ctw + chQ * CS + 4 * g : ctw + 19 * CS + 4 * lane;
+  // the lane's A-fragment origin: ring slot 0, node row Y0 + (g & 1), node column m
+  const uint32_t* const fl = st + (Y0 + (g & 1)) * PITCH + m;
 
   // ---- staging: the node row of node plane q as feature dwords into ring slot q mod 5, plus
   // the mirrored halo columns / rows this lane is the source of (lsrc1) ----
@@ -215,22 +224,21 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
 
   // ---- the channels of output plane c on the matrix cores, into the wave's channel table.  A
   // cell plane outside the tile (c - 1 < 0: Q, c >= Lcz: C) has channels 0, what the
-  // aggregation's masks want ----
-  T* ctw = ct + w * CT;
+  // aggregation's masks want: the cast's upper clamp is 0 for it ----
   auto channels = [&](int c, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC, float biasQ) {
-    const bool doC = c < a.Lcz, doQ = c >= 1;
-    // A fragment: node plane q = c - 2 + t (ring slot), node rows from staged row ry, cells x0 + m
-    int sl[NPL];
+    const float hiC = c < a.Lcz ? 65535.0f : 0.0f, hiQ = c >= 1 ? 65535.0f : 0.0f;
+    // A fragment: node plane c - 2 + t (ring slot (c - 2 + t) mod 5), staged rows Y0 + ry + (g & 1),
+    // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
+    const uint32_t* fb[NPL][2];
 #pragma unroll
-    for (int t = 0; t < NPL; ++t) sl[t] = (c - 2 + t + 2 * NPL) % NPL;
+    for (int t = 0; t < NPL; ++t) {
+      fb[t][0] = fl + ((c - 2 + t + 2 * NPL) % NPL) * (NR * PITCH);
+      fb[t][1] = fb[t][0] + 5 * PITCH;
+    }
     auto frag = [&](int t, int ry, int x0) {
-      const uint32_t* p = st + (sl[t] * NR + ry + (g & 1)) * PITCH + x0 + m;
+      const uint32_t* p = fb[t][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
     };
-    auto put = [&](int k, int row, int x0, const bx::f32x4& d) {
-      *(uint2*)(ctw + k * CS + row * EX + x0 + 4 * g) = bx::cast_pack4<T>(d);
-    };
-    const bx::f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     // tile rows by x tile, row parity, row pair: row Y's node rows 2, 3 (F1) are row Y+2's 0, 1
 #pragma unroll
     for (int xt = 0; xt < TPR; ++xt) {
@@ -238,12 +246,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       for (int par = 0; par < 2; ++par) {
         bx::u32x4 F0[NPL], F1[NPL];
 #pragma unroll
-        for (int t = 0; t < NPL; ++t) F0[t] = frag(t, Y0 + par, 16 * xt);
+        for (int t = 0; t < NPL; ++t) F0[t] = frag(t, par, 16 * xt);
 #pragma unroll
         for (int j = 0; j < ROWS / 2; ++j) {
           const int row = par + 2 * j;
 #pragma unroll
-          for (int t = 0; t < NPL; ++t) F1[t] = frag(t, Y0 + row + 2, 16 * xt);
+          for (int t = 0; t < NPL; ++t) F1[t] = frag(t, row + 2, 16 * xt);
           bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
 #pragma unroll
           for (int i = 0; i < 8; ++i) {  // chunk q (plane offset dz = q / 2, node rows 2 (q & 1) + 0 / 1)
@@ -251,8 +259,8 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
             dC = bx::mfma((q & 1) ? F1[1 + dz] : F0[1 + dz], bC[q], dC);
             dQ = bx::mfma((q & 1) ? F1[dz] : F0[dz], bQ[q], dQ);
           }
-          if (chC >= 0) put(chC, row, 16 * xt, doC ? dC : z4);
-          if (chQ >= 0) put(chQ, row, 16 * xt, doQ ? dQ : z4);
+          *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(dC, hiC);
+          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(dQ, hiQ);
 #pragma unroll
           for (int t = 0; t < NPL; ++t) F0[t] = F1[t];
         }
@@ -260,6 +268,8 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     }
   };
 
+  const T* const upt = (r > 0 ? ctw + (r - 1) * EX : w > 0 ? ctw - CT + (ROWS - 1) * EX : ctw) + X;
+  const uint32_t upm = Y > 0 ? 0xffffffffu : 0u;
   // ---- the maps / coder of output plane c from the channel table (linear3dp's aggregation):
   // channel k of the lane's cells X .. X+3 at index 1 .. 4; the row above from the table (the
   // wave above's last row for r = 0; none above row 0: zeros) ----
@@ -271,13 +281,13 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
     };
     auto rd = [&](int k, uint32_t (&v)[VX + 1]) { rd_at(ctw, k, r, v); };
+    // the row above: this wave's row r - 1, the wave above's last row, or (Y = 0) zeros by a mask
     auto rd_up = [&](int k, uint32_t (&v)[VX + 1]) {
-      if (r > 0) rd_at(ctw, k, r - 1, v);
-      else if (w > 0) rd_at(ctw - CT, k, ROWS - 1, v);
-      else {
+      uint2 u = *(const uint2*)(upt + k * CS);
+      u.x &= upm;
+      u.y &= upm;
 #pragma unroll
-        for (int i = 1; i <= VX; ++i) v[i] = 0u;
-      }
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
     };
     uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
     rd_up(3, A3);
@@ -444,11 +454,6 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
 
 }  // namespace l3q
 
-static int l3q_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 // u16 FULL tiles (Lcy == Ey, Lcx == Ex) with Ex, Ey in {16, 32}; anything else is served by the
 // generic path with kmp_linear.hip's kernel of the same predictor kind (bit-identical arithmetic)
 template <typename T>
@@ -456,7 +461,7 @@ static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
                                const kmp_region* region, l3q::PM& a, dim3& grid, dim3& block) {
   constexpr int P = l3q::P;
   if (!std::is_same<T, uint16_t>::value) return false;
-  if (l3q_env("KMP_DISABLE_FAST", 0) || l3q_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR_MFMA || pred->padding != P || !pred->weights || !pred->bias) return false;
   if (g.E[2] != 16 && g.E[2] != 32) return false;
   if (g.E[1] != 16 && g.E[1] != 32) return false;
@@ -485,7 +490,7 @@ static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   a.zper = (int)ceil_div(nz, nsplit);
   a.nsplit = (int)ceil_div(nz, a.zper);
   const int64_t nblk = B * a.nsplit;
-  a.xcd_per = (l3q_env("KMP_W3_XCD", 1) && B % 8 == 0) ? a.nsplit : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? a.nsplit : 0;
   const int rows = 64 / (a.Ex / 4);
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * (a.Ey / rows)));

@@ -381,20 +381,15 @@ __global__ void __launch_bounds__(256) wave2d_u8_dec_kernel(W2 a) {
 
 }  // namespace w2
 
-static int w2_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 template <typename T>
 static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
                             w2::W2& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (w2_env("KMP_DISABLE_WAVE", 0) || w2_env("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_WAVE, 0) || opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->padding != 0) return false;
   if (pred->kind != KMP_PRED_MEAN && !(pred->kind == KMP_PRED_LINEAR && pred->weights && pred->bias)) return false;
-  if (pred->kind == KMP_PRED_LINEAR && w2_env("KMP_DISABLE_LINEAR_FUSED", 0)) return false;
+  if (pred->kind == KMP_PRED_LINEAR && opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   int64_t yb = 0, ye = g.E[1];
   if (region) {  // only row ranges (full width): the fused chunked drivers' merged slabs
     if (region->begin[2] > 0 || region->end[2] < g.E[2]) return false;
@@ -416,7 +411,7 @@ static bool wave2d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
   a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)nwv; a.ngrp = (int)ngrp;
-  a.xcd_per = (w2_env("KMP_W2_XCD", 1) && B % 8 == 0) ? (int)ngrp : 0;
+  a.xcd_per = (opt(OPT_W2_XCD, 1) && B % 8 == 0) ? (int)ngrp : 0;
   a.ngrp_div = make_udiv((uint32_t)ngrp);
   a.ybeg = (int)yb;
   a.yend = (int)ye;
@@ -439,7 +434,7 @@ static void launch_wave2d_s(bool one, bool lin, dim3 grid, dim3 block, hipStream
     if (lin) w2::wave2d_kernel<T, DEC, false, true, STC><<<grid, block, 0, s>>>(a);
     // SWAR u8 decode: 24.0 vs 24.8 us at C2 on one box; the SWAR encode measured slower (26.2 vs
     // 25.4: bound by its row loads, not VALU) and was removed -- profiles/round1/ab_wave2d_swar.log
-    else if (DEC && std::is_same<T, uint8_t>::value && !w2_env("KMP_DISABLE_SWAR", 0))
+    else if (DEC && std::is_same<T, uint8_t>::value && !opt(OPT_DISABLE_SWAR, 0))
       w2::wave2d_u8_dec_kernel<<<grid, block, 0, s>>>(a);
     else w2::wave2d_kernel<T, DEC, false, false, STC><<<grid, block, 0, s>>>(a);
   }
@@ -448,7 +443,7 @@ static void launch_wave2d_s(bool one, bool lin, dim3 grid, dim3 block, hipStream
 // the encode's lowres / map stores cached (stp8, kmp_wave.h) unless KMP_W2_ST_ENC=0
 template <typename T, bool DEC>
 static void launch_wave2d(bool one, bool lin, dim3 grid, dim3 block, hipStream_t s, const w2::W2& a) {
-  if (!DEC && w2_env("KMP_W2_ST_ENC", 1)) launch_wave2d_s<T, DEC, true>(one, lin, grid, block, s, a);
+  if (!DEC && opt(OPT_W2_ST_ENC, 1)) launch_wave2d_s<T, DEC, true>(one, lin, grid, block, s, a);
   else launch_wave2d_s<T, DEC, false>(one, lin, grid, block, s, a);
 }
 

@@ -2,13 +2,12 @@
 // (SURVEY.md §8a a7-a12 fused for the 2D path; BASELINE config C2 geometry with p > 0).
 //
 // The image counterpart of kmp_codec_wave3dp.hip, with the access pattern of
-// kmp_codec_wave2d.hip: a workgroup owns nwv * rows consecutive output rows of one image, each wave
-// owns rows = 64 / txn of them and issues all its loads up front (its node row, one halo row on
-// the wave's first p+1 rows (above) and one on its last p+1 rows (below), and the output-only row),
-// then computes with shuffles only.  The (2p+2)^2 neighbourhood mean (image/utils.py:120-137 +
+// kmp_codec_wave2d.hip: each wave rolls down a run of output rows of one image in steps of
+// rows = 64 / txn rows (wave2dr_kernel below), with the next steps' loads in flight, and computes
+// with shuffles only.  The (2p+2)^2 neighbourhood mean (image/utils.py:120-137 +
 // tests/image/test_encode_decode.py:46-51) is a separable box sum: x over the lane's elements and
 // its neighbours' (2p+1 shuffles, mirrored in-lane at the row ends), y over the wave's rows by
-// shuffles of the x sums.  A lane may hold an "above" and a "below" halo row (rows >= p+1), so the
+// shuffles of the x sums (the rows above / below a step come from the neighbouring steps), so the
 // C2 geometry (16 lanes per row, 4 rows per wave) serves p = 2 too.  floor(sum / (2p+2)^2) ==
 // the f32 mean + truncation for u8/u16.  Aggregation onto LR / UD / C and the coder are the p = 0
 // kernel's (image/utils.py:58-86, utils.py:38-55).
@@ -36,195 +35,8 @@ struct W2P {
   int32_t rrun;   // wave2dr_kernel: output rows per wave (a multiple of rows)
 };
 
-template <typename T, bool DEC, int P, bool STC = false>
-__global__ void __launch_bounds__(256) wave2dp_kernel(W2P a) {
-  constexpr int VX = 8 / (int)sizeof(T);
-  constexpr int NB = 2 * P + 2;
-  constexpr uint32_t NN = NB * NB;
-  constexpr int NE = VX + 2 * P + 1;
-  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
-  using V = typename std::conditional<DEC, uint2, uint4>::type;
-
-  const int lane = threadIdx.x & 63;
-  const int wv_ = threadIdx.x >> 6;
-  const int tx = lane & (a.txn - 1);
-  const int r = lane >> __builtin_ctz(a.txn);
-  const int X = tx * VX;
-  int blk = (int)blockIdx.x;
-  if (a.xcd_per > 0) {
-    const int x = blk % 8, k = blk / 8;
-    blk = ((k / a.xcd_per) * 8 + x) * a.xcd_per + (k % a.xcd_per);
-  }
-  const int grp = blk % a.ngrp;
-  const int64_t b = blk / a.ngrp;
-  const int rows = a.rows;
-  const int Y0 = (a.wbase + grp * a.nwv + wv_) * rows;
-  if (Y0 >= a.Ey) return;  // whole idle wave
-  const int Y = Y0 + r;
-  const bool live = Y < a.Ey;
-  const int ysrc = live ? Y : lsrc(Y, a.Ly, a.Ey);  // rows past the end: the mirrored rows
-  const bool has_up = r <= P, has_dn = r >= rows - P - 1;
-  const int yup = lsrc(Y0 - P - 1 + r, a.Ly, a.Ey);
-  const int ydn = lsrc(Y0 + rows + (r - (rows - P - 1)), a.Ly, a.Ey);
-  const bool vy1 = Y < a.Lcy;
-  const bool vy0 = Y >= 1;
-  const bool xfirst = tx == 0, xlast = tx == a.txn - 1;
-  const bool xdims = a.Lx != a.Ex;
-
-  const int64_t himg = (int64_t)a.H * a.W;
-  const int hx = 2 * X;
-  const T* hin = DEC ? nullptr : (const T*)a.hi_in + b * himg;
-  T* hout = DEC ? (T*)a.hi_out + b * himg : nullptr;
-  const T* lin = DEC ? (const T*)a.lo_in + b * (int64_t)a.Ey * a.Ex : nullptr;
-  const int Yc = live ? Y : 0;
-  const int64_t m_lr = (b * a.Lcy + Yc) * a.Ex + X;  // LR and C maps: [B, Lcy, Ex]
-  const int64_t m_ud = (b * a.Ey + Yc) * a.Ex + X;   // UD map and lowres: [B, Ey, Ex]
-
-  // ---- every load up front ----
-  V own{}, hu{}, hd{};
-  uint4 o0 = make_uint4(0, 0, 0, 0);
-  uint2 mv[3] = {make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0)};
-  if constexpr (DEC) {
-    own = ld8c(lin + ysrc * a.Ex + X);
-    if (has_up) hu = ld8c(lin + yup * a.Ex + X);
-    if (has_dn) hd = ld8c(lin + ydn * a.Ex + X);
-    if (live && vy1) mv[0] = ld8((const T*)a.maps.p[0] + m_lr);
-    if (live) mv[1] = ld8((const T*)a.maps.p[1] + m_ud);
-    if (live && vy1) mv[2] = ld8((const T*)a.maps.p[2] + m_lr);
-  } else {
-    own = ld16c(hin + 2 * ysrc * a.W + hx);  // node row: re-read as a neighbour's halo
-    if (has_up) hu = ld16c(hin + 2 * yup * a.W + hx);
-    if (has_dn) hd = ld16c(hin + 2 * ydn * a.W + hx);
-    if (live && vy1) o0 = ld16(hin + (2 * Y + 1) * a.W + hx);
-  }
-
-  auto nodes = [&](const V& v, uint32_t (&n)[VX]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) n[i] = el8<T>(v, i);
-      else n[i] = el16<T>(v, 2 * i);
-    }
-  };
-  // x box sum: nodes X+i-P .. X+i+P+1 for the lane's VX cells
-  auto xbox = [&](const uint32_t (&z)[VX], uint32_t (&out)[VX]) __attribute__((always_inline)) {
-    uint32_t e[NE];
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const uint32_t s = shup(z[VX - P + k], 1);
-      e[k] = xfirst ? z[P - 1 - k] : s;
-    }
-#pragma unroll
-    for (int i = 0; i < VX; ++i) e[P + i] = z[i];
-#pragma unroll
-    for (int k = 0; k <= P; ++k) {
-      const uint32_t s = shdn(z[k], 1);
-      e[P + VX + k] = xlast ? (xdims ? z[VX - 1] : z[VX - 1 - k]) : s;
-    }
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int k = 0; k < NB; ++k) acc += e[i + k];
-      out[i] = acc;
-    }
-  };
-  uint32_t n[VX], xo[VX], xu[VX], xd[VX];
-  {
-    uint32_t t[VX];
-    nodes(own, n);
-    xbox(n, xo);
-    nodes(hu, t);
-    xbox(t, xu);
-    nodes(hd, t);
-    xbox(t, xd);
-  }
-  // y box sums over the virtual rows Y0 + j: cell row Y (so) and Y-1 (su).  For 8-bit samples
-  // the sums stay below 2^16 ((2p+2)^2 * 255 <= 9180), so two columns travel packed in one
-  // 32-bit word: half the cross-lane shuffles and half the adds / selects (SWAR).
-  constexpr bool SWAR = sizeof(T) == 1;
-  constexpr int VW = SWAR ? VX / 2 : VX;
-  uint32_t po[VW], pu[VW], pd[VW];
-#pragma unroll
-  for (int w = 0; w < VW; ++w) {
-    po[w] = SWAR ? (xo[2 * w] | xo[2 * w + 1] << 16) : xo[w];
-    pu[w] = SWAR ? (xu[2 * w] | xu[2 * w + 1] << 16) : xu[w];
-    pd[w] = SWAR ? (xd[2 * w] | xd[2 * w + 1] << 16) : xd[w];
-  }
-  uint32_t so[VW], su[VW];
-#pragma unroll
-  for (int w = 0; w < VW; ++w) so[w] = su[w] = 0;
-#pragma unroll
-  for (int d = -P - 1; d <= P + 1; ++d) {
-    const int j = r + d;
-#pragma unroll
-    for (int w = 0; w < VW; ++w) {
-      uint32_t v = d == 0 ? po[w] : (d < 0 ? shup(po[w], -d * a.txn) : shdn(po[w], d * a.txn));
-      if (d < 0) {
-        const uint32_t h = d == -P - 1 ? pu[w] : shdn(pu[w], (d + P + 1) * a.txn);
-        v = j < 0 ? h : v;
-      } else if (d > 0) {
-        const uint32_t h = d == P + 1 ? pd[w] : shup(pd[w], (P + 1 - d) * a.txn);
-        v = j >= rows ? h : v;
-      }
-      if (d >= -P) so[w] += v;
-      if (d <= P) su[w] += v;
-    }
-  }
-  uint32_t M1[VX + 1], M0[VX + 1];  // cell rows Y / Y-1, cols X-1 .. X+VX-1
-#pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    const uint32_t o = SWAR ? (so[i / 2] >> (16 * (i & 1))) & 0xffffu : so[i];
-    const uint32_t u = SWAR ? (su[i / 2] >> (16 * (i & 1))) & 0xffffu : su[i];
-    M1[i + 1] = o / NN;
-    M0[i + 1] = u / NN;
-  }
-  M1[0] = shup(M1[VX], 1);
-  M0[0] = shup(M0[VX], 1);
-  if (!live || Y < a.ybeg || Y >= a.yend) return;
-
-  bool vx[VX + 1];
-  cells_valid<VX>(vx, X, a.Lcx);
-  const uint32_t ny = (uint32_t)vy0 + (uint32_t)vy1;
-#pragma unroll
-  for (int q = 0; q <= VX; ++q) {
-    M1[q] = (vy1 && vx[q]) ? M1[q] : 0u;
-    M0[q] = (vy0 && vx[q]) ? M0[q] : 0u;
-  }
-  uint32_t pred[3][VX];  // LR, UD, C
-#pragma unroll
-  for (int i = 0; i < VX; ++i) {
-    const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
-    pred[0][i] = (M1[i] + M1[i + 1]) >> (nx >> 1);      // LR: cells (Y, x-1), (Y, x)
-    pred[1][i] = (M0[i + 1] + M1[i + 1]) >> (ny >> 1);  // UD: cells (Y-1, x), (Y, x)
-    pred[2][i] = M1[i + 1];                             // C
-  }
-  if constexpr (!DEC) {
-    uint32_t lov[VX], res[3][VX];
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      lov[i] = n[i];
-      res[0][i] = (el16<T>(o0, 2 * i) - pred[0][i]) & MASK;       // LR (1,0)
-      res[1][i] = (el16<T>(own, 2 * i + 1) - pred[1][i]) & MASK;  // UD (0,1)
-      res[2][i] = (el16<T>(o0, 2 * i + 1) - pred[2][i]) & MASK;   // C  (1,1)
-    }
-    stp8<STC>((T*)a.lo_out + m_ud, pack8<T, VX>(lov));
-    if (vy1) stp8<STC>((T*)a.maps.p[0] + m_lr, pack8<T, VX>(res[0]));
-    stp8<STC>((T*)a.maps.p[1] + m_ud, pack8<T, VX>(res[1]));
-    if (vy1) stp8<STC>((T*)a.maps.p[2] + m_lr, pack8<T, VX>(res[2]));
-  } else {
-    uint32_t dv[3][VX];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int i = 0; i < VX; ++i) dv[k][i] = (pred[k][i] + el8<T>(mv[k], i)) & MASK;
-    T* h0 = hout + 2 * Y * a.W + hx;
-    st16(h0, pack16<T, VX>(n, dv[1]));                    // row 2Y: lowres | UD
-    if (vy1) st16(h0 + a.W, pack16<T, VX>(dv[0], dv[2]));  // row 2Y+1: LR | C
-  }
-}
-
-// ---- y-rolling variant: a wave owns a run of a.rrun consecutive output rows (steps of ``rows``
-// rows, full width) instead of one row group.  The x box sums of a step's node rows are computed
+// ---- the y-rolling kernel: a wave owns a run of a.rrun consecutive output rows (steps of ``rows``
+// rows, full width).  The x box sums of a step's node rows are computed
 // once and serve three steps: as the current rows, as the previous step's rows (the p+1 rows
 // above come from them by one shuffle instead of a halo load) and as the next step's rows (the
 // p+1 rows below).  So a step loads one node row and its output rows per lane, against the
@@ -458,28 +270,19 @@ __global__ void __launch_bounds__(256) wave2dr_kernel(W2P a) {
 
 }  // namespace w2p
 
-static int w2p_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
-// y-rolling kernel (wave2dr_kernel): output rows per wave, 0 = the row-group kernel; rounded up to
-// a multiple of the wave's rows.  Default 32 (C2 p = 1: 33.5 / 31.4 -> 28.4 / 28.1 us per
-// direction, profiles/round2/ab_wave2dr.log); runs of 8 steps take the unrolled form (C2 p = 1
+// y-rolling kernel (wave2dr_kernel): 32 output rows per wave, rounded up to a multiple of the wave's
+// rows (C2 p = 1: 33.5 / 31.4 -> 28.4 / 28.1 us per direction against the row-group kernel it
+// replaced, profiles/round2/ab_wave2dr.log); runs of 8 steps take the unrolled form (C2 p = 1
 // 28.5 / 26.0 -> 27.0-28.2 / 24.7-25.7 us, p = 2 32.2 / 29.5 -> 31.3-31.7 / 27.8-28.8 us by
-// rocprofv3, profiles/round4/ab_wave2dr_unroll_r4w.log).  KMP_W2R_RUN overrides.
-static int w2p_run(int P, int bytes) {
-  (void)P;
-  (void)bytes;
-  return w2p_env("KMP_W2R_RUN", 32);
-}
+// rocprofv3, profiles/round4/ab_wave2dr_unroll_r4w.log)
+constexpr int kW2Run = 32;
 
 template <typename T>
 static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
                              const kmp_region* region, int run, w2p::W2P& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (w2p_env("KMP_DISABLE_WAVE", 0) || w2p_env("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_WAVE, 0) || opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding < 1 || pred->padding > 2) return false;
   const int P = pred->padding;
   int64_t yb = 0, ye = g.E[1];
@@ -497,11 +300,10 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   if (rows < P + 1) return false;  // an "above" and a "below" halo row per lane at most
   // only the waves covering the region's rows are launched
   int64_t w0 = yb / rows, w1 = ceil_div(ye, rows);
-  if (run > 0) {  // rolling: runs of ``run`` rows from the region's first row
-    run = (int)(ceil_div(run, rows) * rows);
-    w0 = 0;
-    w1 = ceil_div(ye - yb, (int64_t)run);
-  }
+  // runs of ``run`` rows from the region's first row
+  run = (int)(ceil_div(run, rows) * rows);
+  w0 = 0;
+  w1 = ceil_div(ye - yb, (int64_t)run);
   const int64_t waves = w1 - w0;
   const int64_t nwv = waves < 4 ? waves : 4;
   const int64_t ngrp = ceil_div(waves, nwv);
@@ -510,7 +312,7 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   a.Ey = (int)g.E[1]; a.Ex = (int)g.E[2];
   a.Lcy = (int)g.Lc[1]; a.Lcx = (int)g.Lc[2];
   a.txn = (int)txn; a.rows = (int)rows; a.nwv = (int)nwv; a.ngrp = (int)ngrp;
-  a.xcd_per = (w2p_env("KMP_W2_XCD", 1) && B % 8 == 0) ? (int)ngrp : 0;
+  a.xcd_per = (opt(OPT_W2_XCD, 1) && B % 8 == 0) ? (int)ngrp : 0;
   a.ybeg = (int)yb;
   a.yend = (int)ye;
   a.wbase = (int)w0;
@@ -523,18 +325,13 @@ static bool wave2dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
 
 template <typename T, bool DEC, bool STC>
 static void launch_wave2dp_s(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
-  if (a.rrun > 0) {
-    if (a.rrun == 8 * a.rows && a.Lcy >= 1 && a.Ly >= a.rrun + a.rows) {  // C2: runs of 32 rows, 4 per step
-      if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC, 8><<<grid, block, 0, s>>>(a);
-      else w2p::wave2dr_kernel<T, DEC, 2, STC, 8><<<grid, block, 0, s>>>(a);
-      return;
-    }
-    if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
-    else w2p::wave2dr_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
+  if (a.rrun == 8 * a.rows && a.Lcy >= 1 && a.Ly >= a.rrun + a.rows) {  // C2: runs of 32 rows, 4 per step
+    if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC, 8><<<grid, block, 0, s>>>(a);
+    else w2p::wave2dr_kernel<T, DEC, 2, STC, 8><<<grid, block, 0, s>>>(a);
     return;
   }
-  if (P == 1) w2p::wave2dp_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
-  else w2p::wave2dp_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
+  if (P == 1) w2p::wave2dr_kernel<T, DEC, 1, STC><<<grid, block, 0, s>>>(a);
+  else w2p::wave2dr_kernel<T, DEC, 2, STC><<<grid, block, 0, s>>>(a);
 }
 
 // the encode's lowres / map stores: cached (MALL-allocating, stp8 in kmp_wave.h; alternating pairs at
@@ -542,7 +339,7 @@ static void launch_wave2dp_s(int P, dim3 grid, dim3 block, hipStream_t s, const 
 // KMP_W2P_ST_ENC=0 (non-temporal)
 template <typename T, bool DEC>
 static void launch_wave2dp(int P, dim3 grid, dim3 block, hipStream_t s, const w2p::W2P& a) {
-  if (!DEC && w2p_env("KMP_W2P_ST_ENC", 1)) launch_wave2dp_s<T, DEC, true>(P, grid, block, s, a);
+  if (!DEC && opt(OPT_W2P_ST_ENC, 1)) launch_wave2dp_s<T, DEC, true>(P, grid, block, s, a);
   else launch_wave2dp_s<T, DEC, false>(P, grid, block, s, a);
 }
 
@@ -552,7 +349,7 @@ int try_wave2dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w2p::W2P a{};
     dim3 grid, block;
-    if (!wave2dp_geometry<T>(g, B, C, pred, region, w2p_run(pred->padding, (int)sizeof(T)), a, grid, block))
+    if (!wave2dp_geometry<T>(g, B, C, pred, region, kW2Run, a, grid, block))
       return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 3; ++k)
@@ -561,7 +358,7 @@ int try_wave2dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
     a.lo_out = lowres;
     a.maps = maps;
     launch_wave2dp<T, false>(pred->padding, grid, block, stream, a);
-    return check_launch(a.rrun > 0 ? "wave2dr_encode" : "wave2dp_encode");
+    return check_launch("wave2dr_encode");
   }
   return KMP_ERR_UNSUPPORTED;
 }
@@ -572,7 +369,7 @@ int try_wave2dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w2p::W2P a{};
     dim3 grid, block;
-    if (!wave2dp_geometry<T>(g, B, C, pred, region, w2p_run(pred->padding, (int)sizeof(T)), a, grid, block))
+    if (!wave2dp_geometry<T>(g, B, C, pred, region, kW2Run, a, grid, block))
       return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 3; ++k) {
@@ -582,7 +379,7 @@ int try_wave2dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
     a.hi_out = hi;
     a.lo_in = lowres;
     launch_wave2dp<T, true>(pred->padding, grid, block, stream, a);
-    return check_launch(a.rrun > 0 ? "wave2dr_decode" : "wave2dp_decode");
+    return check_launch("wave2dr_decode");
   }
   return KMP_ERR_UNSUPPORTED;
 }

@@ -378,17 +378,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ------------------------------------------------------------------------------------------
 // Host: eligibility + launch geometry
 // ------------------------------------------------------------------------------------------
-static int w3_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 template <typename T>
 static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, const kmp_region* region,
                             int pl, w3::W3& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (w3_env("KMP_DISABLE_WAVE", 0) || w3_env("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_WAVE, 0) || opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0) return false;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;  // 32-bit offsets inside a tile
@@ -418,7 +413,7 @@ static bool wave3d_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predic
   a.slab = pl;
   a.nslab = (int)nslab;
   const int64_t nblk = B * nslab * nyg;
-  a.xcd_per = (w3_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
   a.nt_nodes = 0;
   a.nB = B;
   a.nvblk = (int)nblk;
@@ -444,7 +439,7 @@ static void launch_wave3d_s(int pl, dim3 grid, dim3 block, hipStream_t stream, c
 template <typename T, bool DEC>
 static void launch_wave3d(int pl, dim3 grid, dim3 block, hipStream_t stream, const w3::W3& a) {
   // non-temporal stores in both directions; KMP_W3_ST_ENC=1: the encode's cached (stp8)
-  if (!DEC && w3_env("KMP_W3_ST_ENC", 0)) launch_wave3d_s<T, DEC, true>(pl, grid, block, stream, a);
+  if (!DEC && opt(OPT_W3_ST_ENC, 0)) launch_wave3d_s<T, DEC, true>(pl, grid, block, stream, a);
   else launch_wave3d_s<T, DEC, false>(pl, grid, block, stream, a);
 }
 
@@ -454,7 +449,7 @@ int try_wave3d_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w3::W3 a{};
     dim3 grid, block;
-    const int pl = w3_env("KMP_W3_PL", 2) == 1 ? 1 : 2;
+    const int pl = opt(OPT_W3_PL, 2) == 1 ? 1 : 2;
     if (!wave3d_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
@@ -474,7 +469,7 @@ int try_wave3d_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64
   if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     w3::W3 a{};
     dim3 grid, block;
-    const int pl = w3_env("KMP_W3_PL", 2) == 1 ? 1 : 2;
+    const int pl = opt(OPT_W3_PL, 2) == 1 ? 1 : 2;
     if (!wave3d_geometry<T>(g, B, C, pred, region, pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {

@@ -309,11 +309,6 @@ __global__ void __launch_bounds__(256) wave3d32_kernel(W32 a) {
 
 }  // namespace w32
 
-static int w32_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 constexpr int kW32PL = 2;
 
 template <typename T>
@@ -321,7 +316,7 @@ static bool wave3d32_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
                               const kmp_region* region, w32::W32& a, dim3& grid, dim3& block) {
   constexpr int VX = 2;
   if (!(std::is_same<T, uint32_t>::value || std::is_same<T, int32_t>::value)) return false;
-  if (w32_env("KMP_DISABLE_WAVE", 0) || w32_env("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_WAVE, 0) || opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding != 0) return false;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
@@ -349,7 +344,7 @@ static bool wave3d32_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pred
   const int64_t nslab = ceil_div(ze - zb, (int64_t)kW32PL);
   a.nslab = (int)nslab;
   const int64_t nblk = B * nslab * nyg;
-  a.xcd_per = (w32_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);

@@ -607,18 +607,13 @@ wave3dr_kernel(W3P a) {
 // ------------------------------------------------------------------------------------------
 // Host: eligibility + launch geometry
 // ------------------------------------------------------------------------------------------
-static int w3p_env(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-
 // Output planes per workgroup and register budget, per (p, direction): the measured optimum at C3
 // (profiles/round1/w3p_sweep.log; 64^3 u16 tiles): p = 1 PL 2 (decode at 4 waves / SIMD),
 // p = 2 encode PL 1, decode PL 2 at 3 waves / SIMD.  KMP_W3P_PL overrides the planes.
 static void w3p_cfg(int P, bool dec, int& pl, int& wpe) {
   pl = (P == 2 && !dec) ? 1 : 2;
   wpe = dec ? (P == 1 ? 4 : 3) : 1;
-  pl = w3p_env("KMP_W3P_PL", pl) == 1 ? 1 : 2;
+  pl = opt(OPT_W3P_PL, pl) == 1 ? 1 : 2;
 }
 
 template <typename T>
@@ -626,7 +621,7 @@ static bool wave3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
                              const kmp_region* region, int pl, w3p::W3P& a, dim3& grid, dim3& block) {
   constexpr int VX = 8 / (int)sizeof(T);
   if (!(std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value)) return false;
-  if (w3p_env("KMP_DISABLE_WAVE", 0) || w3p_env("KMP_DISABLE_FAST", 0)) return false;
+  if (opt(OPT_DISABLE_WAVE, 0) || opt(OPT_DISABLE_FAST, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_MEAN || pred->padding < 1 || pred->padding > 2) return false;
   const int P = pred->padding;
   if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
@@ -655,32 +650,28 @@ static bool wave3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predi
   const int64_t nslab = ceil_div(ze - zb, (int64_t)pl);
   a.nslab = (int)nslab;
   const int64_t nblk = B * nslab * nyg;
-  a.xcd_per = (w3p_env("KMP_W3_XCD", 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
+  a.xcd_per = (opt(OPT_W3_XCD, 1) && B % 8 == 0) ? (int)(nslab * nyg) : 0;
   grid = dim3((unsigned)nblk);
   block = dim3((unsigned)(64 * nwv));
   return nblk < ((int64_t)1 << 31);
 }
 
-// z-rolling kernel (wave3dr_kernel): the z run per workgroup in output planes, 0 = the plane-block
-// kernel.  Default: runs of 8 for p = 2 with 16-bit samples (C3: 151 / 127 -> 124 / 108 us per
-// direction, profiles/round2/ab_wave3dr.log); the plane-block kernel stays faster for p = 1 (91 /
-// 91 vs 112 / 106) and for 8-bit samples the rolling form is untuned.  KMP_W3P_ROLL overrides.
-static int w3p_roll(int P, int bytes) {
-  const int zr = w3p_env("KMP_W3P_ROLL", P == 2 && bytes == 2 ? 8 : 0);
-  return zr >= 2 ? (zr + 1) / 2 * 2 : 0;
-}
+// z-rolling kernel (wave3dr_kernel): runs of 8 output planes per workgroup for p = 2 with 16-bit
+// samples (C3: 151 / 127 -> 124 / 108 us per direction, profiles/round2/ab_wave3dr.log); 0 = the
+// plane-block kernel, which stays faster for p = 1 (91 / 91 vs 112 / 106) and serves 8-bit samples
+static int w3p_roll(int P, int bytes) { return P == 2 && bytes == 2 ? 8 : 0; }
 
 // the encode's lowres / map stores, chosen on the pipelines that follow an encode at C3
 // (tools/pipeline_rows.py, profiles/round3/pipeline_store_policy_r3.log; DESIGN §5 "pipeline"):
 // p = 1 non-temporal (encodes back to back 103 -> 91 us, encode -> Rice pack and Rice unpack ->
 // decode within 1-4 us either way); p = 2 cached, MALL-allocating (stp8 in kmp_wave.h: back to back
 // the same, encode -> Rice pack -13 us, encode -> decode -35 us).  KMP_W3P_ST_ENC=0 / 1 forces one
-static bool w3p_stc(bool dec, int P) { return !dec && w3p_env("KMP_W3P_ST_ENC", P == 2 ? 1 : 0); }
+static bool w3p_stc(bool dec, int P) { return !dec && opt(OPT_W3P_ST_ENC, P == 2 ? 1 : 0); }
 
 template <typename T, bool DEC, bool STC>
 static void launch_wave3dr_s(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {
-  if (P == 1) w3p::wave3dr_kernel<T, DEC, 1, STC><<<grid, block, 0, stream>>>(a);
-  else w3p::wave3dr_kernel<T, DEC, 2, STC><<<grid, block, 0, stream>>>(a);
+  (void)P;  // p = 2 only (w3p_roll)
+  w3p::wave3dr_kernel<T, DEC, 2, STC><<<grid, block, 0, stream>>>(a);
 }
 template <typename T, bool DEC>
 static void launch_wave3dr(int P, dim3 grid, dim3 block, hipStream_t stream, const w3p::W3P& a) {

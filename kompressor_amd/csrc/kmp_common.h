@@ -46,6 +46,18 @@ __device__ __forceinline__ void dcheck_span(const T* base, const T* p, int64_t c
 }
 #define KMP_SPAN(base, p, cnt, n) ::kmp::dcheck_span((base), (p), (int64_t)(cnt), (int64_t)(n), __LINE__)
 
+// ------------------------------------------------------------------------------------------
+// Dispatch options (kmp_set_option): one table per process, seeded from the
+// environment once at load (kmp_options.hip); a launch reads it with one relaxed atomic load.
+// ------------------------------------------------------------------------------------------
+enum Opt {
+  OPT_DISABLE_WAVE, OPT_DISABLE_FAST, OPT_DISABLE_LINEAR_FUSED, OPT_DISABLE_ROWS, OPT_DISABLE_SWAR,
+  OPT_W3_PL, OPT_W3P_PL, OPT_W3_XCD, OPT_W2_XCD, OPT_W3_ST_ENC, OPT_W3P_ST_ENC, OPT_W2_ST_ENC,
+  OPT_W2P_ST_ENC, OPT_L3Y, OPT_COUNT
+};
+// the option's value, or ``dflt`` while it is unset
+int opt(Opt id, int dflt);
+
 #define KMP_REQUIRE(cond, msg)                                         \
   do {                                                                 \
     if (!(cond)) return ::kmp::fail(KMP_ERR_ARG, std::string(__func__) + ": " + (msg)); \

@@ -1292,11 +1292,7 @@ static inline int64_t vol(int64_t B, const Ext3& e, int64_t C) { return B * e.e[
 
 // the row kernels serve C == 1 arrays below 2^30 elements (KMP_DISABLE_ROWS=1: element kernels)
 static bool rows_ok(int64_t C, std::initializer_list<int64_t> counts) {
-  static const bool off = [] {
-    const char* v = std::getenv("KMP_DISABLE_ROWS");
-    return v && std::atoi(v);
-  }();
-  return !off && C == 1 && fits32(counts);
+  return !opt(OPT_DISABLE_ROWS, 0) && C == 1 && fits32(counts);
 }
 static inline E3<int32_t> e32(const Ext3& x) { return e3<int32_t>(x); }
 template <typename T>
@@ -1582,15 +1578,14 @@ static int mean_predict_maps_impl(int32_t nsp, int32_t dtype, int32_t out_dtype,
       const int64_t plane = S.e[1] * S.e[2];
       // PPB output planes per workgroup: 2 where its LDS fits (the cell plane between the two output
       // planes summed once: p = 0 101 -> 94 us, p = 1 300 -> 270 us at 512 C3 windows,
-      // profiles/round2/ab_mean_predict_ppb.log), else 1; KMP_MP_PPB=1 forces one
+      // profiles/round2/ab_mean_predict_ppb.log), else 1 (e.g. the C3 window at p = 2)
       auto lds_for = [&](int q, int64_t& nb_, int64_t& xs_) {
         nb_ = 16 * (ceil_div((2 * padding + 2 + q) * plane * (int64_t)sizeof(T), 16) + 1);
         xs_ = padding > 0 ? 4 * (2 * padding + 2 + q) * S.e[1] * cells.e[2] : 0;
         return nb_ + xs_ + 4 * (q + 1) * cells.e[1] * cells.e[2] + 8 * mp_pad_words(cells.e[2]);
       };
-      const char* ppb_env = std::getenv("KMP_MP_PPB");
       int64_t nodes_bytes = 0, xs_bytes = 0;
-      int ppb = ppb_env && std::atoi(ppb_env) == 1 ? 1 : 2;
+      int ppb = 2;
       int64_t lds_plane = lds_for(ppb, nodes_bytes, xs_bytes);
       if (ppb == 2 && lds_plane > 64 * 1024) {
         ppb = 1;

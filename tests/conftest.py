@@ -45,3 +45,20 @@ def kom():
 def ramp(shape, max_value, dtype):
     # tests/volume/test_encode_decode.py:39-41
     return (np.arange(np.prod(shape)).reshape(shape) % max_value).astype(dtype)
+
+
+@pytest.fixture
+def kmp_opt(kom):
+    """``kmp_opt('KMP_DISABLE_FAST', 1)``: set a library dispatch option for this test (the library
+    reads its environment once, at load; ``None`` = the kernel's default); restored after."""
+    from kompressor_amd import _lib
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = _lib.get_option(name)
+        _lib.set_option(name, value)
+
+    yield set_
+    for name, value in saved.items():
+        _lib.set_option(name, value)

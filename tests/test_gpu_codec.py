@@ -37,11 +37,10 @@ def _assert_encoded(g, lowres, maps, dims, ndim):
 
 
 @pytest.fixture(params=['fast', 'generic'])
-def kernel_mode(request, monkeypatch):
+def kernel_mode(request, kmp_opt):
     # 'fast' lets the C layer pick the one-pass kernel where eligible; 'generic' forces the
     # two-pass kernels (kmp_codec_generic.hip) for every shape.
-    if request.param == 'generic':
-        monkeypatch.setenv('KMP_DISABLE_FAST', '1')
+    kmp_opt('KMP_DISABLE_FAST', 1 if request.param == 'generic' else None)
     return request.param
 
 
@@ -167,16 +166,13 @@ def float_predictions_fn(kom, padding, ndim, seen, special=True):
 @pytest.mark.parametrize('name', ['vol_rand_mixed_p1', 'vol_ramp_odd_p0', 'vol_rand_u8_c3_p1', 'vol_ramp_i32_raw_p0',
                                   'img_rand_p2', 'img_ramp_even_p1', 'img_rand_u16_c2_p1', 'vol_tile_small_p0'])
 @pytest.mark.parametrize('rows', ['1', '0'])
-def test_callback_float32_predictions(kom, name, rows, monkeypatch):
+def test_callback_float32_predictions(kom, name, rows, kmp_opt):
     """A predictions_fn returning float32 maps (what a trained network gives) with the built-in coder
     stays on the fused callback coder (kmp_*_with_predictions_typed): residuals bit-exact to the
     oracle's step sequence on the same maps (the coder reads jnp.int32(pred): truncating, saturating,
     NaN -> 0), and lossless.  rows=0: the per-element kernel instead of the 16-byte row kernel."""
     import oracle
-    if rows == '0':
-        monkeypatch.setenv('KMP_DISABLE_ROWS', '1')
-    else:
-        monkeypatch.delenv('KMP_DISABLE_ROWS', raising=False)
+    kmp_opt('KMP_DISABLE_ROWS', 1 if rows == '0' else None)
     g = load_golden(name)
     ndim, p = int(g['ndim']), int(g['padding'])
     ns, ons = _ns(kom, ndim), (oracle.volume if ndim == 3 else oracle.image)
@@ -547,20 +543,18 @@ def _last_launch(kom):
     ((2, 7, 5, 32, 1), np.uint16, 2),      # odd height, rows beyond the volume
     ((1, 64, 64, 64, 1), np.uint16, 2),
 ])
-@pytest.mark.parametrize('pl', [None, '1', '2', 'roll8', 'roll16'])
-def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, monkeypatch):
+@pytest.mark.parametrize('pl', [None, '1', '2'])
+def test_wave_p12_matches_oracle(kom, shape, dtype, p, pl, kmp_opt):
     """The p = 1, 2 wave kernels (kmp_codec_wave3dp.hip) against the oracle, encode and decode, and
-    chunked (z-region) launches: the plane-block kernel at the default and both forced
-    planes-per-workgroup, and the z-rolling kernel with runs of 8 and 16 planes (KMP_W3P_ROLL);
-    asserts the kernel served the call."""
+    chunked (z-region) launches: the default kernel per (p, dtype) -- the z-rolling kernel (runs of
+    8 planes) for p = 2 with 16-bit samples, else the plane-block kernel -- and the plane-block
+    kernel's two planes-per-workgroup forms (KMP_W3P_PL, where it serves); asserts the kernel served
+    the call."""
     kernel = 'wave3dr' if p == 2 and dtype == np.uint16 else 'wave3dp'  # the default per (p, dtype)
-    if pl is not None and pl.startswith('roll'):
-        monkeypatch.setenv('KMP_W3P_ROLL', pl[4:])
-        kernel = 'wave3dr'
-    elif pl is not None:
-        monkeypatch.setenv('KMP_W3P_PL', pl)
-        monkeypatch.setenv('KMP_W3P_ROLL', '0')
-        kernel = 'wave3dp'
+    if pl is not None:
+        if kernel == 'wave3dr':
+            pytest.skip('KMP_W3P_PL applies to the plane-block kernel')
+        kmp_opt('KMP_W3P_PL', int(pl))
     import oracle
     from oracle import predictors as OP
     ns, ons = kom.volume, oracle.volume
@@ -602,14 +596,10 @@ def _W2P_DEFAULT(p, dtype):
     ((2, 141, 256, 1), np.uint8, 2),
     ((2, 142, 128, 1), np.uint16, 1),    # 16-bit, 4 rows per wave, unrolled, partial last run
 ])
-@pytest.mark.parametrize('run', [None, '0', '8', '12', '64'])
-def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
-    """The p = 1, 2 image wave kernels (kmp_codec_wave2dp.hip) against the oracle, whole-image and
-    row-region (chunked) launches: the row-group kernel and the y-rolling kernel with runs of 8, 12
-    and 64 rows per wave (KMP_W2R_RUN, rounded up to the wave's rows); asserts which kernel served
-    the call."""
-    if run is not None:
-        monkeypatch.setenv('KMP_W2R_RUN', run)
+def test_wave2d_p12_matches_oracle(kom, shape, dtype, p):
+    """The p = 1, 2 image wave kernel (kmp_codec_wave2dp.hip: y-rolling, runs of 32 rows per wave,
+    the unrolled form where the run is 8 steps) against the oracle, whole-image and row-region
+    (chunked) launches; asserts which kernel served the call."""
     import oracle
     from oracle import predictors as OP
     ns, ons = kom.image, oracle.image
@@ -620,7 +610,7 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
     pred = kom.MeanPredictor(p, 2)
     lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
     wave = (shape[2] // 2 // (8 // np.dtype(dtype).itemsize)) in (1, 2, 4, 8, 16, 32, 64)
-    kern = _W2P_DEFAULT(p, dtype) if run is None else ('wave2dp' if run == '0' else 'wave2dr')
+    kern = _W2P_DEFAULT(p, dtype)
     assert _last_launch(kom) == (kern + '_encode' if wave else 'fast2d_encode')
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, b) in enumerate(zip(maps, want_maps)):
@@ -642,11 +632,11 @@ def test_wave2d_p12_matches_oracle(kom, shape, dtype, p, run, monkeypatch):
     (1, 40, 1024, 1),      # 64 lanes per row: the one-row wave (generic kernel only)
 ])
 @pytest.mark.parametrize('mode', ['swar_dec', 'generic'])
-def test_wave2d_u8_p0_matches_oracle(kom, shape, mode, monkeypatch):
+def test_wave2d_u8_p0_matches_oracle(kom, shape, mode, kmp_opt):
     """The p = 0 uint8 image kernels of kmp_codec_wave2d.hip -- the SWAR decode (the default) and
     the generic per-cell form (KMP_DISABLE_SWAR) -- against the oracle, whole-image and chunked."""
     if mode == 'generic':
-        monkeypatch.setenv('KMP_DISABLE_SWAR', '1')
+        kmp_opt('KMP_DISABLE_SWAR', 1)
     import oracle
     from oracle import predictors as OP
     ns, ons = kom.image, oracle.image
@@ -721,13 +711,13 @@ def test_trace_ranges_do_not_change_results(kom, monkeypatch):
     ('KMP_W2P_ST_ENC', (3, 40, 128, 1), np.uint16, 2, 'wave2d'),
 ])
 @pytest.mark.parametrize('cached', ['0', '1'])
-def test_encode_store_policy_is_output_neutral(kom, case, cached, monkeypatch):
+def test_encode_store_policy_is_output_neutral(kom, case, cached, kmp_opt):
     """The encode kernels' lowres / map stores are cached (MALL-allocating) or non-temporal
     (KMP_*_ST_ENC = 1 / 0, INTEGRATION.md knobs; the defaults per kernel and padding were chosen on
     the pipeline rows): both policies give the oracle's bytes and a lossless decode, and
     the wave kernel family served the call."""
     knob, shape, dtype, p, family = case
-    monkeypatch.setenv(knob, cached)
+    kmp_opt(knob, int(cached))
     import oracle
     from oracle import predictors as OP
     ndim = len(shape) - 2

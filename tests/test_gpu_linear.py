@@ -229,7 +229,7 @@ def test_linear_bf16x2_rejects_32bit_samples(kom):
         kom.volume.encode(pred, kom.volume.encode_values_raw, hi)
 
 
-def test_linear_bf16x2_p1_fused_sweep(kom, monkeypatch):
+def test_linear_bf16x2_p1_fused_sweep(kom):
     """Seeded sweep of fused-eligible p = 1 volumes (u16, 16 / 32-wide rows and planes, any depth,
     batch sizes that do and do not take the XCD order, smooth and full-range data, chunked regions):
     linear3pm's lowres + maps equal the generic bf16x2 path's bit for bit (KMP_DISABLE_LINEAR_FUSED),
@@ -251,8 +251,7 @@ def test_linear_bf16x2_p1_fused_sweep(kom, monkeypatch):
         assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_encode', (B, D, H, W)
         chunk = int(rng.integers(4, 12))
         lo_c, (maps_c, _) = V.encode_chunks(pred, V.encode_values_uint16, hi_t, chunk=chunk, padding=1)
-        with monkeypatch.context() as mp:
-            mp.setenv('KMP_DISABLE_LINEAR_FUSED', '1')
+        with kom._lib.option('KMP_DISABLE_LINEAR_FUSED', 1):
             lo_g, (maps_g, _) = V.encode(pred, V.encode_values_uint16, hi_t, padding=1)
             assert kom._lib.lib.kmp_last_launch().decode() == 'encode_generic'
         assert torch.equal(lo, lo_g) and torch.equal(lo_c, lo_g)

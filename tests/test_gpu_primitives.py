@@ -136,30 +136,19 @@ def _mp_lds_bytes(window_shape, itemsize, padding, q):
                                          ((16, 17, 12, 32, 1), np.uint8)])  # B % 8 == 0, odd plane count
 @pytest.mark.parametrize('padding', [0, 1, 2])
 def test_mean_predictor_plane_kernel(kom, shape, dtype, padding):
-    """The LDS-staged mean predictor (3D, C == 1): two output planes per workgroup by default where
-    the LDS fits ('mean_predict_plane2'), else one ('mean_predict_plane', also forced with
-    KMP_MP_PPB=1), on C3 tiles, ragged windows, and batches that take the XCD-contiguous block order
-    with an even and an odd output-plane count (the last group then holds one plane), against the
-    oracle; both forms give the same bits."""
-    import os
+    """The LDS-staged mean predictor (3D, C == 1): two output planes per workgroup where the LDS
+    fits ('mean_predict_plane2'), else one ('mean_predict_plane': e.g. the C3 window at p = 2), on
+    C3 tiles, ragged windows, and batches that take the XCD-contiguous block order with an even and
+    an odd output-plane count (the last group then holds one plane), against the oracle."""
     hi = _rand(shape, dtype, 11)
     lo = oracle.volume.lowres_from_highres(oracle.volume.pad_highres(hi)[0])
     window = oracle.volume.pad_neighborhood(lo, padding)
     want = oracle.predictors.mean_predictions_fn(padding, 3)(window)
     two = _mp_lds_bytes(window.shape, window.itemsize, padding, 2) <= 64 * 1024
     x8 = padding == 0 and (window.shape[3] - 1) % 8 == 0  # p = 0, cell rows of 8k: mean_predict_p0x8
-    runs = {}
-    for env, val, name in ((None, None, 'mean_predict_p0x8' if x8 else 'mean_predict_plane2' if two
-                            else 'mean_predict_plane'),
-                           ('KMP_MP_PPB', '1', 'mean_predict_p0x8' if x8 else 'mean_predict_plane')):
-        if env:
-            os.environ[env] = val
-        try:
-            runs[(env, val)] = kom.MeanPredictor(padding, 3)(torch.from_numpy(window).cuda())
-            assert kom._lib.lib.kmp_last_launch().decode() == name, env
-        finally:
-            if env:
-                del os.environ[env]
+    runs = {'default': kom.MeanPredictor(padding, 3)(torch.from_numpy(window).cuda())}
+    assert kom._lib.lib.kmp_last_launch().decode() == (
+        'mean_predict_p0x8' if x8 else 'mean_predict_plane2' if two else 'mean_predict_plane')
     for key, got in runs.items():
         for a, b in zip(got, want):
             _eq(a, b)

@@ -212,3 +212,28 @@ def test_container_rejects_foreign_and_truncated_files(tmp_path):
     for name in ('foreign.kmp', 'short.kmp', 'trunc.kmp', 'crc.kmp'):
         with pytest.raises(ValueError):
             kom.container.decompress(str(tmp_path / name))
+
+
+def test_dispatch_options_are_a_table_not_the_environment():
+    """Kernel dispatch options live in a process-wide table the library seeds
+    from the environment once, at load; set / get / clear work without a GPU and unknown names are
+    refused (no getenv per launch)."""
+    from kompressor_amd import _lib as L
+    assert L.get_option('KMP_DISABLE_FAST') is None
+    with L.option('KMP_DISABLE_FAST', 1):
+        assert L.get_option('KMP_DISABLE_FAST') == 1
+        with L.option('KMP_DISABLE_FAST', None):
+            assert L.get_option('KMP_DISABLE_FAST') is None
+        assert L.get_option('KMP_DISABLE_FAST') == 1
+    assert L.get_option('KMP_DISABLE_FAST') is None
+    os.environ['KMP_W3_XCD'] = '0'  # read at load only: changing it now has no effect
+    try:
+        assert L.get_option('KMP_W3_XCD') is None
+    finally:
+        del os.environ['KMP_W3_XCD']
+    for bad in ('KMP_MP_PPB', 'KMP_W3P_ROLL', 'KMP_W2R_RUN', 'NOT_AN_OPTION'):
+        with pytest.raises(L.KompressorHipError):
+            L.set_option(bad, 1)
+    src = ''.join(open(os.path.join(ROOT, 'kompressor_amd', 'csrc', f)).read()
+                  for f in os.listdir(os.path.join(ROOT, 'kompressor_amd', 'csrc')) if f != 'kmp_options.hip')
+    assert 'getenv' not in src
