@@ -147,7 +147,9 @@ int64_t generic_workspace_bytes(int dtype, int nsp, const Geo& g, int64_t B, int
     const int64_t nb = 2 * pred->padding + 2, N = nsp == 3 ? nb * nb * nb : nb * nb;
     int64_t wbytes = N * K * (int64_t)sizeof(float);
     // the matrix-core kernels' B fragments (3 column tiles x 8 chunks x 64 lanes x 16 B) + biases
-    if (pred->kind == KMP_PRED_LINEAR_MFMA) wbytes = wbytes > 3 * 8 * 64 * 16 + 3 * 64 * 4 ? wbytes : 3 * 8 * 64 * 16 + 3 * 64 * 4;
+    // + linear3pm's dummy store slots (64 lanes x 16 B)
+    constexpr int64_t kMfmaWs = 3 * 8 * 64 * 16 + 3 * 64 * 4 + 64 * 16;
+    if (pred->kind == KMP_PRED_LINEAR_MFMA) wbytes = wbytes > kMfmaWs ? wbytes : kMfmaWs;
     need = need > wbytes ? need : wbytes;
   }
   return need;

@@ -13,29 +13,35 @@
 //
 // A workgroup owns a run of output planes of one tile (all 32 at C3) and rolls along z; its waves own
 // ROWS lowres rows each (the lane layout, loads and aggregation of kmp_codec_linear3dp.hip).  Per
-// output plane c:
-//   1. the coder phase: plane c-1's maps and coder (below); node plane c+2's rows, loaded a step
-//      earlier, staged in LDS as feature dwords (bf16 hi byte | bf16 lo byte) with the mirrored
-//      halo rows / columns of the symmetric neighbourhood pad over the even reflect pad
-//      (volume/utils.py:213-237) into a 5-slot ring; node plane c+3 and plane c's streams loaded
-//      for the next step -- so each node plane is read from HBM and staged once per run; a barrier;
-//   2. the channel phase: per 16-cell tile (16 consecutive x of one row) two column tiles: cell plane
-//      c (node planes c-1 .. c+2, its 14 channels) and cell plane c-1 (node planes c-2 .. c+1,
-//      channels 5, 13, 14, 17, 18), 8 MFMAs each.  Chunk q = 2 dz + h covers node rows dy = 2h, 2h+1
-//      of plane dz: the A fragment of lane (g, m) is its cell's 4 consecutive nodes x-1 .. x+2 of
-//      node row 2h + (g & 1) -- so the plane-c tile's chunk (dz, h) and the plane-(c-1) tile's chunk
-//      (dz+1, h) read the same fragment, and row Y's h = 1 fragment is row Y+2's h = 0 one: the wave
-//      walks its rows by parity and reads 5 fragments per row instead of 16.  The weights' B
-//      fragments (built once per call, fragments_kernel) stay in registers for the whole run.  Each
-//      MFMA leaves a lane one channel of 4 cells, cast to u16 and written to the wave's channel table
-//      [channel][row][x] in LDS; a barrier;
-//   3. (in the next step's coder phase) each lane reads back its cells' channels (the row above from
-//      the same table, the wave above's last row included) and runs linear3dp's aggregation, coder
-//      and stores.
-// 75 KB of LDS a workgroup (ring 34 KB, channel tables 41 KB), 2 workgroups per CU,
-// so one workgroup's channel phase overlaps the other's coder phase.  LDS pitches are padded so the
-// fragment reads (ds_read2_b32: banks (a/4) mod 32 per half wave) and the channel-table writes are
-// conflict-free.
+// output plane c, two phases between barriers:
+//   1. each lane fetches its cells' channels of plane c-1 from the channel table into registers
+//      (the row above too: the wave above's last row, or zeros on row 0); node plane c+2's rows,
+//      loaded a step earlier, are staged in LDS as feature dwords (bf16 hi byte | bf16 lo byte)
+//      with the mirrored halo rows / columns of the symmetric neighbourhood pad over the even
+//      reflect pad (volume/utils.py:213-237) into a 5-slot ring; node plane c+3 and plane c's
+//      streams are loaded for the next step -- so each node plane is read from HBM and staged once
+//      per run;
+//   2. the channel phase of plane c and, between its MFMA groups, the maps and coder of plane c-1
+//      from the fetched registers (linear3dp's aggregation; four parts after tile rows 3, 7, 11,
+//      15), so one wave issues vector work in the cycles its own MFMAs leave free.  Per 16-cell
+//      tile (16 consecutive x of one row) two column tiles: cell plane c (node planes c-1 .. c+2,
+//      its 14 channels) and cell plane c-1 (node planes c-2 .. c+1, channels 5, 13, 14, 17, 18),
+//      8 MFMAs each.  Chunk q = 2 dz + h covers node rows dy = 2h, 2h+1 of plane dz: the A fragment
+//      of lane (g, m) is its cell's 4 consecutive nodes x-1 .. x+2 of node row 2h + (g & 1) -- so
+//      the plane-c tile's chunk (dz, h) and the plane-(c-1) tile's chunk (dz+1, h) read the same
+//      fragment, and row Y's h = 1 fragment is row Y+2's h = 0 one: the wave walks its rows by
+//      parity and reads 5 fragments per row instead of 16, the next row's while this row's odd
+//      chunks run.  The weights' B fragments (built once per call, fragments_kernel) stay in
+//      registers for the whole run.  Each MFMA leaves a lane one channel of 4 cells, cast to u16
+//      (clamped first, kmp_bf16x2.h) and written to the wave's channel table [slot][row][x].
+// 75 KB of LDS a workgroup (ring 34 KB, channel tables 42 KB), 2 workgroups per CU (<= 256 VGPRs).
+// LDS pitches and the table's slot order are chosen so the fragment reads (ds_read2_b32: banks
+// (a/4) mod 32 per half wave) and the channel-table writes (ds_write_b64, every column of the tile,
+// the unused ones into dummy slots: no exec-mask branches) are conflict-free.
+// Round 5: 296 / 289 -> 262-270 / 256-266 us per direction at C3 (rocprofv3, alternating;
+// profiles/round5/): fragment bases in 10 LDS pointers per plane with immediate offsets (VALU per
+// wave and plane 819 -> 601), the coder overlapped with the channel phase, the row-above masked
+// instead of branched, conflict-free table slots (LDS bank-conflict cycles 6.8 M -> 2.6 M).
 #include <cstdlib>
 
 #include "kmp_bf16x2.h"
@@ -62,11 +68,22 @@ struct PM {
   int32_t xcd_per;
 };
 
+// a 32-bit LDS pointer (kept as one through inline-asm barriers, unlike a generic pointer)
+typedef const uint32_t __attribute__((address_space(3)))* lds_cptr;
+
 constexpr int P = 1;         // padding
 constexpr int NPL = 2 * P + 3;  // staged node planes c-1-P .. c+1+P
 // column tiles: cell plane c (C) and c-1 (Q); -1 = unused column
 __constant__ int8_t kCch[16] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16, -1, -1};
 __constant__ int8_t kQch[16] = {5, 13, 14, 17, 18, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+// the channel table's slot of channel k: column m of the C tile is slot m, column m of the Q tile
+// slot 14 + m, so the lanes of one ds_write_b64 lane group (one column each) land on distinct bank
+// pairs (a slot moves the bank by 2: CS / 2 = 2 mod 32) -- the channel numbers themselves collide
+// (0 and 16)
+__host__ __device__ constexpr int slot_of(int k) {
+  constexpr int8_t s[19] = {0, 1, 2, 3, 4, 14, 5, 6, 7, 8, 9, 10, 11, 15, 16, 12, 13, 17, 18};
+  return s[k];
+}
 
 // The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
 // biases, built once per call into the workspace instead of in every wave (64 bf16 splits a lane)
@@ -83,9 +100,11 @@ __global__ void __launch_bounds__(64) fragments_kernel(const float* __restrict__
   }
 }
 constexpr size_t kFragBytes = 3 * 8 * 64 * sizeof(bx::u32x4) + 3 * 64 * sizeof(float);
+// + the dummy store slots (8 u16 per lane) after the fragments
+constexpr size_t kWsBytes = kFragBytes + 64 * 8 * sizeof(uint16_t);
 
 template <bool DEC, int EX, int EY>
-__global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a) {
+__global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_waves_per_eu(2, 2))) linear3pm_kernel(PM a) {
   typedef uint16_t T;
   constexpr int VX = 4;               // u16 cells per lane
   constexpr int TXN = EX / VX;        // lanes per row
@@ -99,13 +118,15 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   // g = 0 / 1 (adjacent node rows) then take disjoint banks
   constexpr int PITCH0 = EX + P + NHR;
   constexpr int PITCH = PITCH0 + ((16 - PITCH0 % 32) + 32) % 32;
-  // a wave's channel table (u16) [channel][row][x], the channel stride padded 2 banks past a
-  // multiple of 32 so that an MFMA's 16 channels (one ds_write_b64 lane group) write 32 banks, then
-  // DMY u16 where the MFMA columns that carry no channel write (each lane its own 8 bytes: no
-  // exec-mask branch around the table stores)
+  // a wave's channel table (u16) [slot][row][x], the slot stride padded 2 banks past a multiple
+  // of 32 so that an MFMA's 16 columns (one ds_write_b64 lane group) write 32 banks, then DMY u16
+  // where the MFMA columns that carry no channel write (no exec-mask branch around the table
+  // stores): a column's dummy address takes the bank pair of a slot its tile does not use
   constexpr int CS = ROWS * EX + 4;
-  constexpr int DMY = 64 * 4 + (ROWS - 1) * EX + EX / 2;
+  constexpr int DPAD = (64 - (19 * CS) % 64) % 64;  // dummy base: bank offset 0, like slot 0
+  constexpr int DMY = DPAD + 4 * 15 + 4 * 3 + (ROWS - 1) * EX + EX / 2 + 4;
   constexpr int CT = 19 * CS + DMY;
+  static_assert(CS % 64 == 4, "bank layout");
   constexpr uint32_t MASK = 0xffffu;
   static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
   using V = typename std::conditional<DEC, uint2, uint4>::type;
@@ -162,29 +183,32 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     uint4 e1, o0, o1;
   };
   auto load_streams = [&](int c, Streams& sv) {
+    // unconditional: a plane past an odd-sized z axis (c >= Lcz) re-reads the one before, its
+    // values unused (the outputs go to the dummy slot)
     const bool vz1 = c < a.Lcz;
     if constexpr (DEC) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         int par[3];
         map_parity(3, k, par);
-        sv.mv[k] = (!par[0] || vz1) ? ld8(mbase[k] + c * lplane) : make_uint2(0, 0);
+        sv.mv[k] = ld8(mbase[k] + ((!par[0] || vz1) ? c : c - 1) * lplane);
       }
     } else {
       const T* p = hin + 2 * c * hplane;
+      const int o = vz1 ? hplane : 0;
       sv.e1 = ld16(p + ho_own + a.W_);
-      sv.o0 = vz1 ? ld16(p + hplane + ho_own) : make_uint4(0, 0, 0, 0);
-      sv.o1 = vz1 ? ld16(p + hplane + ho_own + a.W_) : make_uint4(0, 0, 0, 0);
+      sv.o0 = ld16(p + o + ho_own);
+      sv.o1 = ld16(p + o + ho_own + a.W_);
     }
   };
 
   const int chC = kCch[m], chQ = kQch[m];
   T* const ctw = ct + w * CT;
   // the lane's column of the channel table (its C / Q channel, 4 cells from x0 + 4g), or its dummy slot
-  T* const ctC = chC >= 0 ? ctw + chC * CS + 4 * g : ctw + 19 * CS + 4 * lane;
-  T* const ctQ = chQ >= 0 ? ctw + chQ * CS + 4 * g : ctw + 19 * CS + 4 * lane;
+  T* const ctC = ctw + (m < 14 ? m * CS : 19 * CS + DPAD + 4 * m) + 4 * g;             // dummy: slots 14, 15's banks
+  T* const ctQ = ctw + (m < 5 ? (14 + m) * CS : 19 * CS + DPAD + 4 * (m - 2)) + 4 * g;  // dummy: slots 3 .. 13's
   // the lane's A-fragment origin: ring slot 0, node row Y0 + (g & 1), node column m
-  const uint32_t* const fl = st + (Y0 + (g & 1)) * PITCH + m;
+  const lds_cptr fl = (lds_cptr)st + (Y0 + (g & 1)) * PITCH + m;
 
   // ---- staging: the node row of node plane q as feature dwords into ring slot q mod 5, plus
   // the mirrored halo columns / rows this lane is the source of (lsrc1) ----
@@ -225,44 +249,64 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   // ---- the channels of output plane c on the matrix cores, into the wave's channel table.  A
   // cell plane outside the tile (c - 1 < 0: Q, c >= Lcz: C) has channels 0, what the
   // aggregation's masks want: the cast's upper clamp is 0 for it ----
-  auto channels = [&](int c, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC, float biasQ) {
+  // hook(tr) runs after tile row tr (0 .. 2 ROWS - 1): the caller's vector work placed between the
+  // MFMA groups in program order
+  auto channels = [&](int c, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC, float biasQ,
+                      auto&& hook) {
     const float hiC = c < a.Lcz ? 65535.0f : 0.0f, hiQ = c >= 1 ? 65535.0f : 0.0f;
     // A fragment: node plane c - 2 + t (ring slot (c - 2 + t) mod 5), staged rows Y0 + ry + (g & 1),
     // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
-    const uint32_t* fb[NPL][2];
+    lds_cptr fb[NPL][2];
 #pragma unroll
     for (int t = 0; t < NPL; ++t) {
       fb[t][0] = fl + ((c - 2 + t + 2 * NPL) % NPL) * (NR * PITCH);
       fb[t][1] = fb[t][0] + 5 * PITCH;
+      // opaque to the optimiser: otherwise it folds fb[t][1] back into fb[t][0] + a constant past
+      // ds_read2_b32's 8-bit offsets and pays a v_add_u32 per fragment half
+      asm volatile("" : "+v"(fb[t][0]));
+      asm volatile("" : "+v"(fb[t][1]));
     }
     auto frag = [&](int t, int ry, int x0) {
-      const uint32_t* p = fb[t][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
+      const lds_cptr p = fb[t][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
     };
-    // tile rows by x tile, row parity, row pair: row Y's node rows 2, 3 (F1) are row Y+2's 0, 1
+    // tile rows by x tile, row parity, row pair: row Y's node rows 2, 3 (its odd chunks' fragments)
+    // are row Y+2's 0, 1 (its even chunks').  Two fragment sets alternate: once a row's even-chunk
+    // MFMAs have issued, their set receives the next row's odd-chunk fragments, so those LDS reads
+    // run under this row's odd-chunk MFMAs (no extra registers, no exposed LDS latency per row)
 #pragma unroll
     for (int xt = 0; xt < TPR; ++xt) {
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
-        bx::u32x4 F0[NPL], F1[NPL];
+        bx::u32x4 F[2][NPL];
 #pragma unroll
-        for (int t = 0; t < NPL; ++t) F0[t] = frag(t, par, 16 * xt);
+        for (int t = 0; t < NPL; ++t) F[0][t] = frag(t, par, 16 * xt);
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) F[1][t] = frag(t, par + 2, 16 * xt);
 #pragma unroll
         for (int j = 0; j < ROWS / 2; ++j) {
           const int row = par + 2 * j;
-#pragma unroll
-          for (int t = 0; t < NPL; ++t) F1[t] = frag(t, row + 2, 16 * xt);
+          const int e = j & 1, o = e ^ 1;  // this row's even- / odd-chunk fragment sets
           bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
+          // chunk q = 2 dz + h (plane offset dz, node rows 2h + 0 / 1), in chunk_at order: even q, then odd
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {  // chunk q (plane offset dz = q / 2, node rows 2 (q & 1) + 0 / 1)
-            const int q = bx::chunk_at(i, 8), dz = q >> 1;
-            dC = bx::mfma((q & 1) ? F1[1 + dz] : F0[1 + dz], bC[q], dC);
-            dQ = bx::mfma((q & 1) ? F1[dz] : F0[dz], bQ[q], dQ);
+          for (int dz = 0; dz < 4; ++dz) {
+            dC = bx::mfma(F[e][1 + dz], bC[2 * dz], dC);
+            dQ = bx::mfma(F[e][dz], bQ[2 * dz], dQ);
           }
+          if (j + 1 < ROWS / 2) {
+#pragma unroll
+            for (int t = 0; t < NPL; ++t) F[e][t] = frag(t, row + 4, 16 * xt);
+          }
+#pragma unroll
+          for (int dz = 0; dz < 4; ++dz) {
+            dC = bx::mfma(F[o][1 + dz], bC[2 * dz + 1], dC);
+            dQ = bx::mfma(F[o][dz], bQ[2 * dz + 1], dQ);
+          }
+          static_assert(bx::chunk_at(3, 8) == 6 && bx::chunk_at(4, 8) == 1, "even chunks, then odd");
           *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(dC, hiC);
           *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(dQ, hiQ);
-#pragma unroll
-          for (int t = 0; t < NPL; ++t) F0[t] = F1[t];
+          hook(xt * ROWS + par * (ROWS / 2) + j);
         }
       }
     }
@@ -270,31 +314,48 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
 
   const T* const upt = (r > 0 ? ctw + (r - 1) * EX : w > 0 ? ctw - CT + (ROWS - 1) * EX : ctw) + X;
   const uint32_t upm = Y > 0 ? 0xffffffffu : 0u;
-  // ---- the maps / coder of output plane c from the channel table (linear3dp's aggregation):
-  // channel k of the lane's cells X .. X+3 at index 1 .. 4; the row above from the table (the
-  // wave above's last row for r = 0; none above row 0: zeros) ----
-  auto aggregate = [&](int c, const V& own, const Streams& sv) {
+  // the channels the coder of one output plane reads: the lane's 4 cells of all 19 channels (slot
+  // order) and the 5 row-above channels (3, 9, 10, 16, 17; this wave's row r - 1, the wave above's
+  // last row, or zeros by a mask on row 0), as packed u16.  Fetched right after the barrier that
+  // completes the plane's table, so the next plane's channel phase may overwrite the table while
+  // this plane is coded from registers.
+  struct Chan {
+    uint2 v[19];
+    uint2 up[5];
+  };
+  auto fetch = [&](Chan& ch) {
+#pragma unroll
+    for (int k = 0; k < 19; ++k) ch.v[k] = *(const uint2*)(ctw + slot_of(k) * CS + r * EX + X);
+    constexpr int kUp[5] = {3, 9, 10, 16, 17};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      uint2 u = *(const uint2*)(upt + slot_of(kUp[j]) * CS);
+      ch.up[j] = make_uint2(u.x & upm, u.y & upm);
+    }
+  };
+  // where the stores of outputs that do not exist go (a plane past an odd-sized axis): a scratch
+  // slot per lane in the workspace, so the store needs no branch
+  T* const dummy = (T*)((char*)a.frag + kFragBytes) + 8 * lane;
+
+  // ---- the maps / coder of output plane c from its channels (linear3dp's aggregation): channel k
+  // of the lane's cells X .. X+3 at index 1 .. 4 ----
+  // part 0: the lowres and X map; 1: Z, UD; 2: Y, FB; 3: LR, C
+  auto aggregate = [&](int c, const V& own, const Streams& sv, const Chan& ch, int part) {
     const bool vz1 = c < a.Lcz, vz0 = c >= 1;
-    auto rd_at = [&](const T* tab, int k, int row, uint32_t (&v)[VX + 1]) {
-      const uint2 u = *(const uint2*)(tab + k * CS + row * EX + X);
+    auto rd = [&](int k, uint32_t (&v)[VX + 1]) {
 #pragma unroll
-      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(ch.v[k], i);
     };
-    auto rd = [&](int k, uint32_t (&v)[VX + 1]) { rd_at(ctw, k, r, v); };
-    // the row above: this wave's row r - 1, the wave above's last row, or (Y = 0) zeros by a mask
-    auto rd_up = [&](int k, uint32_t (&v)[VX + 1]) {
-      uint2 u = *(const uint2*)(upt + k * CS);
-      u.x &= upm;
-      u.y &= upm;
+    auto rd_up = [&](int j, uint32_t (&v)[VX + 1]) {
 #pragma unroll
-      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(u, i);
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(ch.up[j], i);
     };
     uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
-    rd_up(3, A3);
-    rd_up(9, A9);
-    rd_up(10, A10);
-    rd_up(16, A16);
-    rd_up(17, QA17);
+    rd_up(0, A3);
+    rd_up(1, A9);
+    rd_up(2, A10);
+    rd_up(3, A16);
+    rd_up(4, QA17);
     A9[0] = shup(A9[VX], 1);
 
     const bool vy0 = Y >= 1;
@@ -308,7 +369,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     auto put8 = [&](int k, const uint32_t (&res)[VX]) {
       int par[3];
       map_parity(3, k, par);
-      if (!par[0] || vz1) st8(mbase[k] + c * lplane, pack8<T, VX>(res));
+      st8((!par[0] || vz1) ? mbase[k] + c * lplane : dummy, pack8<T, VX>(res));
     };
     const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own;
     T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
@@ -327,7 +388,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     };
 
     // X map (0,0,1): ch15 (z,y) ch16 (z,y-1) ch17 (z-1,y-1) ch18 (z-1,y); with the lowres
-    {
+    if (part == 0) {
       uint32_t P15[VX + 1], Q18[VX + 1], pred[VX], outv[VX];
       rd(15, P15);
       rd(18, Q18);
@@ -342,7 +403,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       }
     }
     // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
-    {
+    if (part == 1) {
       uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
       uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
       rd(7, P7);
@@ -358,14 +419,14 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       code(4, pZ, sv.o0, 0, oZ);
       code(1, pU, sv.o0, 1, oU);
       if constexpr (DEC) {
-        if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
+        st16(vz1 ? h0 + hplane : dummy, pack16<T, VX>(oZ, oU));
       } else {
         put8(4, oZ);
         put8(1, oU);
       }
     }
     // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
-    {
+    if (part == 2) {
       uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
       uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
       rd(11, P11);
@@ -392,7 +453,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       }
     }
     // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
-    {
+    if (part == 3) {
       uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
       uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
       rd(0, P0);
@@ -408,7 +469,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
       code(0, pL, sv.o1, 0, oL);
       code(3, pC, sv.o1, 1, oC);
       if constexpr (DEC) {
-        if (vz1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
+        st16(vz1 ? h0 + hplane + a.W_ : dummy, pack16<T, VX>(oL, oC));
       } else {
         put8(0, oL);
         put8(3, oC);
@@ -416,10 +477,14 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
     }
   };
 
-  // ---- the run: per output plane c, [code plane c-1 | stage node plane c+2 | load node plane
-  // c+3 and plane c's streams] barrier [channels of plane c] barrier.  Node planes c-1 .. c+3 stay
-  // in registers (R0 .. R4) until their coder step; each node plane is loaded and staged once
-  // per run.  Two workgroups share a CU (LDS), one in its channel phase while the other codes ----
+  // ---- the run, one barrier pair per output plane c:
+  //   [fetch plane c-1's channels | stage node plane c+2 | load node plane c+3 and plane c's streams]
+  //   barrier
+  //   [channels of plane c (matrix cores, into the table) || maps + coder of plane c-1 (registers)]
+  //   barrier
+  // The second phase holds both the MFMA work and the vector work, independent of each other, so
+  // one wave issues vector instructions between its own MFMAs.  Node planes c-1 .. c+3 stay in
+  // registers (R0 .. R4) until their coder step; each node plane is loaded and staged once per run.
   bx::u32x4 bC[8], bQ[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -434,22 +499,35 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) linear3pm_kernel(PM a)
   stage(R1, cb);
   stage(R2, cb + 1);
   Streams Sp, Sc;
-  for (int c = cb; c < ce; ++c) {
-    if (c > cb) aggregate(c - 1, R0, Sp);
-    stage(R3, c + 2);
-    V R4{};
-    if (c + 1 < ce) R4 = node_row(c + 3);
-    load_streams(c, Sc);
-    __syncthreads();
-    channels(c, bC, bQ, biasC, biasQ);
-    __syncthreads();
+  Chan ch;
+  // plane cb: no coder work yet
+  stage(R3, cb + 2);
+  V R4 = node_row(cb + 3 < ce + 2 ? cb + 3 : cb + 2);
+  load_streams(cb, Sc);
+  __syncthreads();
+  channels(cb, bC, bQ, biasC, biasQ, [](int) {});
+  __syncthreads();
+  for (int c = cb + 1; c < ce; ++c) {
     R0 = R1;
     R1 = R2;
     R2 = R3;
     R3 = R4;
     Sp = Sc;
+    fetch(ch);
+    stage(R3, c + 2);
+    R4 = node_row(c + 1 < ce ? c + 3 : c + 2);  // the last step re-reads a plane (unused)
+    load_streams(c, Sc);
+    __syncthreads();
+    // the coder's vector work in four parts between the MFMA groups (an MFMA leaves 8 of its 16
+    // cycles free for issue), not after the last one
+    channels(c, bC, bQ, biasC, biasQ, [&](int tr) {
+      if ((tr & 3) == 3) aggregate(c - 1, R0, Sp, ch, tr >> 2);
+    });
+    __syncthreads();
   }
-  aggregate(ce - 1, R0, Sp);
+  fetch(ch);
+#pragma unroll
+  for (int part = 0; part < 4; ++part) aggregate(ce - 1, R1, Sc, ch, part);
 }
 
 }  // namespace l3q
@@ -526,7 +604,7 @@ int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     a.maps = maps;
     a.W = pred->weights;
     a.b = pred->bias;
-    if (!ws || ws_bytes < l3q::kFragBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
+    if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
     l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
     launch_linear3pm<false>(a, grid, block, stream);
@@ -552,7 +630,7 @@ int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     a.lo_in = lowres;
     a.W = pred->weights;
     a.b = pred->bias;
-    if (!ws || ws_bytes < l3q::kFragBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
+    if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
     l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
     launch_linear3pm<true>(a, grid, block, stream);
