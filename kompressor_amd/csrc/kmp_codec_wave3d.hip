@@ -45,7 +45,7 @@ struct W3 {
   int32_t xcd_per;  // > 0: XCD-contiguous block order (blocks per XCD), 0: identity
   int32_t nt_nodes; // plane kernel: 1 = non-temporal node-row loads, 0 = default policy (L2-shared halo)
   int64_t nB;       // tiles in the batch (debug-build bounds checks only)
-  int32_t nvblk;    // virtual blocks, grid-strided over the workgroups
+  int32_t nvblk;    // blocks (= workgroups launched)
 };
 
 // rows a lane reads for one node plane: its own, and (wave's first / last row) one halo row;
@@ -366,11 +366,13 @@ __device__ __forceinline__ void wave3d_plane_body(const W3& a, int vblk) {
   }
 }
 
-// A workgroup codes the virtual blocks blockIdx.x, + gridDim.x, ... (grid-stride; gridDim a multiple
-// of 8 keeps each virtual block on the XCD the tile-per-XCD order gives it)
+// One workgroup per block (the host launches a.nvblk workgroups).  Not a grid-stride loop: kept
+// live across iterations, the loop's kernel arguments overflowed the scalar registers (29 / 32 SGPRs
+// spilled into VGPR lanes: 98 / 72 v_readlane per encode / decode wave); without it none spill and
+// the waves issue 849 -> 731 / 818 -> 713 VALU instructions (round 5)
 template <typename T, bool DEC, int PL, int WPE, bool ONE, bool STC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) wave3d_plane_kernel(W3 a) {
-  for (int v = (int)blockIdx.x; v < a.nvblk; v += (int)gridDim.x) wave3d_plane_body<T, DEC, PL, ONE, STC>(a, v);
+  wave3d_plane_body<T, DEC, PL, ONE, STC>(a, (int)blockIdx.x);
 }
 
 }  // namespace w3
