@@ -72,17 +72,20 @@ struct PM {
 typedef const uint32_t __attribute__((address_space(3)))* lds_cptr;
 
 constexpr int P = 1;         // padding
-constexpr int NPL = 2 * P + 3;  // staged node planes c-1-P .. c+1+P
-// column tiles: cell plane c (C) and c-1 (Q); -1 = unused column
+constexpr int NPL = 2 * P + 2;  // staged node planes: cell plane c's neighbourhood c-P .. c+1+P
+// column tiles of one cell plane: the 14 channels its own output plane reads (C) and the 5 the next
+// output plane reads as its z-1 channels (Q); -1 = unused column
 __constant__ int8_t kCch[16] = {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 15, 16, -1, -1};
 __constant__ int8_t kQch[16] = {5, 13, 14, 17, 18, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 // the channel table's slot of channel k: column m of the C tile is slot m, column m of the Q tile
-// slot 14 + m, so the lanes of one ds_write_b64 lane group (one column each) land on distinct bank
-// pairs (a slot moves the bank by 2: CS / 2 = 2 mod 32) -- the channel numbers themselves collide
-// (0 and 16)
-__host__ __device__ constexpr int slot_of(int k) {
+// slot 14 + 5 q + m (q: the parity of the Q channels' cell plane -- they live one output plane
+// longer than the C channels), so the lanes of one ds_write_b64 lane group (one column each) land
+// on distinct bank pairs (a slot moves the bank by 2: CS / 2 = 2 mod 32) -- the channel numbers
+// themselves collide (0 and 16)
+constexpr int kSlots = 24;
+__host__ __device__ constexpr int slot_of(int k, int q) {
   constexpr int8_t s[19] = {0, 1, 2, 3, 4, 14, 5, 6, 7, 8, 9, 10, 11, 15, 16, 12, 13, 17, 18};
-  return s[k];
+  return s[k] + (s[k] >= 14 ? 5 * q : 0);
 }
 
 // The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
@@ -123,15 +126,15 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   // where the MFMA columns that carry no channel write (no exec-mask branch around the table
   // stores): a column's dummy address takes the bank pair of a slot its tile does not use
   constexpr int CS = ROWS * EX + 4;
-  constexpr int DPAD = (64 - (19 * CS) % 64) % 64;  // dummy base: bank offset 0, like slot 0
+  constexpr int DPAD = (64 - (kSlots * CS) % 64) % 64;  // dummy base: bank offset 0, like slot 0
   constexpr int DMY = DPAD + 4 * 15 + 4 * 3 + (ROWS - 1) * EX + EX / 2 + 4;
-  constexpr int CT = 19 * CS + DMY;
+  constexpr int CT = kSlots * CS + DMY;
   static_assert(CS % 64 == 4, "bank layout");
   constexpr uint32_t MASK = 0xffffu;
   static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
   using V = typename std::conditional<DEC, uint2, uint4>::type;
 
-  __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];  // ring of 5 node planes
+  __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];  // ring of 4 node planes
   __shared__ __attribute__((aligned(16))) T ct[NW * CT];
 
   const int lane = threadIdx.x & 63;
@@ -205,8 +208,13 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   const int chC = kCch[m], chQ = kQch[m];
   T* const ctw = ct + w * CT;
   // the lane's column of the channel table (its C / Q channel, 4 cells from x0 + 4g), or its dummy slot
-  T* const ctC = ctw + (m < 14 ? m * CS : 19 * CS + DPAD + 4 * m) + 4 * g;             // dummy: slots 14, 15's banks
-  T* const ctQ = ctw + (m < 5 ? (14 + m) * CS : 19 * CS + DPAD + 4 * (m - 2)) + 4 * g;  // dummy: slots 3 .. 13's
+  // dummy addresses mimic the bank pair of a slot (mod 16) the tile's real columns do not take:
+  // C: slots 14, 15; Q of parity 0 (slots 14 .. 18, banks of slots 14, 15, 0, 1, 2): slots 3 .. 13;
+  // Q of parity 1 (slots 19 .. 23, banks of slots 3 .. 7): slots 8 .. 15, 0 .. 2
+  T* const dmy = ctw + kSlots * CS + DPAD + 4 * g;
+  T* const ctC = m < 14 ? ctw + m * CS + 4 * g : dmy + 4 * m;
+  T* const ctQ0 = m < 5 ? ctw + (14 + m) * CS + 4 * g : dmy + 4 * (m - 2);
+  T* const ctQ1 = m < 5 ? ctw + (19 + m) * CS + 4 * g : dmy + 4 * ((m + 3) & 15);
   // the lane's A-fragment origin: ring slot 0, node row Y0 + (g & 1), node column m
   const lds_cptr fl = (lds_cptr)st + (Y0 + (g & 1)) * PITCH + m;
 
@@ -246,20 +254,22 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     }
   };
 
-  // ---- the channels of output plane c on the matrix cores, into the wave's channel table.  A
-  // cell plane outside the tile (c - 1 < 0: Q, c >= Lcz: C) has channels 0, what the
-  // aggregation's masks want: the cast's upper clamp is 0 for it ----
+  // ---- the channels of cell plane c on the matrix cores, into the wave's channel table: its C
+  // channels (skipped with withC = false) and its Q channels (into the slots of parity c & 1).  A
+  // cell plane outside the tile (c < 0 or c >= Lcz) has channels 0, what the aggregation's masks
+  // want: the cast's upper clamp is 0 for it ----
   // hook(tr) runs after tile row tr (0 .. 2 ROWS - 1): the caller's vector work placed between the
   // MFMA groups in program order
-  auto channels = [&](int c, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC, float biasQ,
-                      auto&& hook) {
-    const float hiC = c < a.Lcz ? 65535.0f : 0.0f, hiQ = c >= 1 ? 65535.0f : 0.0f;
-    // A fragment: node plane c - 2 + t (ring slot (c - 2 + t) mod 5), staged rows Y0 + ry + (g & 1),
+  auto channels = [&](int c, bool withC, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC,
+                      float biasQ, auto&& hook) {
+    const float hi = c >= 0 && c < a.Lcz ? 65535.0f : 0.0f;
+    T* const ctQ = (c & 1) ? ctQ1 : ctQ0;
+    // A fragment: node plane c - 1 + t (ring slot (c - 1 + t) mod 4), staged rows Y0 + ry + (g & 1),
     // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
     lds_cptr fb[NPL][2];
 #pragma unroll
     for (int t = 0; t < NPL; ++t) {
-      fb[t][0] = fl + ((c - 2 + t + 2 * NPL) % NPL) * (NR * PITCH);
+      fb[t][0] = fl + ((c - 1 + t + 2 * NPL) % NPL) * (NR * PITCH);
       fb[t][1] = fb[t][0] + 5 * PITCH;
       // opaque to the optimiser: otherwise it folds fb[t][1] back into fb[t][0] + a constant past
       // ds_read2_b32's 8-bit offsets and pays a v_add_u32 per fragment half
@@ -270,8 +280,9 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
       const lds_cptr p = fb[t][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
     };
-    // tile rows by x tile, row parity, row pair: row Y's node rows 2, 3 (its odd chunks' fragments)
-    // are row Y+2's 0, 1 (its even chunks').  Two fragment sets alternate: once a row's even-chunk
+    // tile rows by x tile, row parity, row pair: the C and Q tiles of a row read the same fragments
+    // (the same neighbourhood), and row Y's node rows 2, 3 (its odd chunks' fragments) are row Y+2's
+    // 0, 1 (its even chunks'): 4 fragments per row.  Two fragment sets alternate: once a row's even-chunk
     // MFMAs have issued, their set receives the next row's odd-chunk fragments, so those LDS reads
     // run under this row's odd-chunk MFMAs (no extra registers, no exposed LDS latency per row)
 #pragma unroll
@@ -291,7 +302,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
           // chunk q = 2 dz + h (plane offset dz, node rows 2h + 0 / 1), in chunk_at order: even q, then odd
 #pragma unroll
           for (int dz = 0; dz < 4; ++dz) {
-            dC = bx::mfma(F[e][1 + dz], bC[2 * dz], dC);
+            if (withC) dC = bx::mfma(F[e][dz], bC[2 * dz], dC);
             dQ = bx::mfma(F[e][dz], bQ[2 * dz], dQ);
           }
           if (j + 1 < ROWS / 2) {
@@ -300,12 +311,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
           }
 #pragma unroll
           for (int dz = 0; dz < 4; ++dz) {
-            dC = bx::mfma(F[o][1 + dz], bC[2 * dz + 1], dC);
+            if (withC) dC = bx::mfma(F[o][dz], bC[2 * dz + 1], dC);
             dQ = bx::mfma(F[o][dz], bQ[2 * dz + 1], dQ);
           }
           static_assert(bx::chunk_at(3, 8) == 6 && bx::chunk_at(4, 8) == 1, "even chunks, then odd");
-          *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(dC, hiC);
-          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(dQ, hiQ);
+          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(dC, hi);
+          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(dQ, hi);
           hook(xt * ROWS + par * (ROWS / 2) + j);
         }
       }
@@ -323,13 +334,14 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     uint2 v[19];
     uint2 up[5];
   };
-  auto fetch = [&](Chan& ch) {
+  // (q: the parity of the output plane before the one being coded -- its Q slots hold the z-1 channels)
+  auto fetch = [&](Chan& ch, int q) {
 #pragma unroll
-    for (int k = 0; k < 19; ++k) ch.v[k] = *(const uint2*)(ctw + slot_of(k) * CS + r * EX + X);
+    for (int k = 0; k < 19; ++k) ch.v[k] = *(const uint2*)(ctw + slot_of(k, q) * CS + r * EX + X);
     constexpr int kUp[5] = {3, 9, 10, 16, 17};
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      uint2 u = *(const uint2*)(upt + slot_of(kUp[j]) * CS);
+      uint2 u = *(const uint2*)(upt + slot_of(kUp[j], q) * CS);
       ch.up[j] = make_uint2(u.x & upm, u.y & upm);
     }
   };
@@ -494,10 +506,15 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   const float* fb = (const float*)(a.frag + 3 * 8 * 64);
   const float biasC = fb[lane], biasQ = fb[64 + lane];
   V R0 = node_row(cb - 1), R1 = node_row(cb), R2 = node_row(cb + 1), R3 = node_row(cb + 2);
+  // the Q channels of cell plane cb - 1 (the first output plane's z-1 channels; zeros at cb = 0),
+  // from node planes cb - 2 .. cb + 1
   stage(node_row(cb - 2), cb - 2);
   stage(R0, cb - 1);
   stage(R1, cb);
   stage(R2, cb + 1);
+  __syncthreads();
+  channels(cb - 1, false, bC, bQ, biasC, biasQ, [](int) {});
+  __syncthreads();
   Streams Sp, Sc;
   Chan ch;
   // plane cb: no coder work yet
@@ -505,7 +522,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   V R4 = node_row(cb + 3 < ce + 2 ? cb + 3 : cb + 2);
   load_streams(cb, Sc);
   __syncthreads();
-  channels(cb, bC, bQ, biasC, biasQ, [](int) {});
+  channels(cb, true, bC, bQ, biasC, biasQ, [](int) {});
   __syncthreads();
   for (int c = cb + 1; c < ce; ++c) {
     R0 = R1;
@@ -513,19 +530,19 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     R2 = R3;
     R3 = R4;
     Sp = Sc;
-    fetch(ch);
+    fetch(ch, c & 1);  // plane c-1's channels, the Q channels of cell plane c-2
     stage(R3, c + 2);
     R4 = node_row(c + 1 < ce ? c + 3 : c + 2);  // the last step re-reads a plane (unused)
     load_streams(c, Sc);
     __syncthreads();
     // the coder's vector work in four parts between the MFMA groups (an MFMA leaves 8 of its 16
     // cycles free for issue), not after the last one
-    channels(c, bC, bQ, biasC, biasQ, [&](int tr) {
+    channels(c, true, bC, bQ, biasC, biasQ, [&](int tr) {
       if ((tr & 3) == 3) aggregate(c - 1, R0, Sp, ch, tr >> 2);
     });
     __syncthreads();
   }
-  fetch(ch);
+  fetch(ch, ce & 1);
 #pragma unroll
   for (int part = 0; part < 4; ++part) aggregate(ce - 1, R1, Sc, ch, part);
 }
