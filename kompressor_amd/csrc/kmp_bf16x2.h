@@ -8,14 +8,18 @@
 //   * a u8 / u16 feature f = 256 * hi + lo splits into two bf16-exact bytes (hi, lo <= 255);
 //   * a weight splits into w1 = bf16(w), w2 = bf16(w - w1) (round to nearest even), so
 //     |w - w1 - w2| <= 2^-18 |w|; the hi parts take 256 * w1, 256 * w2 (exact: a power of two);
-//   * features are taken in chunks of 8 in the reference's order (features_from_lowres,
-//     volume/utils.py:199-210); per chunk ONE v_mfma_f32_16x16x32_bf16 with
-//         K = 32 = [hi_0, lo_0, ..., hi_7, lo_7 | the same 16] x [u1 of the chunk | u2 of the chunk],
-//     accumulated from the bias, the even chunks first, then the odd ones (chunk_at):
-//     acc = b[k]; acc = mfma(A_0, B_0, acc); acc = mfma(A_2, B_2, acc) ... acc = mfma(A_1, B_1, acc) ...
-//     (features past N and padded columns are zeros).  For the volume p = 1 neighbourhood the even
-//     chunks are node rows dy = 0, 1 of each plane and the odd ones dy = 2, 3, so a kernel walking
-//     cell rows can load the next row's fragments into the registers of this row's first half;
+//   * features are taken in steps of 8; per step ONE v_mfma_f32_16x16x32_bf16 with
+//         K = 32 = [hi_0, lo_0, ..., hi_7, lo_7 | the same 16] x [u1 of the step | u2 of the step],
+//     accumulated from the bias in step order: acc = b[k]; acc = mfma(A_0, B_0, acc); ...
+//     (features past N and padded columns are zeros).  Step t, lane half h, element i takes feature
+//     step_feature(nsp, p, t, h, i) of the reference's order (features_from_lowres,
+//     volume/utils.py:199-210: n = dz (2p+2)^2 + dy (2p+2) + dx):
+//       - the volume p = 1 neighbourhood (4 x 4 x 4 nodes): step t = 2 dy + e holds node row dy of
+//         the planes dz = 2 e + h, nodes dx = i -- one node row per step and plane pair, so a kernel
+//         walking the node rows of a plane block reads each row's fragment once and applies it to
+//         the four cell rows that share it (dy = 0 .. 3 of rows Y .. Y-3; kmp_codec_linear3pm.hip);
+//       - every other neighbourhood: 8 consecutive features per chunk q (4 h + i within it), the
+//         even chunks first, then the odd ones (chunk_at);
 //   * then the sample dtype's truncating, saturating cast (XLA astype).
 // Error: <= 2^-18 sum|f w| from the split plus the f32 accumulation inside the MFMA, well within
 // 1e-5 of sum|f w| + |b| (tests/test_gpu_linear.py).  An MFMA output element depends only on its
@@ -39,6 +43,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // the i-th chunk (of nq) in accumulation order: 0, 2, 4, ..., then 1, 3, 5, ...
 __host__ __device__ constexpr int chunk_at(int i, int nq) {
   return i < (nq + 1) / 2 ? 2 * i : 2 * (i - (nq + 1) / 2) + 1;
+}
+
+// the feature (reference order) of accumulation step t (of nq = ceil(N / 8)), lane half h, element i
+__host__ __device__ constexpr int step_feature(int nsp, int p, int nq, int t, int h, int i) {
+  return (nsp == 3 && p == 1) ? (2 * (t & 1) + h) * 16 + (t >> 1) * 4 + i : 8 * chunk_at(t, nq) + 4 * h + i;
 }
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN)
@@ -70,13 +79,16 @@ __device__ __forceinline__ uint32_t feature_dword(uint32_t v) {
   return __builtin_amdgcn_perm(fl, fh, 0x07060302u);  // {fh[31:16], fl[31:16]} -> low, high
 }
 
-// B fragment of one chunk for the lane of group g, column weights Wcol[n * ldw] (n < N, else 0):
-// element j of K = 8g + j -> feature 8q + 4(g & 1) + (j >> 1), byte j & 1 (0 = hi), term g >> 1
-__device__ __forceinline__ u32x4 b_fragment(const float* Wcol, int ldw, int N, int q, int g, bool valid) {
+// B fragment of accumulation step t for the lane of group g, column weights Wcol[n * ldw] (n < N,
+// else 0): element j of K = 8g + j -> feature step_feature(nsp, p, nq, t, g & 1, j >> 1), byte j & 1
+// (0 = hi), term g >> 1
+__device__ __forceinline__ u32x4 b_fragment(const float* Wcol, int ldw, int N, int nsp, int p, int t, int g,
+                                            bool valid) {
+  const int nq = (N + 7) / 8;
   u32x4 r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int n = 8 * q + 4 * (g & 1) + i;
+    const int n = step_feature(nsp, p, nq, t, g & 1, i);
     const float w = (valid && n < N) ? Wcol[(int64_t)n * ldw] : 0.0f;
     r[i] = weight_part(w, g >> 1, 1) | (weight_part(w, g >> 1, 0) << 16);
   }

@@ -108,8 +108,8 @@ __global__ void __launch_bounds__(64) linear3m_kernel(M3 a) {
   // the tile gets zero weights and bias: its channels are 0, as the aggregation's masks want ----
   const int chP = kPch[m], chQ = kQch[m];
   const bool okP = chP >= 0 && vz1, okQ = chQ >= 0 && vz0;
-  const bx::u32x4 bP = bx::b_fragment(a.W + (chP >= 0 ? chP : 0), 19, 8, 0, g, okP);
-  const bx::u32x4 bQ = bx::b_fragment(a.W + (chQ >= 0 ? chQ : 0), 19, 8, 0, g, okQ);
+  const bx::u32x4 bP = bx::b_fragment(a.W + (chP >= 0 ? chP : 0), 19, 8, 3, 0, 0, g, okP);
+  const bx::u32x4 bQ = bx::b_fragment(a.W + (chQ >= 0 ? chQ : 0), 19, 8, 3, 0, 0, g, okQ);
   const float biasP = okP ? a.b[chP] : 0.0f, biasQ = okQ ? a.b[chQ] : 0.0f;
 
   const int hplane = a.H * a.W_;

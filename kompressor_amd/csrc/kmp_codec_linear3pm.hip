@@ -98,7 +98,8 @@ __global__ void __launch_bounds__(64) fragments_kernel(const float* __restrict__
   for (int t = 0; t < 3; ++t) {  // C, Q, and a zero tile (the channels of a cell plane outside the tile)
     const int ch = t == 0 ? kCch[m] : t == 1 ? kQch[m] : -1;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) frag[(t * 8 + q) * 64 + lane] = bx::b_fragment(W + (ch >= 0 ? ch : 0), 19, 64, q, g, ch >= 0);
+    for (int q = 0; q < 8; ++q)
+      frag[(t * 8 + q) * 64 + lane] = bx::b_fragment(W + (ch >= 0 ? ch : 0), 19, 64, 3, 1, q, g, ch >= 0);
     fb[t * 64 + lane] = ch >= 0 ? bias[ch] : 0.0f;
   }
 }
@@ -170,7 +171,9 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     int par[3];
     map_parity(3, k, par);
     const int ez = par[0] ? a.Lcz : a.Ez;
-    mbase[k] = (T*)a.maps.p[k] + b * (int64_t)ez * lplane + lo_own;  // FULL: Lcy == Ey
+    // a uniform base per map (scalar registers) and the lane's 32-bit offset lo_own: no 64-bit
+    // pointer per map in vector registers
+    mbase[k] = (T*)a.maps.p[k] + b * (int64_t)ez * lplane;  // FULL: Lcy == Ey
   }
 
   // the lane's node row of node plane q (any q within one reflection of the axis)
@@ -194,7 +197,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
       for (int k = 0; k < 7; ++k) {
         int par[3];
         map_parity(3, k, par);
-        sv.mv[k] = ld8(mbase[k] + ((!par[0] || vz1) ? c : c - 1) * lplane);
+        sv.mv[k] = ld8(mbase[k] + (((!par[0] || vz1) ? c : c - 1) * lplane + lo_own));
       }
     } else {
       const T* p = hin + 2 * c * hplane;
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   T* const ctQ0 = m < 5 ? ctw + (14 + m) * CS + 4 * g : dmy + 4 * (m - 2);
   T* const ctQ1 = m < 5 ? ctw + (19 + m) * CS + 4 * g : dmy + 4 * ((m + 3) & 15);
   // the lane's A-fragment origin: ring slot 0, node row Y0 + (g & 1), node column m
-  const lds_cptr fl = (lds_cptr)st + (Y0 + (g & 1)) * PITCH + m;
+  const lds_cptr fl = (lds_cptr)st + Y0 * PITCH + m;
 
   // ---- staging: the node row of node plane q as feature dwords into ring slot q mod 5, plus
   // the mirrored halo columns / rows this lane is the source of (lsrc1) ----
@@ -266,59 +269,62 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     T* const ctQ = (c & 1) ? ctQ1 : ctQ0;
     // A fragment: node plane c - 1 + t (ring slot (c - 1 + t) mod 4), staged rows Y0 + ry + (g & 1),
     // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
-    lds_cptr fb[NPL][2];
+    // A fragment of plane pair e: this lane's plane c - 1 + 2 e + (g & 1) (ring slot mod 4), staged
+    // row Y0 + ry, cells x0 + m: one base per pair and half of the wave's rows, the rest immediate
+    // offsets
+    lds_cptr fb[2][2];
 #pragma unroll
-    for (int t = 0; t < NPL; ++t) {
-      fb[t][0] = fl + ((c - 1 + t + 2 * NPL) % NPL) * (NR * PITCH);
-      fb[t][1] = fb[t][0] + 5 * PITCH;
-      // opaque to the optimiser: otherwise it folds fb[t][1] back into fb[t][0] + a constant past
+    for (int e = 0; e < 2; ++e) {
+      fb[e][0] = fl + ((c - 1 + 2 * e + (g & 1) + 2 * NPL) % NPL) * (NR * PITCH);
+      fb[e][1] = fb[e][0] + 5 * PITCH;
+      // opaque to the optimiser: otherwise it folds fb[e][1] back into fb[e][0] + a constant past
       // ds_read2_b32's 8-bit offsets and pays a v_add_u32 per fragment half
-      asm volatile("" : "+v"(fb[t][0]));
-      asm volatile("" : "+v"(fb[t][1]));
+      asm volatile("" : "+v"(fb[e][0]));
+      asm volatile("" : "+v"(fb[e][1]));
     }
-    auto frag = [&](int t, int ry, int x0) {
-      const lds_cptr p = fb[t][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
+    auto frag = [&](int e, int ry, int x0) {
+      const lds_cptr p = fb[e][ry >= 5] + (ry >= 5 ? ry - 5 : ry) * PITCH + x0;
       return (bx::u32x4){p[0], p[1], p[2], p[3]};
     };
-    // tile rows by x tile, row parity, row pair: the C and Q tiles of a row read the same fragments
-    // (the same neighbourhood), and row Y's node rows 2, 3 (its odd chunks' fragments) are row Y+2's
-    // 0, 1 (its even chunks'): 4 fragments per row.  Two fragment sets alternate: once a row's even-chunk
-    // MFMAs have issued, their set receives the next row's odd-chunk fragments, so those LDS reads
-    // run under this row's odd-chunk MFMAs (no extra registers, no exposed LDS latency per row)
+    // per x tile, the node rows j = 0 .. ROWS+2 of the wave's rows (node row Y0-1+j): the two
+    // fragments of node row j (plane pairs 0, 1) feed accumulation steps 2 (j - r) + e of the cell
+    // rows r = j-3 .. j (C and Q tiles alike), so each fragment is read once and used by up to 4
+    // rows x 2 tiles; row r starts at j = r (from the bias) and is cast and stored after j = r + 3.
+    // The next node row's fragments are read while this one's MFMAs run.
+    constexpr int NJ = ROWS + 3;
 #pragma unroll
     for (int xt = 0; xt < TPR; ++xt) {
+      bx::u32x4 F[2][2];
+      F[0][0] = frag(0, 0, 16 * xt);
+      F[0][1] = frag(1, 0, 16 * xt);
+      bx::f32x4 aC[4], aQ[4];  // cell row r in slot r & 3
 #pragma unroll
-      for (int par = 0; par < 2; ++par) {
-        bx::u32x4 F[2][NPL];
-#pragma unroll
-        for (int t = 0; t < NPL; ++t) F[0][t] = frag(t, par, 16 * xt);
-#pragma unroll
-        for (int t = 0; t < NPL; ++t) F[1][t] = frag(t, par + 2, 16 * xt);
-#pragma unroll
-        for (int j = 0; j < ROWS / 2; ++j) {
-          const int row = par + 2 * j;
-          const int e = j & 1, o = e ^ 1;  // this row's even- / odd-chunk fragment sets
-          bx::f32x4 dC = {biasC, biasC, biasC, biasC}, dQ = {biasQ, biasQ, biasQ, biasQ};
-          // chunk q = 2 dz + h (plane offset dz, node rows 2h + 0 / 1), in chunk_at order: even q, then odd
-#pragma unroll
-          for (int dz = 0; dz < 4; ++dz) {
-            if (withC) dC = bx::mfma(F[e][dz], bC[2 * dz], dC);
-            dQ = bx::mfma(F[e][dz], bQ[2 * dz], dQ);
-          }
-          if (j + 1 < ROWS / 2) {
-#pragma unroll
-            for (int t = 0; t < NPL; ++t) F[e][t] = frag(t, row + 4, 16 * xt);
-          }
-#pragma unroll
-          for (int dz = 0; dz < 4; ++dz) {
-            if (withC) dC = bx::mfma(F[o][dz], bC[2 * dz + 1], dC);
-            dQ = bx::mfma(F[o][dz], bQ[2 * dz + 1], dQ);
-          }
-          static_assert(bx::chunk_at(3, 8) == 6 && bx::chunk_at(4, 8) == 1, "even chunks, then odd");
-          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(dC, hi);
-          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(dQ, hi);
-          hook(xt * ROWS + par * (ROWS / 2) + j);
+      for (int j = 0; j < NJ; ++j) {
+        const int cur = j & 1;
+        if (j + 1 < NJ) {
+          F[cur ^ 1][0] = frag(0, j + 1, 16 * xt);
+          F[cur ^ 1][1] = frag(1, j + 1, 16 * xt);
         }
+        if (j < ROWS) {
+          aC[j & 3] = (bx::f32x4){biasC, biasC, biasC, biasC};
+          aQ[j & 3] = (bx::f32x4){biasQ, biasQ, biasQ, biasQ};
+        }
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) {  // cell row r = j - dy: steps 2 dy + e in order
+          const int rr = j - dy;
+          if (rr < 0 || rr >= ROWS) continue;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            if (withC) aC[rr & 3] = bx::mfma(F[cur][e], bC[2 * dy + e], aC[rr & 3]);
+            aQ[rr & 3] = bx::mfma(F[cur][e], bQ[2 * dy + e], aQ[rr & 3]);
+          }
+        }
+        if (j >= 3) {  // cell row j - 3 is complete
+          const int row = j - 3;
+          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(aC[row & 3], hi);
+          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(aQ[row & 3], hi);
+        }
+        hook(xt * NJ + j);
       }
     }
   };
@@ -381,7 +387,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     auto put8 = [&](int k, const uint32_t (&res)[VX]) {
       int par[3];
       map_parity(3, k, par);
-      st8((!par[0] || vz1) ? mbase[k] + c * lplane : dummy, pack8<T, VX>(res));
+      st8((!par[0] || vz1) ? mbase[k] + (c * lplane + lo_own) : dummy, pack8<T, VX>(res));
     };
     const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own;
     T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
@@ -537,8 +543,9 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     __syncthreads();
     // the coder's vector work in four parts between the MFMA groups (an MFMA leaves 8 of its 16
     // cycles free for issue), not after the last one
-    channels(c, true, bC, bQ, biasC, biasQ, [&](int tr) {
-      if ((tr & 3) == 3) aggregate(c - 1, R0, Sp, ch, tr >> 2);
+    constexpr int NSTEP = TPR * (ROWS + 3);
+    channels(c, true, bC, bQ, biasC, biasQ, [&](int st_) {
+      if ((st_ + 1) * 4 / NSTEP != st_ * 4 / NSTEP) aggregate(c - 1, R0, Sp, ch, (st_ + 1) * 4 / NSTEP - 1);
     });
     __syncthreads();
   }

@@ -103,8 +103,8 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
 }
 
 // KMP_PRED_LINEAR_MFMA (kmp_bf16x2.h): one wave per 16-row tile (rows = (b, cell, c) as above),
-// the K outputs in column tiles of 16, per chunk of 8 features one v_mfma_f32_16x16x32_bf16 per
-// column tile.  u8 / u16 samples only (the byte split is exact for them).
+// the K outputs in column tiles of 16, per accumulation step (8 features, kmp_bf16x2.h
+// step_feature) one v_mfma_f32_16x16x32_bf16 per column tile.  u8 / u16 samples only (the byte split is exact for them).
 template <typename T>
 __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict__ src, LinSrc s, int nsp, int p,
                                                             int64_t B, int64_t C, const float* __restrict__ W,
@@ -129,16 +129,15 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
       const bool col_ok = k < K;
       const float bk = col_ok ? bias[k] : 0.0f;
       bx::f32x4 acc = {bk, bk, bk, bk};
-      for (int qi = 0; qi < nq; ++qi) {
-        const int q = bx::chunk_at(qi, nq);
+      for (int t = 0; t < nq; ++t) {  // accumulation steps (kmp_bf16x2.h step_feature)
         bx::u32x4 a;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int n = 8 * q + 4 * (g & 1) + i;
+          const int n = bx::step_feature(nsp, p, nq, t, g & 1, i);
           const uint32_t v = (row_ok && n < N) ? (uint32_t)lin_feature(src, s, nsp, p, b, c, C, z, y, x, n) : 0u;
           a[i] = bx::feature_dword(v);
         }
-        acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, q, g, col_ok), acc);
+        acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, nsp, p, t, g, col_ok), acc);
       }
       if (!col_ok) continue;
 #pragma unroll
