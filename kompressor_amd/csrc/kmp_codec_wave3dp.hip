@@ -322,9 +322,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // are the plane-block kernel's above.
 template <bool DEC>
 struct RollStep {
-  typename NodeRow<DEC>::V add_own, add_halo, sub_own, sub_halo, cur;  // cur: node plane c's own row
+  typename NodeRow<DEC>::V add_own, add_halo, cur;  // cur: node plane c's own row
   OutRows o;
 };
+
+// the VX node values of a lane's row segment packed into 8 bytes: the decode's lowres row as
+// loaded; the encode's highres row keeps its even elements (one byte permute per dword)
+template <typename T>
+__device__ __forceinline__ uint2 node_bytes(const uint2& v) { return v; }
+template <typename T>
+__device__ __forceinline__ uint2 node_bytes(const uint4& v) {
+  constexpr uint32_t sel = sizeof(T) == 2 ? 0x05040100u : 0x06040200u;
+  return make_uint2(__builtin_amdgcn_perm(v.y, v.x, sel), __builtin_amdgcn_perm(v.w, v.z, sel));
+}
 
 template <typename T, bool DEC, int P, bool STC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 3 : 1)))
@@ -425,17 +435,23 @@ wave3dr_kernel(W3P a) {
   // plane c-1 to c), node plane c's own row (the lowres / X map samples), the stream rows
   auto load_step = [&](int c, RollStep<DEC>& S) __attribute__((always_inline)) {
     load_node(c + P + 1, S.add_own, S.add_halo);
-    load_node(c - 1 - P, S.sub_own, S.sub_halo);
     if constexpr (DEC) S.cur = ld8c(lin + c * lplane + lo_own);
     else S.cur = ld16c(hin + 2 * c * hplane + ho_own);
     load_out(c, S.o);
   };
 
+  // The node values a step subtracts (node plane c-1-P, own and halo row) are the ones step
+  // c - (2P+2) added: each lane keeps its own in an LDS ring of 2P+2 slots (slot c mod 2P+2, read
+  // before the step overwrites it with plane c+P+1's), so a node row is read from memory once per
+  // run instead of twice -- no cross-lane traffic, no barrier (a lane reads back its own bytes)
+  __shared__ __attribute__((aligned(16))) uint4 zring[NB][256];
+  uint4* const zr = &zring[0][threadIdx.x];
   // z sums of cell plane c0-1 (node planes c0-1-P .. c0+P): the prologue's 2P+2 planes
   uint32_t zo[VX], zh[VX];
 #pragma unroll
   for (int i = 0; i < VX; ++i) zo[i] = zh[i] = 0;
   RollStep<DEC> S[PD + 1];
+  int zslot = c0 % NB;  // c mod NB
   {
     V own[NB], halo[NB];
 #pragma unroll
@@ -444,12 +460,17 @@ wave3dr_kernel(W3P a) {
     for (int k = 0; k < PD; ++k)
       if (c0 + k < c1) load_step(c0 + k, S[k]);
 #pragma unroll
-    for (int t = 0; t < NB; ++t)
+    for (int t = 0; t < NB; ++t) {
+      const uint2 no = node_bytes<T>(own[t]), nh = node_bytes<T>(halo[t]);
+      // prologue plane t is the one step c0 + t subtracts
+      const int sl = zslot + t < NB ? zslot + t : zslot + t - NB;
+      zr[sl * 256] = make_uint4(no.x, no.y, nh.x, nh.y);
 #pragma unroll
       for (int i = 0; i < VX; ++i) {
-        zo[i] += node_el<T, DEC>(own[t], i);
-        zh[i] += node_el<T, DEC>(halo[t], i);
+        zo[i] += el8<T>(no, i);
+        zh[i] += el8<T>(nh, i);
       }
+    }
   }
 
   auto xbox = [&](const uint32_t (&z)[VX], uint32_t (&out)[VX]) __attribute__((always_inline)) {
@@ -517,10 +538,16 @@ wave3dr_kernel(W3P a) {
   // one output plane: Sc holds its loads; plane c+PD's loads go into Sn first
   auto step = [&](int c, RollStep<DEC>& Sc, RollStep<DEC>& Sn) __attribute__((always_inline)) {
     if (c + PD < c1) load_step(c + PD, Sn);  // in flight during planes c .. c+PD-1
+    {
+      const uint4 sub = zr[zslot * 256];  // node plane c-1-P, added by step c - NB
+      const uint2 ao = node_bytes<T>(Sc.add_own), ah = node_bytes<T>(Sc.add_halo);
+      zr[zslot * 256] = make_uint4(ao.x, ao.y, ah.x, ah.y);
+      zslot = zslot + 1 < NB ? zslot + 1 : 0;
 #pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      zo[i] += node_el<T, DEC>(Sc.add_own, i) - node_el<T, DEC>(Sc.sub_own, i);
-      zh[i] += node_el<T, DEC>(Sc.add_halo, i) - node_el<T, DEC>(Sc.sub_halo, i);
+      for (int i = 0; i < VX; ++i) {
+        zo[i] += el8<T>(ao, i) - el8<T>(make_uint2(sub.x, sub.y), i);
+        zh[i] += el8<T>(ah, i) - el8<T>(make_uint2(sub.z, sub.w), i);
+      }
     }
     cell_means(Mo[1], Ma[1]);  // all lanes (shuffles)
     if (live) {

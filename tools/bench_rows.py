@@ -386,16 +386,21 @@ def main():
                 kom.container.compress(path, host, pred, levels=levels)
                 assert np.array_equal(kom.container.decompress(path), host)
                 tc, td_ = [], []
+                splits_c, splits_d = [], []
                 for _ in range(max(3, args.reps // 2)):
                     t = time.perf_counter()
                     info = kom.container.compress(path, host, pred, levels=levels)
                     tc.append(time.perf_counter() - t)
-                    split_c = dict(kom.container.last_timing)
+                    splits_c.append(dict(kom.container.last_timing))
                     t = time.perf_counter()
-                    kom.container.decompress(path)
+                    back = kom.container.decompress(path)  # kept: freeing the 256 MiB result is the caller's
                     td_.append(time.perf_counter() - t)
-                    split_d = dict(kom.container.last_timing)
+                    splits_d.append(dict(kom.container.last_timing))
+                    del back
                 tcm, tdm = float(np.median(tc)), float(np.median(td_))
+                # the split of the median repetition, and the wall time it leaves outside its parts
+                split_c = dict(splits_c[int(np.argsort(tc)[len(tc) // 2])], wall=tcm)
+                split_d = dict(splits_d[int(np.argsort(td_)[len(td_) // 2])], wall=tdm)
                 tag = f'file_l{levels}'
                 for name, tm, split in (('compress', tcm, split_c), ('decompress', tdm, split_d)):
                     print(json.dumps({'row': f'{tag}:{name}', 'what': f'numpy 512^3 u16 (512 x 64^3) -> file -> numpy, '

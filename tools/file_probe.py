@@ -108,6 +108,26 @@ def main():
     for k in (2, 4, 8):
         emit(f'file pwrite from pinned, {k} threads', wall(lambda: pwrite_par(k)), nb)
 
+    import mmap
+
+    def mmap_write_par(k):
+        # the file sized first, then filled through a shared mapping by k threads (page faults of
+        # one file's mapping run in parallel; write() serialises on the inode)
+        fd = os.open(out, os.O_RDWR | os.O_CREAT | os.O_TRUNC)
+        try:
+            os.ftruncate(fd, nb)
+            mm = mmap.mmap(fd, nb, mmap.MAP_SHARED, mmap.PROT_WRITE | mmap.PROT_READ)
+            dst = np.frombuffer(mm, dtype=np.uint8)
+            step = (nb + k - 1) // k
+            list(pool.map(lambda i: np.copyto(dst[i * step:min(nb, (i + 1) * step)], pin_np[i * step:min(nb, (i + 1) * step)]),
+                          range(k)))
+            del dst
+            mm.close()
+        finally:
+            os.close(fd)
+    for k in (1, 4, 8):
+        emit(f'file write via mmap from pinned, {k} threads', wall(lambda: mmap_write_par(k)), nb)
+
     def pread_par(k):
         fd = os.open(path, os.O_RDONLY)
         try:
