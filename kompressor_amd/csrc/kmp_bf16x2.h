@@ -117,5 +117,20 @@ __device__ __forceinline__ uint2 cast_pack4(const f32x4& v, float hi) {
   }
 }
 
+// u16 without a clamp instruction: v_cvt_u32_f32 (truncates; NaN and negatives 0; saturates) and
+// v_cvt_pk_u16_u32 (saturates to 65535) are XLA's astype to uint16 exactly -- 6 instead of 10 VALU
+// per 4 samples.  The conversion is inline asm because a C++ float -> unsigned conversion of an
+// out-of-range value is undefined; the asm reads an MFMA's D, a hazard hipcc does not pad inside an
+// asm string: s_nop 7 = the 8 wait states of a 4-pass XDL write -> VALU read on gfx950 (the
+// 16-cycle v_mfma_f32_16x16x32_bf16; an 8-pass one needs 12)
+__device__ __forceinline__ uint2 cast_pack4_u16(const f32x4& v) {
+  uint32_t u0, u1, u2, u3;
+  asm("s_nop 7\n\tv_cvt_u32_f32 %0, %4\n\tv_cvt_u32_f32 %1, %5\n\tv_cvt_u32_f32 %2, %6\n\tv_cvt_u32_f32 %3, %7"
+      : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+  return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u0, u1)),
+                    __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u2, u3)));
+}
+
 }  // namespace bx
 }  // namespace kmp

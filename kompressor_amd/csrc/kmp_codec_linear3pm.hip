@@ -260,13 +260,13 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   // ---- the channels of cell plane c on the matrix cores, into the wave's channel table: its C
   // channels (skipped with withC = false) and its Q channels (into the slots of parity c & 1).  A
   // cell plane outside the tile (c < 0 or c >= Lcz) has channels 0, what the aggregation's masks
-  // want: the cast's upper clamp is 0 for it ----
+  // want: its computed channels are overwritten with zeros ----
   // hook(tr) runs after tile row tr (0 .. 2 ROWS - 1): the caller's vector work placed between the
   // MFMA groups in program order
   auto channels = [&](int c, bool withC, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC,
                       float biasQ, auto&& hook) {
-    const float hi = c >= 0 && c < a.Lcz ? 65535.0f : 0.0f;
     T* const ctQ = (c & 1) ? ctQ1 : ctQ0;
+    constexpr int NJ = ROWS + 3;
     // A fragment: node plane c - 1 + t (ring slot (c - 1 + t) mod 4), staged rows Y0 + ry + (g & 1),
     // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
     // A fragment of plane pair e: this lane's plane c - 1 + 2 e + (g & 1) (ring slot mod 4), staged
@@ -291,7 +291,6 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     // rows r = j-3 .. j (C and Q tiles alike), so each fragment is read once and used by up to 4
     // rows x 2 tiles; row r starts at j = r (from the bias) and is cast and stored after j = r + 3.
     // The next node row's fragments are read while this one's MFMAs run.
-    constexpr int NJ = ROWS + 3;
 #pragma unroll
     for (int xt = 0; xt < TPR; ++xt) {
       bx::u32x4 F[2][2];
@@ -321,11 +320,20 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
         }
         if (j >= 3) {  // cell row j - 3 is complete
           const int row = j - 3;
-          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4<T>(aC[row & 3], hi);
-          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4<T>(aQ[row & 3], hi);
+          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16(aC[row & 3]);
+          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16(aQ[row & 3]);
         }
         hook(xt * NJ + j);
       }
+    }
+    if (c < 0 || c >= a.Lcz) {  // (uniform; the tile's first / last plane) overwritten with zeros
+#pragma unroll
+      for (int xt = 0; xt < TPR; ++xt)
+#pragma unroll
+        for (int row = 0; row < ROWS; ++row) {
+          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = make_uint2(0, 0);
+          *(uint2*)(ctQ + row * EX + 16 * xt) = make_uint2(0, 0);
+        }
     }
   };
 
@@ -355,10 +363,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   // slot per lane in the workspace, so the store needs no branch
   T* const dummy = (T*)((char*)a.frag + kFragBytes) + 8 * lane;
 
+  constexpr int kAggParts = 7;
   // ---- the maps / coder of output plane c from its channels (linear3dp's aggregation): channel k
   // of the lane's cells X .. X+3 at index 1 .. 4 ----
-  // part 0: the lowres and X map; 1: Z, UD; 2: Y, FB; 3: LR, C
-  auto aggregate = [&](int c, const V& own, const Streams& sv, const Chan& ch, int part) {
+  // part 0: the lowres and X map; 1: Z; 2: UD; 3: Y; 4: FB; 5: LR; 6: C (the decode's Z, Y, LR
+  // values wait in ``keep`` for the map stored in the same highres row)
+  auto aggregate = [&](int c, const V& own, const Streams& sv, const Chan& ch, int part, uint32_t (&keep)[VX]) {
     const bool vz1 = c < a.Lcz, vz0 = c >= 1;
     auto rd = [&](int k, uint32_t (&v)[VX + 1]) {
 #pragma unroll
@@ -422,76 +432,76 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     }
     // Z map (1,0,0): ch7 (y,x) ch8 (y,x-1) ch9 (y-1,x-1) ch10 (y-1,x);  UD (1,0,1): ch2, ch3
     if (part == 1) {
-      uint32_t P7[VX + 1], P8[VX + 1], P2[VX + 1];
-      uint32_t pZ[VX], pU[VX], oZ[VX], oU[VX];
+      uint32_t P7[VX + 1], P8[VX + 1], pZ[VX];
       rd(7, P7);
       rd(8, P8);
-      rd(2, P2);
       left(P8);
 #pragma unroll
       for (int i = 0; i < VX; ++i) {
         const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
         pZ[i] = (P7[i + 1] + mk(P8, i) + mk(A9, i) + A10[i + 1]) >> ((ny * nx) >> 1);
-        pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
       }
-      code(4, pZ, sv.o0, 0, oZ);
+      code(4, pZ, sv.o0, 0, keep);
+      if constexpr (!DEC) put8(4, keep);
+    }
+    if (part == 2) {
+      uint32_t P2[VX + 1], pU[VX], oU[VX];
+      rd(2, P2);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
       code(1, pU, sv.o0, 1, oU);
-      if constexpr (DEC) {
-        st16(vz1 ? h0 + hplane : dummy, pack16<T, VX>(oZ, oU));
-      } else {
-        put8(4, oZ);
-        put8(1, oU);
-      }
+      if constexpr (DEC) st16(vz1 ? h0 + hplane : dummy, pack16<T, VX>(keep, oU));
+      else put8(1, oU);
     }
     // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
-    if (part == 2) {
-      uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], P4[VX + 1], Q5[VX + 1];
-      uint32_t pY[VX], pF[VX], oY[VX], oF[VX];
+    if (part == 3) {
+      uint32_t P11[VX + 1], P12[VX + 1], Q13[VX + 1], Q14[VX + 1], pY[VX];
       rd(11, P11);
       rd(12, P12);
       rd(13, Q13);
       rd(14, Q14);
-      rd(4, P4);
-      rd(5, Q5);
       left(P12);
       left(Q13);
 #pragma unroll
       for (int i = 0; i < VX; ++i) {
         const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
         pY[i] = (P11[i + 1] + mk(P12, i) + mk(Q13, i) + Q14[i + 1]) >> ((nz * nx) >> 1);
-        pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
       }
-      code(5, pY, sv.e1, 0, oY);
+      code(5, pY, sv.e1, 0, keep);
+      if constexpr (!DEC) put8(5, keep);
+    }
+    if (part == 4) {
+      uint32_t P4[VX + 1], Q5[VX + 1], pF[VX], oF[VX];
+      rd(4, P4);
+      rd(5, Q5);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
       code(2, pF, sv.e1, 1, oF);
-      if constexpr (DEC) {
-        st16(h0 + a.W_, pack16<T, VX>(oY, oF));
-      } else {
-        put8(5, oY);
-        put8(2, oF);
-      }
+      if constexpr (DEC) st16(h0 + a.W_, pack16<T, VX>(keep, oF));
+      else put8(2, oF);
     }
     // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
-    if (part == 3) {
-      uint32_t P0[VX + 1], P1[VX + 1], P6[VX + 1];
-      uint32_t pL[VX], pC[VX], oL[VX], oC[VX];
+    if (part == 5) {
+      uint32_t P0[VX + 1], P1[VX + 1], pL[VX];
       rd(0, P0);
       rd(1, P1);
-      rd(6, P6);
       left(P1);
 #pragma unroll
       for (int i = 0; i < VX; ++i) {
         const uint32_t nx = (uint32_t)vx[i] + (uint32_t)vx[i + 1];
         pL[i] = (P0[i + 1] + mk(P1, i)) >> (nx >> 1);
-        pC[i] = P6[i + 1];
       }
-      code(0, pL, sv.o1, 0, oL);
+      code(0, pL, sv.o1, 0, keep);
+      if constexpr (!DEC) put8(0, keep);
+    }
+    if (part == 6) {
+      uint32_t P6[VX + 1], pC[VX], oC[VX];
+      rd(6, P6);
+#pragma unroll
+      for (int i = 0; i < VX; ++i) pC[i] = P6[i + 1];
       code(3, pC, sv.o1, 1, oC);
-      if constexpr (DEC) {
-        st16(vz1 ? h0 + hplane + a.W_ : dummy, pack16<T, VX>(oL, oC));
-      } else {
-        put8(0, oL);
-        put8(3, oC);
-      }
+      if constexpr (DEC) st16(vz1 ? h0 + hplane + a.W_ : dummy, pack16<T, VX>(keep, oC));
+      else put8(3, oC);
     }
   };
 
@@ -523,6 +533,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   __syncthreads();
   Streams Sp, Sc;
   Chan ch;
+  uint32_t keep[VX];
   // plane cb: no coder work yet
   stage(R3, cb + 2);
   V R4 = node_row(cb + 3 < ce + 2 ? cb + 3 : cb + 2);
@@ -541,17 +552,18 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     R4 = node_row(c + 1 < ce ? c + 3 : c + 2);  // the last step re-reads a plane (unused)
     load_streams(c, Sc);
     __syncthreads();
-    // the coder's vector work in four parts between the MFMA groups (an MFMA leaves 8 of its 16
-    // cycles free for issue), not after the last one
+    // the coder's vector work in kAggParts parts between the MFMA groups (an MFMA leaves 8 of its
+    // 16 cycles free for issue), not after the last one
     constexpr int NSTEP = TPR * (ROWS + 3);
     channels(c, true, bC, bQ, biasC, biasQ, [&](int st_) {
-      if ((st_ + 1) * 4 / NSTEP != st_ * 4 / NSTEP) aggregate(c - 1, R0, Sp, ch, (st_ + 1) * 4 / NSTEP - 1);
+      if ((st_ + 1) * kAggParts / NSTEP != st_ * kAggParts / NSTEP)
+        aggregate(c - 1, R0, Sp, ch, (st_ + 1) * kAggParts / NSTEP - 1, keep);
     });
     __syncthreads();
   }
   fetch(ch, ce & 1);
 #pragma unroll
-  for (int part = 0; part < 4; ++part) aggregate(ce - 1, R1, Sc, ch, part);
+  for (int part = 0; part < kAggParts; ++part) aggregate(ce - 1, R1, Sc, ch, part, keep);
 }
 
 }  // namespace l3q
