@@ -453,14 +453,14 @@ def _ptrs(tensors):
 def workspace_bytes(h, predictor, nsp):
     """Device workspace the fused calls may need for highres ``h`` (0 on the one-pass path)."""
     B, sp, C = h.shape[0], _sp(h.shape, nsp), _C(h.shape, nsp)
-    pstruct = predictor._kmp_predictor()
+    pstruct = predictor._kmp_predictor(h.dtype)
     fn = lib.kmp_volume_workspace_bytes if nsp == 3 else lib.kmp_image_workspace_bytes
     return int(fn(dev.dtype_code(h), B, *sp, C, ctypes.byref(pstruct)))
 
 
 def fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=None, workspace=None):
     B, sp, C = h.shape[0], _sp(h.shape, nsp), _C(h.shape, nsp)
-    pstruct = predictor._kmp_predictor()
+    pstruct = predictor._kmp_predictor(h.dtype)
     if nsp == 3:
         need = lib.kmp_volume_workspace_bytes(dev.dtype_code(h), B, *sp, C, ctypes.byref(pstruct))
     else:
@@ -478,7 +478,7 @@ def fused_encode_into(h, predictor, coder, lowres, maps, nsp, region=None, works
 
 def fused_decode_into(lowres, maps, dims, predictor, coder, out, nsp, region=None, workspace=None):
     B, E, C = lowres.shape[0], _sp(lowres.shape, nsp), _C(lowres.shape, nsp)
-    pstruct = predictor._kmp_predictor()
+    pstruct = predictor._kmp_predictor(lowres.dtype)
     hs = [2 * e - 1 + d for e, d in zip(E, dims)]
     if nsp == 3:
         need = lib.kmp_volume_workspace_bytes(dev.dtype_code(lowres), B, *hs, C, ctypes.byref(pstruct))

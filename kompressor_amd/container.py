@@ -49,11 +49,14 @@ _NP_NAME = {torch.uint8: 'uint8', torch.uint16: 'uint16', torch.int32: 'int32', 
             torch.float32: 'float32'}
 
 
-def _predictor_meta(predictor, padding, ndim):
+def _predictor_meta(predictor, padding, ndim, dtype):
+    """(``dtype``: the coded samples' torch dtype -- a LinearPredictor's arithmetic is recorded
+    resolved for it, so a reader needs no rule for ``'auto'``)"""
     if isinstance(predictor, MeanPredictor):
         return {'kind': 'mean', 'padding': predictor.padding, 'ndim': predictor.ndim}
     if isinstance(predictor, LinearPredictor):
-        return {'kind': 'linear', 'padding': predictor.padding, 'ndim': predictor.ndim, 'arith': predictor.arith,
+        return {'kind': 'linear', 'padding': predictor.padding, 'ndim': predictor.ndim,
+                'arith': predictor.arith_for(dtype),
                 'weights': predictor.weights.tolist(), 'bias': predictor.bias.tolist()}
     # an opaque predictions_fn: recorded by name; decoding needs the caller to pass it again
     return {'kind': 'external', 'padding': padding, 'ndim': ndim,
@@ -152,7 +155,7 @@ def save(path, lowres, encoded, predictor=None, padding=None, ndim=None, method=
             'method': method, 'lowres_shape': list(lo_t.shape), 'lowres_dtype': _NP_NAME[lo_t.dtype],
             'map_dtype': _NP_NAME[maps_t[0].dtype],
             'sample_dtype': sample_dtype or _NP_NAME[lo_t.dtype],
-            'predictor': _predictor_meta(predictor, padding, ndim) if predictor is not None else None}
+            'predictor': _predictor_meta(predictor, padding, ndim, lo_t.dtype) if predictor is not None else None}
     blob, total, crc = _bundle(lo_t, maps_t, dims, method)
     return _write(path, meta, blob, total, crc, t0)
 
@@ -251,7 +254,7 @@ def compress(path, highres, predictor, levels='auto', method='rice'):
         x = lowres
     meta = {'format': 'kompressor_amd', 'ndim': ndim, 'padding': padding, 'method': method,
             'sample_dtype': sample, 'levels': meta_levels, 'lowres_shape': list(x.shape),
-            'predictor': _predictor_meta(predictor, padding, ndim)}
+            'predictor': _predictor_meta(predictor, padding, ndim, x.dtype)}
     # one bundle: the coarsest lowres, then every level's maps finest first (no bundle dims: the
     # per-level dims live in the metadata)
     blob, total, crc = _bundle(x, arrays, (), method)
@@ -279,8 +282,9 @@ def decompress(path, predictor=None, as_numpy=True):
     if isinstance(pred, LinearPredictor) and meta['predictor'] and meta['predictor'].get('kind') == 'linear':
         # the two arithmetics are not bit-equal: decoding with the other one returns wrong samples
         arith = meta['predictor'].get('arith', 'f32')
-        if pred.arith != arith:
-            raise AssertionError(f"{path} was coded with arith='{arith}'; the predictor passed has arith='{pred.arith}'")
+        if pred.arith_for(lowres.dtype) != arith:
+            raise AssertionError(f"{path} was coded with arith='{arith}'; the predictor passed evaluates with "
+                                 f"arith='{pred.arith_for(lowres.dtype)}'")
     nmaps = _nd.NMAPS[ndim]
     levels = meta.get('levels') or [{'dims': list(bundle_dims)}]  # save(): one level, dims in the bundle
     if len(arrays) != nmaps * len(levels):

@@ -39,7 +39,7 @@ class MeanPredictor:
         self.padding, self.ndim = padding, ndim
         self.maps_dtype = None if maps_dtype is None else torch.float32
 
-    def _kmp_predictor(self):
+    def _kmp_predictor(self, dtype=None):
         return _lib.Predictor(_lib.PRED_MEAN, self.padding, None, None)
 
     def __call__(self, lowres):
@@ -52,7 +52,20 @@ class MeanPredictor:
         return f'MeanPredictor(padding={self.padding}, ndim={self.ndim}{md})'
 
 
-ARITHS = ('f32', 'bf16x2')
+ARITHS = ('auto', 'f32', 'bf16x2')
+
+
+def resolve_arith(arith, padding, ndim, dtype):
+    """The arithmetic a LinearPredictor evaluates with for samples of ``dtype``: ``'auto'`` is the
+    matrix-core form (``'bf16x2'``) for volumes with padding 1 and uint16 samples -- the learned-
+    predictor configuration SURVEY.md §8d prices, where the fused ``linear3pm`` kernel codes a C3
+    direction in about half the f32 chain's time (profiles/round5/rows_linear_auto_r5a1.log) -- and the
+    f32 chain everywhere else (padding 0, where the f32 kernel is the faster one; images; 8- and
+    32-bit samples).  A function of the predictor and the sample dtype only, so encode, decode,
+    chunked and whole-volume calls, and a file's reader all resolve it the same way."""
+    if arith != 'auto':
+        return arith
+    return 'bf16x2' if ndim == 3 and padding == 1 and dtype == torch.uint16 else 'f32'
 
 
 class LinearPredictor:
@@ -62,14 +75,16 @@ class LinearPredictor:
     ``arith`` picks the arithmetic, and every path (fused codec kernels, the callable, the generic
     codec) evaluates a predictor with the same one, so encode and decode agree bit for bit:
 
-    * ``'f32'`` (default): the k-ordered float32 fma chain from the bias -- bit-identical to the
-      oracle's restatement (``oracle.predictors.linear_fma_chain``);
+    * ``'f32'``: the k-ordered float32 fma chain from the bias -- bit-identical to the oracle's
+      restatement (``oracle.predictors.linear_fma_chain``);
     * ``'bf16x2'``: the matrix cores (kmp_bf16x2.h) -- features split into two exact bf16 bytes,
       weights into two bf16 terms, one ``v_mfma_f32_16x16x32_bf16`` per 8 features; within the north
       star's 1e-5 (relative to sum|f w| + |b|) of the float64 value rather than equal to the f32
-      chain.  uint8 / uint16 samples."""
+      chain.  uint8 / uint16 samples;
+    * ``'auto'`` (default): ``'bf16x2'`` where the matrix cores are the fast path (volumes, padding 1,
+      uint16 samples), ``'f32'`` elsewhere (:func:`resolve_arith`)."""
 
-    def __init__(self, weights, bias, padding=0, ndim=3, arith='f32'):
+    def __init__(self, weights, bias, padding=0, ndim=3, arith='auto'):
         if ndim not in (2, 3):
             raise ValueError('ndim must be 2 (image) or 3 (volume)')
         if arith not in ARITHS:
@@ -101,9 +116,13 @@ class LinearPredictor:
             self._b = self._b_host.to('cuda')
         return self._w, self._b
 
-    def _kmp_predictor(self):
+    def arith_for(self, dtype):
+        """The arithmetic for samples of ``dtype`` (``arith`` with ``'auto'`` resolved)."""
+        return resolve_arith(self.arith, self.padding, self.ndim, dtype)
+
+    def _kmp_predictor(self, dtype):
         w, b = self._device_params()
-        kind = _lib.PRED_LINEAR if self.arith == 'f32' else _lib.PRED_LINEAR_MFMA
+        kind = _lib.PRED_LINEAR if self.arith_for(dtype) == 'f32' else _lib.PRED_LINEAR_MFMA
         return _lib.Predictor(kind, self.padding, w.data_ptr(), b.data_ptr())
 
     def predict_cells(self, lowres, with_f32=False):
@@ -117,7 +136,7 @@ class LinearPredictor:
         shape = (t.shape[0], *cells, NPRED[nsp], *_ch(t.shape, nsp))
         out = dev.empty(shape, t.dtype)
         f32 = dev.empty(shape, torch.float32) if with_f32 else None
-        fn = lib.kmp_linear_predict if self.arith == 'f32' else lib.kmp_linear_predict_mfma
+        fn = lib.kmp_linear_predict if self.arith_for(t.dtype) == 'f32' else lib.kmp_linear_predict_mfma
         check(fn(nsp, dev.dtype_code(t), t.data_ptr(), t.shape[0], _lib.i64x3(S),
                                      _C(t.shape, nsp), self.padding, w.data_ptr(), b.data_ptr(), out.data_ptr(),
                                      f32.data_ptr() if f32 is not None else None, dev.stream()), 'linear_predict')
@@ -131,5 +150,5 @@ class LinearPredictor:
         return tuple(dev.from_device(m, kind) for m in d_maps_from_predictions(cells, self.ndim))
 
     def __repr__(self):
-        ar = '' if self.arith == 'f32' else f", arith='{self.arith}'"
+        ar = '' if self.arith == 'auto' else f", arith='{self.arith}'"
         return f'LinearPredictor(padding={self.padding}, ndim={self.ndim}{ar})'

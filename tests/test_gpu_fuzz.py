@@ -62,7 +62,7 @@ def test_random_configuration_matches_oracle(kom, seed):
         n, k = (2 * padding + 2) ** ndim, 19 if ndim == 3 else 5
         w = (1.0 / n + rng.standard_normal((n, k)) * (0.3 / n)).astype(np.float32)
         b = (rng.standard_normal(k) * 2).astype(np.float32)
-        pred, opf = kom.LinearPredictor(w, b, padding, ndim), OP.linear_predictions_fn(padding, w, b, ndim)
+        pred, opf = kom.LinearPredictor(w, b, padding, ndim, arith='f32'), OP.linear_predictions_fn(padding, w, b, ndim)
     else:
         pred, opf = kom.MeanPredictor(padding, ndim), OP.mean_predictions_fn(padding, ndim)
     enc, dec = getattr(ns, f'encode_values_{coder}'), getattr(ns, f'decode_values_{coder}')

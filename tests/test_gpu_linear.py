@@ -1,6 +1,7 @@
-"""LinearPredictor parity.  arith='f32' (default): float32 intermediates bit-exact to the oracle's
-fma chain and within the north star's 1e-5 of a float64 reference; residual maps bit-exact;
-lossless.  arith='bf16x2' (the matrix cores): see the section at the end."""
+"""LinearPredictor parity.  arith='f32': float32 intermediates bit-exact to the oracle's fma chain
+and within the north star's 1e-5 of a float64 reference; residual maps bit-exact; lossless.
+arith='bf16x2' (the matrix cores) and 'auto' (the default, one of the two by configuration): see
+the sections at the end."""
 
 import numpy as np
 import pytest
@@ -39,7 +40,7 @@ def test_linear_cell_predictions(kom, ndim, p, shape, dtype):
     hi = _data(shape, dtype, 1)
     w, b = _weights(ndim, p, 2, dtype)
     window = ons.pad_neighborhood(ons.lowres_from_highres(ons.pad_highres(hi)[0]), p)
-    pred = kom.LinearPredictor(w, b, p, ndim)
+    pred = kom.LinearPredictor(w, b, p, ndim, arith='f32')
     cells_t, cells_f = pred.predict_cells(window, with_f32=True)
     feats = ons.features_from_lowres(window, p)
     exact = OP.linear_fma_chain(feats, w, b)
@@ -57,7 +58,7 @@ def test_linear_codec(kom, ndim, p, shape, dtype):
     ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
     hi = _data(shape, dtype, 3)
     w, b = _weights(ndim, p, 4, dtype)
-    pred = kom.LinearPredictor(w, b, p, ndim)
+    pred = kom.LinearPredictor(w, b, p, ndim, arith='f32')
     enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if dtype == np.uint16 else \
                (ns.encode_values_uint8, ns.decode_values_uint8)
     oenc = ons.encode_values_uint16 if dtype == np.uint16 else ons.encode_values_uint8
@@ -73,7 +74,7 @@ def test_linear_codec(kom, ndim, p, shape, dtype):
 def test_linear_chunks(kom):
     hi = _data((2, 17, 16, 15, 1), np.uint16, 5)
     w, b = _weights(3, 1, 6, np.uint16)
-    pred = kom.LinearPredictor(w, b, 1, 3)
+    pred = kom.LinearPredictor(w, b, 1, 3, arith='f32')
     lo, (maps, dims) = kom.volume.encode(pred, kom.volume.encode_values_uint16, hi, padding=1)
     for chunk in (6, (6, 11, 7)):
         lo2, (maps2, dims2) = kom.volume.encode_chunks(pred, kom.volume.encode_values_uint16, hi, chunk=chunk, padding=1)
@@ -90,7 +91,7 @@ def test_linear_fused_p1(kom, shape):
     (chunked) launches, over lowres widths 4 .. 64 and partial last waves."""
     hi = _data(shape, np.uint16, 7)
     w, b = _weights(3, 1, 8, np.uint16)
-    pred = kom.LinearPredictor(w, b, 1, 3)
+    pred = kom.LinearPredictor(w, b, 1, 3, arith='f32')
     V, OV = kom.volume, oracle.volume
     want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
                                                 padding=1)
@@ -125,7 +126,7 @@ def test_linear_fused_p0(kom, shape, dtype, kernel):
     1 / 2 / 4 / 8 row steps for both sample sizes, and the general body."""
     hi = _data(shape, dtype, 9)
     w, b = _weights(3, 0, 10, dtype)
-    pred = kom.LinearPredictor(w, b, 0, 3)
+    pred = kom.LinearPredictor(w, b, 0, 3, arith='f32')
     V, OV = kom.volume, oracle.volume
     enc, dec, oenc = ((V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16) if dtype == np.uint16
                       else (V.encode_values_uint8, V.decode_values_uint8, OV.encode_values_uint8))
@@ -263,3 +264,45 @@ def test_linear_bf16x2_p1_fused_sweep(kom):
         assert torch.equal(rec, hi_t)
         rec_c = V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=chunk, padding=1)
         assert torch.equal(rec_c, hi_t)
+
+
+# ---- arith='auto' (the default) ----
+
+AUTO_CASES = [(3, 1, (2, 32, 32, 32, 1), np.uint16, 'bf16x2'), (3, 1, (1, 17, 30, 16, 1), np.uint16, 'bf16x2'),
+              (3, 0, (2, 32, 32, 32, 1), np.uint16, 'f32'), (3, 1, (2, 32, 32, 32, 1), np.uint8, 'f32'),
+              (2, 1, (2, 64, 64, 1), np.uint16, 'f32')]
+
+
+@pytest.mark.parametrize('ndim,p,shape,dtype,want', AUTO_CASES)
+def test_linear_auto_arith(kom, tmp_path, ndim, p, shape, dtype, want):
+    """arith='auto' evaluates with the matrix cores for volumes with padding 1 and uint16 samples and
+    with the f32 chain elsewhere: the same maps and lowres as the explicit arithmetic (fused kernels
+    and the callback path), lossless, chunk-invariant, and a file records the resolved arithmetic,
+    so a reader holding an explicit predictor of it decodes the file."""
+    hi = _data(shape, dtype, 11)
+    w, b = _weights(ndim, p, 12, dtype)
+    auto = kom.LinearPredictor(w, b, p, ndim)
+    explicit = kom.LinearPredictor(w, b, p, ndim, arith=want)
+    tdt = torch.uint16 if dtype == np.uint16 else torch.uint8
+    assert auto.arith == 'auto' and auto.arith_for(tdt) == want
+    ns = kom.volume if ndim == 3 else kom.image
+    enc, dec = (ns.encode_values_uint16, ns.decode_values_uint16) if dtype == np.uint16 else \
+               (ns.encode_values_uint8, ns.decode_values_uint8)
+    want_lo, (want_maps, want_dims) = ns.encode(explicit, enc, hi, padding=p)
+    for fn in (auto, lambda x: auto(x)):
+        lo, (maps, dims) = ns.encode(fn, enc, hi, padding=p)
+        assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+        assert all(np.array_equal(a, c) for a, c in zip(maps, want_maps))
+        assert np.array_equal(ns.decode(fn, dec, lo, (maps, dims), padding=p), hi)
+    if ndim == 3:
+        lo2, (maps2, _) = ns.encode_chunks(auto, enc, hi, chunk=7, padding=p)
+        assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
+        path = str(tmp_path / 'auto.kmp')
+        kom.container.compress(path, hi, auto)
+        assert kom.container.load(path)[2]['predictor']['arith'] == want
+        assert np.array_equal(kom.container.decompress(path), hi)
+        assert np.array_equal(kom.container.decompress(path, predictor=explicit), hi)
+        other = 'f32' if want == 'bf16x2' else 'bf16x2'
+        if dtype == np.uint16:
+            with pytest.raises(AssertionError):
+                kom.container.decompress(path, predictor=kom.LinearPredictor(w, b, p, ndim, arith=other))

@@ -237,3 +237,16 @@ def test_dispatch_options_are_a_table_not_the_environment():
     src = ''.join(open(os.path.join(ROOT, 'kompressor_amd', 'csrc', f)).read()
                   for f in os.listdir(os.path.join(ROOT, 'kompressor_amd', 'csrc')) if f != 'kmp_options.hip')
     assert 'getenv' not in src
+
+
+def test_linear_auto_arith_rule():
+    """LinearPredictor(arith='auto'), the default, resolves by configuration only: the matrix cores
+    (bf16x2) for volumes with padding 1 and uint16 samples, the f32 chain elsewhere."""
+    import torch
+    from kompressor_amd.predictors import resolve_arith
+    assert resolve_arith('auto', 1, 3, torch.uint16) == 'bf16x2'
+    for p, nd, dt in ((0, 3, torch.uint16), (2, 3, torch.uint16), (1, 3, torch.uint8), (1, 2, torch.uint16),
+                      (1, 3, torch.int32), (1, 3, torch.uint32)):
+        assert resolve_arith('auto', p, nd, dt) == 'f32'
+    for a in ('f32', 'bf16x2'):
+        assert resolve_arith(a, 1, 3, torch.uint16) == a

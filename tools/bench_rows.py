@@ -124,7 +124,7 @@ def main():
         n = (2 * p + 2) ** 3
         w = (1.0 / n + rng.standard_normal((n, 19)) * (0.3 / n)).astype(np.float32)
         b = np.zeros(19, np.float32)
-        codec_rows(f'volume_linear_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3),
+        codec_rows(f'volume_linear_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3, arith='f32'),
                    OP.linear_predictions_fn(p, w, b, 3), V.encode_values_uint16, V.decode_values_uint16,
                    OV.encode_values_uint16, OV.decode_values_uint16, p, raw_v, 3)
 
@@ -140,7 +140,7 @@ def main():
         n = (2 * p + 2) ** 2
         w = (1.0 / n + rng.standard_normal((n, 5)) * (0.3 / n)).astype(np.float32)
         b = np.zeros(5, np.float32)
-        codec_rows(f'image_linear_p{p}', I, OI, img, img_h, kom.LinearPredictor(w, b, p, 2),
+        codec_rows(f'image_linear_p{p}', I, OI, img, img_h, kom.LinearPredictor(w, b, p, 2, arith='f32'),
                    OP.linear_predictions_fn(p, w, b, 2), I.encode_values_uint8, I.decode_values_uint8,
                    OI.encode_values_uint8, OI.decode_values_uint8, p, raw_i, 2)
 

@@ -6,7 +6,7 @@ from kompressor_amd import _nd
 x = torch.from_numpy(np.random.default_rng(0).integers(0, 65536, size=(512, 64, 64, 64, 1)).astype(np.uint16)).cuda()
 rng = np.random.default_rng(1)
 w = (1.0 / 64 + rng.standard_normal((64, 19)) * (0.3 / 64)).astype(np.float32)
-pred = kom.LinearPredictor(w, np.zeros(19, np.float32), 1, 3)
+pred = kom.LinearPredictor(w, np.zeros(19, np.float32), 1, 3, arith='f32')
 coder = _nd.NATURAL_CODER[x.dtype]
 lo, maps, dims = _nd._alloc_encoded(x, coder, 3)
 rec = torch.empty_like(x)
