@@ -209,8 +209,8 @@ constexpr int kCatPF = 4;  // 8 measured no faster (r3s54: decode 394-397 vs 376
 // select (a histogram round is ~35 VALU, one to three rounds per element): a good predictor's ranks
 // (bench_rows decode_small_ranks, ranks < 4) stay on the peel.
 constexpr int kCatPeel = 4;
-// per wave: the 256 bins and 64 trash bins (one per lane), then the owner slots (trash included)
-constexpr int kCatTrash = 256, kCatOwn = 320;
+// per wave: the 256 bins, then the owner slots (bins[kCatOwn + d])
+constexpr int kCatOwn = 320;
 typedef float cat_f32x4 __attribute__((ext_vector_type(4)));
 
 template <int E4>
@@ -287,17 +287,6 @@ __device__ __forceinline__ uint64_t lanes_below(int nl) {  // mask of lanes 0 ..
   return nl <= 0 ? 0ull : nl >= 64 ? ~0ull : ((1ull << nl) - 1);
 }
 
-// two independent inclusive scans, their DPP steps alternating (half the hazard wait states)
-template <typename Op>
-__device__ __forceinline__ void wave_scan2_dpp(uint32_t& x, uint32_t& y, Op op) {
-#define KMP_STEP(CTRL, ROW)                                                                  \
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW, 0xf, false));     \
-  y = op(y, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, CTRL, ROW, 0xf, false));
-  KMP_STEP(0x111, 0xf) KMP_STEP(0x112, 0xf) KMP_STEP(0x114, 0xf) KMP_STEP(0x118, 0xf)
-  KMP_STEP(0x142, 0xa) KMP_STEP(0x143, 0xc)
-#undef KMP_STEP
-}
-
 // ---- decode: keys, rank, radix select ----------------------------------------------------------
 // Every logit in [+0, +inf] (softmax output, the reference's categorical predictor): the float bits
 // are already order-preserving -- no work per key when every class exists (FULL), + 1 to keep key 0
@@ -351,100 +340,6 @@ __device__ __forceinline__ uint32_t cat_dif(const uint32_t (&key)[E4][4], const 
   return dif;
 }
 
-// Radix select on digits of up to 8 bits from the top of the bits in which the keys differ (P of
-// them below the common prefix): per round a 256-bin LDS histogram of the digit over the keys in
-// the current range, a DPP scan over the bins in descending key order, the bin that holds rank k;
-// the range narrows to that bin.  Stops when the bin holds one key or the digits run out (ties).
-// Every key also writes its class into the owner slot of its bin (bins[kCatOwn + j]): when the
-// final bin holds one key, that slot names the class -- one LDS read, no ballots.
-//
-// The range is kept as its top key hi (the bits below the digits still to come all ones) and a
-// key's bin is j = (hi - key) >> sh: the digit counted DOWN from the range's top digit, so the bins
-// are in descending key order and every key outside the range lands past the range's bins (below
-// it: hi - key >= 2^(sh + wd), past bin 2^wd - 1; above it: hi - key wraps above 2^32 - 2^(sh + wd))
-// or, clamped, in the lane's trash bin.  The scan reaches rank k inside the range's bins before any
-// out-of-range count, so every key is counted unconditionally: no per-key branch (exec-mask save /
-// restore on the scalar unit).  A trash bin per lane: same-address LDS atomics serialise, and most
-// keys are out of range after the first round (one shared trash bin: 605 vs 268 us per 1 M x 256).
-struct CatSel {  // one element's select state, wave-uniform
-  uint32_t hi;    // the range's top key
-  uint32_t c_hi;  // keys above the range
-  uint32_t cnt;   // keys in the last picked bin
-  uint32_t jb;    // the last picked bin
-  uint32_t k;     // the rank
-  int sh;         // the digit's low bit
-  __device__ bool more() const { return cnt > 1u && sh != 0; }
-};
-
-__device__ __forceinline__ void cat_sel_init(CatSel& s, uint32_t dif, uint32_t k0, uint32_t k) {
-  const int P = dif == 0 ? 0 : 32 - __clz((int)dif);
-  s.sh = s_floor_sub(P, 8);  // digit = bits [sh, P)
-  s.hi = P >= 32 ? 0xffffffffu : k0 | ((1u << P) - 1u);
-  s.c_hi = 0;
-  s.cnt = 0;
-  s.jb = 0;
-  s.k = k;
-}
-
-// FIRST: the first round, where every valid key is in the range (they share the bits above P)
-template <int E4, bool FIRST>
-__device__ __forceinline__ void cat_hist(const uint32_t (&key)[E4][4], const bool (&ok)[E4][4], const CatSel& s,
-                                         uint32_t* bins, int lane) {
-  const uint32_t trash = (uint32_t)(kCatTrash + lane);
-#pragma unroll
-  for (int e = 0; e < E4; ++e)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t j = (s.hi - key[e][q]) >> s.sh;
-      if (!FIRST) j = min(j, trash);
-      j = ok[e][q] ? j : trash;
-      atomicAdd(bins + j, 1u);
-      bins[kCatOwn + j] = (uint32_t)(e * 256 + 4 * lane + q);
-    }
-}
-
-// The bin that holds rank k: its count; the keys above it into c_hi; the range narrows to it.
-// Each lane finds the bin of its 4 (bins 4 lane .. 4 lane + 3) that would hold rank k on the VALU,
-// branch-free (cat_pick_lane), and one readlane of the first lane whose inclusive count passes k
-// returns the keys before the bin, its count and its index (cat_pick_take).
-__device__ __forceinline__ uint32_t cat_pick_lane(const uint4& bu, uint32_t incl, uint32_t tot, uint32_t r) {
-  const uint32_t c1 = bu.x, c2 = c1 + bu.y, c3 = c2 + bu.z;
-  const uint32_t excl = incl - tot, rl = r - excl;
-  const bool s1 = rl >= c1, s2 = rl >= c2, s3 = rl >= c3;
-  const uint32_t lo = s3 ? c3 : s2 ? c2 : s1 ? c1 : 0u;
-  const uint32_t up = s3 ? tot : s2 ? c3 : s1 ? c2 : c1;
-  const uint32_t q = s3 ? 3u : s2 ? 2u : s1 ? 1u : 0u;
-  return (excl + lo) | ((up - lo) << 10) | (q << 20);  // counts <= 512
-}
-__device__ __forceinline__ void cat_pick_take(CatSel& s, uint32_t pk, uint32_t incl, uint32_t r) {
-  const int ls = (int)__builtin_ctzll(__ballot(r < incl));  // incl ascends over the lanes
-  const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pk, ls);
-  s.c_hi += v & 1023u;
-  s.cnt = (v >> 10) & 1023u;
-  s.jb = 4u * (uint32_t)ls + (v >> 20);
-  s.hi -= s.jb << s.sh;
-}
-__device__ __forceinline__ uint32_t cat_bin_total(const uint4& bu) { return bu.x + bu.y + bu.z + bu.w; }
-__device__ __forceinline__ void cat_pick1(CatSel& s, const uint32_t* bins, int lane) {
-  __builtin_amdgcn_wave_barrier();
-  const uint4 bu = *(const uint4*)(bins + 4 * lane);
-  const uint32_t tot = cat_bin_total(bu);
-  const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
-  const uint32_t r = s.k - s.c_hi;
-  cat_pick_take(s, cat_pick_lane(bu, incl, tot, r), incl, r);
-}
-__device__ __forceinline__ void cat_pick2(CatSel& sa, const uint32_t* ba, CatSel& sb, const uint32_t* bb, int lane) {
-  __builtin_amdgcn_wave_barrier();
-  const uint4 ua = *(const uint4*)(ba + 4 * lane), ub = *(const uint4*)(bb + 4 * lane);
-  const uint32_t ta = cat_bin_total(ua), tb = cat_bin_total(ub);
-  uint32_t ia = ta, ib = tb;
-  wave_scan2_dpp(ia, ib, [](uint32_t a, uint32_t c) { return a + c; });
-  const uint32_t ra = sa.k - sa.c_hi, rb = sb.k - sb.c_hi;
-  const uint32_t pa = cat_pick_lane(ua, ia, ta, ra), pb = cat_pick_lane(ub, ib, tb, rb);
-  cat_pick_take(sa, pa, ia, ra);
-  cat_pick_take(sb, pb, ib, rb);
-}
-
 // the m-th highest class index among the keys whose ballots are w (ties: lanes from the highest,
 // within a lane q from 3 down)
 template <int E4>
@@ -478,24 +373,6 @@ __device__ __forceinline__ int cat_dec_walk(const uint64_t (&w)[E4][4], uint32_t
     }
   }
   return 0;
-}
-
-// the class of rank k once the select has stopped: the final bin's owner slot when it holds one
-// key (the final round's writes precede this read in the wave's LDS order), otherwise the
-// (k - c_hi)-th highest class index among the keys in [hi - span, hi] (ties); padding keys (0) are
-// below every valid key (>= 1), so without FULL the range starts at 1 at the least
-template <int E4, bool FULL>
-__device__ __forceinline__ int cat_dec_class(const uint32_t (&key)[E4][4], const CatSel& s, const uint32_t* bins) {
-  if (s.cnt == 1u) return __builtin_amdgcn_readfirstlane((int)bins[kCatOwn + s.jb]);
-  const uint32_t span = (1u << s.sh) - 1u;  // sh <= 24
-  const uint32_t t = s.hi - span;
-  const uint32_t tlo = FULL || t > 0 ? t : 1u, ext = s.hi - tlo;
-  uint64_t w[E4][4];
-#pragma unroll
-  for (int e = 0; e < E4; ++e)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w[e][q] = __ballot(key[e][q] - tlo <= ext);
-  return cat_dec_walk<E4>(w, s.k - s.c_hi);
 }
 
 template <typename T, int DIR, int E4, bool FULL>
@@ -576,84 +453,108 @@ __device__ __forceinline__ T cat_rank(const CatRow<E4>& cur, int64_t L, int lane
         wmax = wave_max_dpp(best) - c;
       }
     }
-    CatSel sel;
+    // radix select on digits of up to 8 bits from the top of the bits in which the keys differ
+    // (P of them below the common prefix): per round a 256-bin LDS histogram of the digit over the
+    // keys in the current range (bin = digit, one bit-field extract per key), a DPP scan over the
+    // bins in descending digit order, the bin that holds rank k; the range narrows to that bin.
+    // Stops when the bin holds one key or the digits run out (ties).  Every key also writes its
+    // class into the owner slot of its bin (same address register, immediate offset): when the final
+    // bin holds one key, that slot names the class -- one LDS read, no ballots.  Keys outside the
+    // range skip their atomics (an exec-masked branch).  Measured and not kept (round 5,
+    // profiles/round5/ab_categorical_r5c.txt): branch-free rounds -- bins counted down from the
+    // range's top key so out-of-range keys land past the range or in per-lane trash bins, the bin
+    // inside the lane selected on the VALU -- and two elements per wave with interleaved scans: SALU
+    // below VALU (8.8 k vs 13.3 k per wave) but 323 vs 308 us for uniform ranks; the VALU the
+    // unconditional rounds add costs more than the branches cost the scalar unit
+    uint32_t* own = bins + kCatOwn;
     const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[0][0]);  // class 0 exists
-    cat_sel_init(sel, wave_or_dpp(cat_dif<E4>(key, ok, k0)), k0, k);
+    const uint32_t dif = wave_or_dpp(cat_dif<E4>(key, ok, k0));
+    const int P = dif == 0 ? 0 : 32 - __clz((int)dif);
+    int sh = s_floor_sub(P, 8), wd = P - sh;  // digit = bits [sh, sh + wd)
+    uint32_t t = P >= 32 ? 0u : (k0 >> P) << P;
+    uint32_t c_hi = 0, cnt, dig;  // c_hi: keys above the range
+    // the bin that holds rank k: its digit, its count; keys above it into c_hi
+    auto pick_bin = [&](uint32_t dm) {
+      __builtin_amdgcn_wave_barrier();
+      // bins in ascending digit order; lane l takes digits 255 - 4 l down to 252 - 4 l
+      const uint4 bu = *(const uint4*)(bins + 4 * (63 - lane));
+      const uint32_t tot = bu.x + bu.y + bu.z + bu.w;
+      const uint32_t incl = wave_scan_dpp(tot, 0u, [](uint32_t a, uint32_t c) { return a + c; });
+      const uint32_t r = k - c_hi;
+      const int ls = (int)__builtin_ctzll(__ballot(r < incl));  // the first lane past r (incl ascends)
+      // inside that lane, on the scalar unit: the bin whose cumulative range holds r
+      uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)(incl - tot), ls);
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bu.w, ls);
+      const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)bu.z, ls);
+      const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)bu.y, ls);
+      const uint32_t b3 = (uint32_t)__builtin_amdgcn_readlane((int)bu.x, ls);
+      uint32_t q = 0;
+      cnt = b0;
+      if (r >= cb + b0) {
+        cb += b0; cnt = b1; q = 1;
+        if (r >= cb + b1) {
+          cb += b1; cnt = b2; q = 2;
+          if (r >= cb + b2) { cb += b2; cnt = b3; q = 3; }
+        }
+      }
+      c_hi += cb;
+      dig = (255u - (uint32_t)(4 * ls) - q) & dm;
+      t |= dig << sh;
+    };
     *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    cat_hist<E4, true>(key, ok, sel, bins, lane);
-    cat_pick1(sel, bins, lane);
-    while (sel.more()) {
-      sel.sh = s_floor_sub(sel.sh, 8);
+#pragma unroll
+    for (int s = 0; s < E4; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ok[s][q]) {
+          const uint32_t d = __builtin_amdgcn_ubfe(key[s][q], (uint32_t)sh, (uint32_t)wd);
+          atomicAdd(bins + d, 1u);
+          own[d] = (uint32_t)(s * 256 + 4 * lane + q);
+        }
+    pick_bin((1u << wd) - 1u);
+    while (cnt > 1u && sh != 0) {
+      const int nsh = s_floor_sub(sh, 8);
+      wd = sh - nsh;
+      sh = nsh;
+      const uint32_t dm = (1u << wd) - 1u;
       __builtin_amdgcn_wave_barrier();  // the zeroing must not overtake the last round's reads
       *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
       __builtin_amdgcn_wave_barrier();
-      cat_hist<E4, false>(key, ok, sel, bins, lane);
-      cat_pick1(sel, bins, lane);
+      // keys in the range [t, t + 2^(sh + wd)): (key >> sh) - (t >> sh) <= dm, and that is the digit
+      const uint32_t lo = t >> sh;
+#pragma unroll
+      for (int s = 0; s < E4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t d = (key[s][q] >> sh) - lo;
+          if (ok[s][q] && d <= dm) {
+            atomicAdd(bins + d, 1u);
+            own[d] = (uint32_t)(s * 256 + 4 * lane + q);
+          }
+        }
+      pick_bin(dm);
     }
-    return (T)cat_dec_class<E4, FULL>(key, sel, bins);
+    // the final round's writes precede this read in the wave's LDS order
+    if (cnt == 1u) return (T)__builtin_amdgcn_readfirstlane((int)own[dig]);
+    // ties: the (k - c_hi)-th highest class index among the keys in [tlo, t | span]; padding keys
+    // (0) are below every valid key (>= 1), so without FULL the range starts at 1 at the least
+    const uint32_t span = (1u << sh) - 1u;  // sh <= 24
+    const uint32_t tlo = FULL || t > 0 ? t : 1u, ext = (t | span) - tlo;
+    uint64_t w[E4][4];
+#pragma unroll
+    for (int s = 0; s < E4; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[s][q] = __ballot(key[s][q] - tlo <= ext);
+    return (T)cat_dec_walk<E4>(w, k - c_hi);
   }
-}
-
-// Decode two elements at once (both ranks >= kCatPeel): the same radix select with the two
-// elements' dependent chains -- DPP scans, LDS atomics and reads, readlanes -- interleaved, so each
-// fills the other's latency (DPP steps need 2 wait states after the VALU write they read) instead of
-// the wave idling through it.  The second element's bins are at bins + 2 kCatOwn.  Rounds run as
-// pairs while both elements need one, then singly.
-template <int E4, bool FULL>
-__device__ __forceinline__ void cat_dec_pair(const uint32_t (&ka)[E4][4], const bool (&oa)[E4][4], uint32_t rka,
-                                             const uint32_t (&kb)[E4][4], const bool (&ob)[E4][4], uint32_t rkb,
-                                             int lane, uint32_t* bins, int& ca, int& cb) {
-  uint32_t* bb = bins + 2 * kCatOwn;
-  CatSel sa, sb;
-  const uint32_t k0a = (uint32_t)__builtin_amdgcn_readfirstlane((int)ka[0][0]);
-  const uint32_t k0b = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb[0][0]);
-  uint32_t da = cat_dif<E4>(ka, oa, k0a), db = cat_dif<E4>(kb, ob, k0b);
-  wave_scan2_dpp(da, db, [](uint32_t x, uint32_t y) { return x | y; });
-  cat_sel_init(sa, (uint32_t)__builtin_amdgcn_readlane((int)da, 63), k0a, rka);
-  cat_sel_init(sb, (uint32_t)__builtin_amdgcn_readlane((int)db, 63), k0b, rkb);
-  *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
-  *(uint4*)(bb + 4 * lane) = make_uint4(0, 0, 0, 0);
-  __builtin_amdgcn_wave_barrier();
-  cat_hist<E4, true>(ka, oa, sa, bins, lane);
-  cat_hist<E4, true>(kb, ob, sb, bb, lane);
-  cat_pick2(sa, bins, sb, bb, lane);
-  while (sa.more() && sb.more()) {
-    sa.sh = s_floor_sub(sa.sh, 8);
-    sb.sh = s_floor_sub(sb.sh, 8);
-    __builtin_amdgcn_wave_barrier();
-    *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
-    *(uint4*)(bb + 4 * lane) = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();
-    cat_hist<E4, false>(ka, oa, sa, bins, lane);
-    cat_hist<E4, false>(kb, ob, sb, bb, lane);
-    cat_pick2(sa, bins, sb, bb, lane);
-  }
-  while (sa.more()) {
-    sa.sh = s_floor_sub(sa.sh, 8);
-    __builtin_amdgcn_wave_barrier();
-    *(uint4*)(bins + 4 * lane) = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();
-    cat_hist<E4, false>(ka, oa, sa, bins, lane);
-    cat_pick1(sa, bins, lane);
-  }
-  while (sb.more()) {
-    sb.sh = s_floor_sub(sb.sh, 8);
-    __builtin_amdgcn_wave_barrier();
-    *(uint4*)(bb + 4 * lane) = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();
-    cat_hist<E4, false>(kb, ob, sb, bb, lane);
-    cat_pick1(sb, bb, lane);
-  }
-  ca = cat_dec_class<E4, FULL>(ka, sa, bins);
-  cb = cat_dec_class<E4, FULL>(kb, sb, bb);
 }
 
 template <typename T, int DIR, int E4, int PF, bool FULL>
 __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const float* __restrict__ logits, int64_t n,
                                                                           int64_t L, const T* __restrict__ x,
                                                                           T* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t bins_all[kCatWaves][4 * kCatOwn];  // 2 x (bins, owner slots)
+  __shared__ __attribute__((aligned(16))) uint32_t bins_all[kCatWaves][2 * kCatOwn];  // bins, owner slots
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
   uint32_t* bins = bins_all[wv];
@@ -685,26 +586,6 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
     const uint32_t xw = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[u].xv);
     return cat_rank<T, DIR, E4, FULL>(ring[u], L, lane, bins, cat_xval<T>(xe, xw));
   };
-  // decode: elements u and u + 1 together (cat_dec_pair) unless either rank takes the peel
-  auto rank2 = [&](int u, const T* xe, T& c0, T& c1) {
-    const uint32_t xw0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[u].xv);
-    const uint32_t xw1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[u + 1].xv);
-    const int64_t x0 = cat_xval<T>(xe, xw0), x1 = cat_xval<T>(xe + 1, xw1);
-    const uint32_t k0 = cat_dec_k<T>(x0, L), k1 = cat_dec_k<T>(x1, L);
-    if (k0 >= (uint32_t)kCatPeel && k1 >= (uint32_t)kCatPeel) {
-      uint32_t ka[E4][4], kb[E4][4], ma, mb;
-      bool oa[E4][4], ob[E4][4];
-      cat_dec_keys<E4, FULL>(ring[u], L, lane, ka, oa, ma);
-      cat_dec_keys<E4, FULL>(ring[u + 1], L, lane, kb, ob, mb);
-      int ca, cb;
-      cat_dec_pair<E4, FULL>(ka, oa, k0, kb, ob, k1, lane, bins, ca, cb);
-      c0 = (T)ca;
-      c1 = (T)cb;
-    } else {
-      c0 = cat_rank<T, DIR, E4, FULL>(ring[u], L, lane, bins, x0);
-      c1 = cat_rank<T, DIR, E4, FULL>(ring[u + 1], L, lane, bins, x1);
-    }
-  };
   auto load = [&](int u, int j) {  // element e + j into ring[u]
     cat_load<T, E4, FULL>(rows, ro + (uint32_t)j * rstride, xs, xoff(xp + j), L, lane, zero0, ring[u]);
   };
@@ -713,25 +594,11 @@ __global__ void __launch_bounds__(64 * kCatWaves) categorical_vec_kernel(const f
 #pragma unroll
     for (int u = 0; u < PF; ++u) load(u, u);
     do {
-      if constexpr (DIR == KMP_DECODE && PF % 2 == 0) {
 #pragma unroll
-        for (int u = 0; u < PF; u += 2) {
-          T c0, c1;
-          rank2(u, xp + u, c0, c1);
-          if (lane == 0) {
-            op[u] = c0;
-            op[u + 1] = c1;
-          }
-          load(u, u + PF);
-          load(u + 1, u + 1 + PF);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-          const T code = rank(u, xp + u);
-          if (lane == 0) op[u] = code;
-          load(u, u + PF);
-        }
+      for (int u = 0; u < PF; ++u) {
+        const T code = rank(u, xp + u);
+        if (lane == 0) op[u] = code;
+        load(u, u + PF);
       }
       ro += PF * rstride;
       xp += PF;
