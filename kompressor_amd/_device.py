@@ -90,6 +90,7 @@ _SMALL = 4 << 20  # below this a plain .cpu() costs less than the hand-off
 RING_CHUNK = 16 << 20
 RING_SLOTS = 4
 _STAGING_CAP = 64 << 20  # pinned_staging buffers above this are not kept
+PINNED_OUT_MAX = 1 << 30  # to_host results up to this size are pinned arrays
 
 
 def pinned_staging(nbytes, slot='stage'):
@@ -240,14 +241,24 @@ def parallel_copy(dst, src):
 
 
 def to_host(t):
-    """A device tensor as a new numpy array: pinned D2H at the link rate in ``RING_CHUNK`` pieces,
-    each copied out of its pinned chunk (in parallel) while the next pieces cross the link; the
-    result is ordinary pageable memory the caller owns.  Ordered after the work queued on the
-    current stream of ``t``'s device."""
+    """A device tensor as a new numpy array, ordered after the work queued on the current stream of
+    ``t``'s device.  Up to ``PINNED_OUT_MAX`` bytes the array lives in pinned host memory from
+    torch's caching host allocator (one D2H at the link rate, ~57 GB/s, straight into the result;
+    the block returns to torch's cache when the array is freed); larger tensors stream through the
+    pinned chunk ring, each chunk copied out (in parallel) into ordinary pageable memory while the
+    next ones cross the link."""
     nbytes = t.numel() * t.element_size()
     if nbytes < _SMALL:
         return t.cpu().numpy()
     t = t.contiguous()
+    if nbytes <= PINNED_OUT_MAX:
+        host = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+        with torch.cuda.device(t.device):
+            s = torch.cuda.current_stream(t.device)
+            with torch.cuda.stream(s):
+                host.copy_(t, non_blocking=True)
+            s.synchronize()
+        return host.numpy()
     out = np.empty(tuple(t.shape), dtype=torch.empty(0, dtype=t.dtype).numpy().dtype)
     dst = out.reshape(-1).view(np.uint8)
     with torch.cuda.device(t.device):

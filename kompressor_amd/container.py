@@ -119,6 +119,10 @@ def _write(path, meta, blob, total, crc, t0):
     js += b' ' * (-len(js) % 8)
     tmp = f'{path}.tmp{os.getpid()}'
     with open(tmp, 'wb') as f:
+        try:  # the file's blocks allocated up front: the write then only copies (8.0 vs 10.0 ms for
+            os.posix_fallocate(f.fileno(), 0, _HEAD.size + len(js) + total)  # 112 MB, write_probe_r5w2.log)
+        except OSError:
+            pass  # a filesystem without fallocate: the writes allocate
         f.write(_HEAD.pack(MAGIC, VERSION, 0, len(js)))
         f.write(js)
         if total:

@@ -251,15 +251,19 @@ def test_arith_mismatch_is_rejected(kom, tmp_path):
 @pytest.mark.parametrize('chunk', [1 << 20, 16 << 20])
 def test_chunked_host_transfers(kom, tmp_path, monkeypatch, chunk):
     """The pinned chunk rings (``_device.d2h_stream`` / ``h2d_stream``): to_host of tensors spanning
-    several chunks with a ragged tail, and a file whose payload spans several chunks, are exact."""
+    several chunks with a ragged tail (the ring path: results above ``PINNED_OUT_MAX``; and the
+    pinned-result path below it), and a file whose payload spans several chunks, are exact."""
     from kompressor_amd import _device as dev
     monkeypatch.setattr(dev, 'RING_CHUNK', chunk)
     g = torch.Generator(device='cuda').manual_seed(5)
-    for nbytes in (5 << 20, 3 * chunk + 12345, 7 * chunk + 2):
-        t = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device='cuda', generator=g)
-        assert np.array_equal(dev.to_host(t), t.cpu().numpy())
-    t16 = torch.randint(0, 65536, (3, 77, 129, 131), dtype=torch.int32, device='cuda', generator=g).to(torch.uint16)
-    assert np.array_equal(dev.to_host(t16), t16.cpu().numpy())
+    for pin_max in (0, dev.PINNED_OUT_MAX):
+        monkeypatch.setattr(dev, 'PINNED_OUT_MAX', pin_max)
+        for nbytes in (5 << 20, 3 * chunk + 12345, 7 * chunk + 2):
+            t = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device='cuda', generator=g)
+            assert np.array_equal(dev.to_host(t), t.cpu().numpy())
+        t16 = torch.randint(0, 65536, (3, 77, 129, 131), dtype=torch.int32, device='cuda', generator=g).to(torch.uint16)
+        h16 = dev.to_host(t16)
+        assert h16.dtype == np.uint16 and h16.shape == tuple(t16.shape) and np.array_equal(h16, t16.cpu().numpy())
     x = np.random.default_rng(1).integers(0, 65536, size=(3, 96, 96, 96, 1), dtype=np.uint16)  # ~5 MiB, incompressible
     path = str(tmp_path / 'r.kmp')
     kom.container.compress(path, x, kom.MeanPredictor(0, 3))
