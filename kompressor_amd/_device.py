@@ -108,9 +108,11 @@ def pinned_staging(nbytes, slot='stage'):
 
 
 def release_pinned():
-    """Free this thread's cached pinned buffers (staging slots and chunk rings)."""
+    """Free this thread's cached pinned buffers (staging slots and chunk rings) and return the
+    pinned blocks of freed ``to_host`` results from torch's caching host allocator to the system."""
     for k in list(vars(_TLS)):
         delattr(_TLS, k)
+    torch._C._host_emptyCache()
 
 
 class PinnedRing:

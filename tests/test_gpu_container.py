@@ -268,3 +268,18 @@ def test_chunked_host_transfers(kom, tmp_path, monkeypatch, chunk):
     path = str(tmp_path / 'r.kmp')
     kom.container.compress(path, x, kom.MeanPredictor(0, 3))
     assert np.array_equal(kom.container.decompress(path), x)
+
+
+@pytest.mark.gpu
+def test_pinned_results_are_released(kom):
+    """A to_host result is a pinned array from torch's caching host allocator; once freed,
+    ``release_pinned`` hands the cached pinned blocks back (the process does not keep them)."""
+    from kompressor_amd import _device as dev
+    t = torch.full((48 << 20,), 7, dtype=torch.uint8, device='cuda')
+    h = dev.to_host(t)
+    assert h.shape == (48 << 20,) and int(h[::4096].sum()) == 7 * ((48 << 20) // 4096)
+    del h
+    dev.release_pinned()
+    st = torch.cuda.host_memory_stats()
+    assert st.get('reserved_bytes.current', st.get('segment.current', 0)) < (48 << 20)
+    assert np.array_equal(dev.to_host(t[:5 << 20]), np.full(5 << 20, 7, np.uint8))
