@@ -83,6 +83,9 @@ __constant__ int8_t kQch[16] = {5, 13, 14, 17, 18, -1, -1, -1, -1, -1, -1, -1, -
 // on distinct bank pairs (a slot moves the bank by 2: CS / 2 = 2 mod 32) -- the channel numbers
 // themselves collide (0 and 16)
 constexpr int kSlots = 24;
+#ifndef KMP_L3PM_PD
+#define KMP_L3PM_PD 2
+#endif
 __host__ __device__ constexpr int slot_of(int k, int q) {
   constexpr int8_t s[19] = {0, 1, 2, 3, 4, 14, 5, 6, 7, 8, 9, 10, 11, 15, 16, 12, 13, 17, 18};
   return s[k] + (s[k] >= 14 ? 5 * q : 0);
@@ -290,19 +293,24 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     // fragments of node row j (plane pairs 0, 1) feed accumulation steps 2 (j - r) + e of the cell
     // rows r = j-3 .. j (C and Q tiles alike), so each fragment is read once and used by up to 4
     // rows x 2 tiles; row r starts at j = r (from the bias) and is cast and stored after j = r + 3.
-    // The next node row's fragments are read while this one's MFMAs run.
+    // The x tiles' node rows run as one sequence of TPR * NJ steps whose fragments are read KMP_L3PM_PD
+    // steps ahead (a ring of KMP_L3PM_PD + 1 fragment pairs), across the x-tile boundary too: the
+    // steps at the ends of a tile run few MFMAs (1 to 3 rows), too few to cover an LDS read.
+    constexpr int NS = TPR * NJ, PD = KMP_L3PM_PD, NF = PD + 1;
+    bx::u32x4 F[NF][2];
 #pragma unroll
-    for (int xt = 0; xt < TPR; ++xt) {
-      bx::u32x4 F[2][2];
-      F[0][0] = frag(0, 0, 16 * xt);
-      F[0][1] = frag(1, 0, 16 * xt);
-      bx::f32x4 aC[4], aQ[4];  // cell row r in slot r & 3
+    for (int q = 0; q < PD; ++q) {
+      F[q][0] = frag(0, q % NJ, 16 * (q / NJ));
+      F[q][1] = frag(1, q % NJ, 16 * (q / NJ));
+    }
+    bx::f32x4 aC[4], aQ[4];  // cell row r in slot r & 3
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int cur = j & 1;
-        if (j + 1 < NJ) {
-          F[cur ^ 1][0] = frag(0, j + 1, 16 * xt);
-          F[cur ^ 1][1] = frag(1, j + 1, 16 * xt);
+    for (int st = 0; st < NS; ++st) {
+      {
+        const int xt = st / NJ, j = st % NJ, cur = st % NF;
+        if (st + PD < NS) {
+          F[(st + PD) % NF][0] = frag(0, (st + PD) % NJ, 16 * ((st + PD) / NJ));
+          F[(st + PD) % NF][1] = frag(1, (st + PD) % NJ, 16 * ((st + PD) / NJ));
         }
         if (j < ROWS) {
           aC[j & 3] = (bx::f32x4){biasC, biasC, biasC, biasC};
@@ -323,7 +331,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
           if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16(aC[row & 3]);
           *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16(aQ[row & 3]);
         }
-        hook(xt * NJ + j);
+        hook(st);
       }
     }
     if (c < 0 || c >= a.Lcz) {  // (uniform; the tile's first / last plane) overwritten with zeros
