@@ -132,5 +132,17 @@ __device__ __forceinline__ uint2 cast_pack4_u16(const f32x4& v) {
                     __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u2, u3)));
 }
 
+// the same without the hazard pad, for a caller that has issued at least 8 other MFMAs (each at least
+// one wait state) since the last MFMA writing ``v``, with a scheduling barrier in between so the
+// compiler cannot move this above them
+__device__ __forceinline__ uint2 cast_pack4_u16_late(const f32x4& v) {
+  uint32_t u0, u1, u2, u3;
+  asm("v_cvt_u32_f32 %0, %4\n\tv_cvt_u32_f32 %1, %5\n\tv_cvt_u32_f32 %2, %6\n\tv_cvt_u32_f32 %3, %7"
+      : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+  return make_uint2(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u0, u1)),
+                    __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16(u2, u3)));
+}
+
 }  // namespace bx
 }  // namespace kmp

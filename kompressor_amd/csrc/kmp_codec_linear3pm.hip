@@ -83,6 +83,9 @@ __constant__ int8_t kQch[16] = {5, 13, 14, 17, 18, -1, -1, -1, -1, -1, -1, -1, -
 // on distinct bank pairs (a slot moves the bank by 2: CS / 2 = 2 mod 32) -- the channel numbers
 // themselves collide (0 and 16)
 constexpr int kSlots = 24;
+#ifndef KMP_L3PM_DY0
+#define KMP_L3PM_DY0 3
+#endif
 #ifndef KMP_L3PM_PD
 #define KMP_L3PM_PD 2
 #endif
@@ -316,8 +319,10 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
           aC[j & 3] = (bx::f32x4){biasC, biasC, biasC, biasC};
           aQ[j & 3] = (bx::f32x4){biasQ, biasQ, biasQ, biasQ};
         }
+        // cell row r = j - dy (its steps 2 dy + e in order), the row that completes here (dy = 3)
+        // first: the other rows' MFMAs then cover its results' latency before the cast reads them
 #pragma unroll
-        for (int dy = 0; dy < 4; ++dy) {  // cell row r = j - dy: steps 2 dy + e in order
+        for (int dy = KMP_L3PM_DY0; KMP_L3PM_DY0 ? dy >= 0 : dy < 4; dy += KMP_L3PM_DY0 ? -1 : 1) {
           const int rr = j - dy;
           if (rr < 0 || rr >= ROWS) continue;
 #pragma unroll
@@ -328,8 +333,18 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
         }
         if (j >= 3) {  // cell row j - 3 is complete
           const int row = j - 3;
-          if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16(aC[row & 3]);
-          *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16(aQ[row & 3]);
+          // MFMAs issued after the row's last one: those of rows j - 2 .. j
+          int after = 0;
+#pragma unroll
+          for (int rr = j - 2; rr <= j; ++rr) after += (rr < ROWS) ? (withC ? 4 : 2) : 0;
+          if (KMP_L3PM_DY0 && after >= 8) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16_late(aC[row & 3]);
+            *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16_late(aQ[row & 3]);
+          } else {
+            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16(aC[row & 3]);
+            *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16(aQ[row & 3]);
+          }
         }
         hook(st);
       }
