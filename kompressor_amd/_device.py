@@ -90,7 +90,7 @@ _SMALL = 4 << 20  # below this a plain .cpu() costs less than the hand-off
 RING_CHUNK = 16 << 20
 RING_SLOTS = 4
 _STAGING_CAP = 64 << 20  # pinned_staging buffers above this are not kept
-PINNED_OUT_MAX = 1 << 30  # to_host results up to this size are pinned arrays
+PINNED_OUT_MAX = 512 << 20  # to_host results up to this size are pinned arrays (kept in torch's host cache once freed, up to the peak in use; release_pinned() returns them)
 
 
 def pinned_staging(nbytes, slot='stage'):
