@@ -221,15 +221,16 @@ __device__ __forceinline__ int array_of(const RArrs& A, int64_t g) {
 }
 
 // exclusive prefix of v over the 8 block groups of a wave (v is the same on a group's 8 lanes, so
-// shifts by whole groups keep every lane of a group equal); *tot = the wave's total
+// shifts by whole groups keep every lane of a group equal); *tot = the wave's total.  Three DPP adds
+// (row_shr:8 inside each row of 16, then row_bcast:15 / row_bcast:31 across rows) instead of three
+// ds_bpermute round trips
 __device__ __forceinline__ uint32_t wave_groups_excl(uint32_t v, int lane, uint32_t* tot) {
   uint32_t x = v;
-#pragma unroll
-  for (int d = 8; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-    if (lane >= d) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   *tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  (void)lane;
   return x - v;
 }
 
