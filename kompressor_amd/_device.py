@@ -112,7 +112,9 @@ def release_pinned():
     pinned blocks of freed ``to_host`` results from torch's caching host allocator to the system."""
     for k in list(vars(_TLS)):
         delattr(_TLS, k)
-    torch._C._host_emptyCache()
+    empty = getattr(torch._C, '_host_emptyCache', None)  # torch's caching host allocator (private API)
+    if empty is not None:
+        empty()
 
 
 class PinnedRing:
