@@ -561,8 +561,10 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  // ---- per step: unpack the 8 blocks ----
-#pragma unroll 1
+  // ---- per step: unpack the 8 blocks (fully unrolled: the steps' side information, offsets and
+  // uniform branch conditions resolve per step at compile time instead of in a runtime loop --
+  // 157-159 -> 142-143 us per C3 bundle, profiles/round5/ab_rice_decode_unroll_r5k2.txt) ----
+#pragma unroll
   for (int st = 0; st < S; ++st) {
     int param = tile_bad ? 0 : prm[st];
     const int words = tile_bad ? 0 : wds[st];
