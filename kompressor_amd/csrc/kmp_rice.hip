@@ -387,8 +387,12 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
     const uint32_t incl = group8_incl(len, j);
     const uint32_t uw = (group8_last(incl, j) + 31u) >> 5;
     uint32_t* const us = wl + off + 2 * k;
-    if (param > 0)
-      for (uint32_t i = j; i < uw && i < (uint32_t)UMAX; i += 8) us[i] = 0u;
+    // the block's unary words zeroed: lane j clears words j, j + 8, ... (a fixed, unrolled count of
+    // predicated stores instead of a loop with a per-lane trip count)
+    const uint32_t uz = param > 0 ? min(uw, (uint32_t)UMAX) : 0u;
+#pragma unroll
+    for (int t = 0; t < (UMAX + 7) / 8; ++t)
+      if ((uint32_t)(j + 8 * t) < uz) us[j + 8 * t] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
