@@ -289,6 +289,17 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
   uint32_t wtot = 0;
 #pragma unroll
   for (int st = 0; st < S; ++st) load8s<W>(R.x, R.n, (blk0 + 8 * st + g8) * 64 + j * 8, w[st]);
+  // the wave's whole stage zeroed once while the loads are in flight (UMAX / 2 coalesced 8-byte
+  // stores per lane), so pass 2 ORs the unary codes into it with no per-step zeroing and no LDS
+  // wait between a step's zeroing and its ORs
+  uint8_t* const pside = params + blk0 + g8;
+  uint8_t* const wside = bw + blk0 + g8;
+  uint32_t* const wl = stage[wv];
+#pragma unroll
+  for (int t = 0; t < S * UMAX / 16; ++t) ((uint2*)wl)[lane + 64 * t] = make_uint2(0u, 0u);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
   for (int st = 0; st < S; ++st) {
     const int64_t blk = blk0 + 8 * st + g8;
@@ -332,8 +343,8 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
     const uint32_t prm = zero ? 0u : (key & 31u) + 1u;
     const uint32_t words = zero ? 0u : key >> 5;
     if (j == 0 && has) {
-      params[blk] = (uint8_t)prm;
-      bw[blk] = (uint8_t)words;
+      pside[8 * st] = (uint8_t)prm;  // immediate offsets from one lane pointer per array
+      wside[8 * st] = (uint8_t)words;
     }
     uint32_t stot;
     pb[st] = prm | ((wtot + wave_groups_excl(words, lane, &stot)) << 6);
@@ -361,8 +372,7 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
     if (g > 0) v = i >= 0 ? __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
   }
   // ---- pass 2: each step's block payloads staged in LDS at their wave-local word offsets: the k
-  // low planes, then the unary part (zeroed, then one LDS or per 32 bits of a lane's codes) ----
-  uint32_t* const wl = stage[wv];
+  // low planes, then the unary part (one LDS or per 32 bits of a lane's codes into the zeroed stage) ----
 #pragma unroll
   for (int st = 0; st < S; ++st) {
     const int param = (int)(pb[st] & 63u);
@@ -387,15 +397,6 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
     const uint32_t incl = group8_incl(len, j);
     const uint32_t uw = (group8_last(incl, j) + 31u) >> 5;
     uint32_t* const us = wl + off + 2 * k;
-    // the block's unary words zeroed: lane j clears words j, j + 8, ... (a fixed, unrolled count of
-    // predicated stores instead of a loop with a per-lane trip count)
-    const uint32_t uz = param > 0 ? min(uw, (uint32_t)UMAX) : 0u;
-#pragma unroll
-    for (int t = 0; t < (UMAX + 7) / 8; ++t)
-      if ((uint32_t)(j + 8 * t) < uz) us[j + 8 * t] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t pos0 = incl - len;
     if (param > 0) {
       if (len <= 32u) {  // the lane's 8 codes in one 32-bit mask: at most 2 LDS ors
