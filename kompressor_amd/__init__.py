@@ -13,5 +13,6 @@ in ``libkompressor_hip.so`` (hand-written gfx950 kernels behind the C-ABI in
 from . import _lib  # noqa: F401  (fails loudly if libkompressor_hip.so is missing)
 from . import image, volume, predictors, utils, tiles, shard, slabs, stream, packing, container, graphs  # noqa: F401
 from .predictors import MeanPredictor, LinearPredictor  # noqa: F401
+from ._device import release_pinned  # noqa: F401
 
 VERSION = 'v1.0a'

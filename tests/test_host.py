@@ -250,3 +250,12 @@ def test_linear_auto_arith_rule():
         assert resolve_arith('auto', p, nd, dt) == 'f32'
     for a in ('f32', 'bf16x2'):
         assert resolve_arith(a, 1, 3, torch.uint16) == a
+
+
+def test_release_pinned_exported():
+    """The package exports the pinned-memory release ("Host memory of numpy
+    results"), and the pinned-result threshold is the documented 512 MiB."""
+    import kompressor_amd as kom
+    from kompressor_amd import _device
+    assert kom.release_pinned is _device.release_pinned
+    assert _device.PINNED_OUT_MAX == 512 << 20
