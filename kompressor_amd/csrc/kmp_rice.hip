@@ -119,16 +119,16 @@ __device__ __forceinline__ uint32_t group8_suffix2(uint32_t x, int j) {
   return x;
 }
 
-// the value of the group's lane 0 / lane 7 on all its 8 lanes
-__device__ __forceinline__ uint32_t group8_first(uint32_t x, int j) {
-  const uint32_t t = dpp<0x00>(x);   // quad_perm [0,0,0,0]
-  const uint32_t u = dpp<0x114>(t);  // row_shr:4: lanes 4-7 take lane 0's
-  return (j & 4) ? u : t;
+// the value of the group's lane 0 / lane 7 on all its 8 lanes: row_newbcast of the second group's
+// lane (row lane 8 / 15) to the whole row of 16, then of the first group's (row lane 0 / 7) to banks
+// 0-1 (lanes 0-7) only -- two DPP moves, no select
+__device__ __forceinline__ uint32_t group8_first(uint32_t x, int) {
+  const int b = __builtin_amdgcn_update_dpp(0, (int)x, 0x158, 0xf, 0xf, false);  // row_newbcast:8
+  return (uint32_t)__builtin_amdgcn_update_dpp(b, (int)x, 0x150, 0xf, 0x3, false);  // row_newbcast:0, lanes 0-7
 }
-__device__ __forceinline__ uint32_t group8_last(uint32_t x, int j) {
-  const uint32_t t = dpp<0xFF>(x);   // quad_perm [3,3,3,3]
-  const uint32_t u = dpp<0x104>(t);  // row_shl:4: lanes 0-3 take lane 7's
-  return (j & 4) ? t : u;
+__device__ __forceinline__ uint32_t group8_last(uint32_t x, int) {
+  const int b = __builtin_amdgcn_update_dpp(0, (int)x, 0x15F, 0xf, 0xf, false);  // row_newbcast:15
+  return (uint32_t)__builtin_amdgcn_update_dpp(b, (int)x, 0x157, 0xf, 0x3, false);  // row_newbcast:7, lanes 0-7
 }
 
 // sum over the group (every lane of the group ends with it)
@@ -147,15 +147,18 @@ __device__ __forceinline__ uint32_t group8_min(uint32_t v, int j) {
   return min(v, (j & 4) ? dn : up);
 }
 
-// inclusive prefix over the block's 8 lanes (j = lane & 7)
-__device__ __forceinline__ uint32_t group8_incl(uint32_t v, int j) {
-  uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  if (j & 7) v += t;
-  t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  if ((j & 7) >= 2) v += t;
-  t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  if ((j & 7) >= 4) v += t;
-  return v;
+// inclusive prefix over the block's 8 lanes: the inclusive scan over the row of 16 (row_shr 1, 2,
+// 4, 8 with zeros shifted in at the row's start: one DPP add each, no per-lane masks), then lanes
+// 8-15 take off the first group's total (row lane 7's prefix, row_newbcast:7).  The last step is a
+// broadcast and a select, not a bank-masked DPP subtract: that form (v_subrev_u32_dpp, banks 2-3)
+// left lanes 8-15 unsubtracted on the GPU
+__device__ __forceinline__ uint32_t group8_incl(uint32_t v, int j8) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x157, 0xf, 0xf, false);  // row_newbcast:7
+  return j8 ? v - t : v;
 }
 
 // position of the t-th (0-based) set bit of x (t < popcount(x))
@@ -394,7 +397,7 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int e = 1; e < 8; ++e) r[e] = r[e - 1] + q[e] + 1u;
     const uint32_t len = r[7] + 1u;
-    const uint32_t incl = group8_incl(len, j);
+    const uint32_t incl = group8_incl(len, lane & 8);
     const uint32_t uw = (group8_last(incl, j) + 31u) >> 5;
     uint32_t* const us = wl + off + 2 * k;
     const uint32_t pos0 = incl - len;
@@ -609,7 +612,7 @@ __global__ void __launch_bounds__(256) rice_bundle_decode_kernel(RArrs A, int64_
     if (short_stream) {
       const uint32_t wm = (param > 0 && j < uw) ? us[j] : 0u;
       const uint32_t cm = __builtin_popcount(wm);
-      const uint32_t cum = group8_incl(cm, j);
+      const uint32_t cum = group8_incl(cm, lane & 8);
       const uint32_t d = cum >> 3;
       const uint32_t f = d >= 7u ? 0u : 0x11111110u & (~0u << (4u * (d + 1u)));
       const uint32_t F = group8_sum(f, j);
