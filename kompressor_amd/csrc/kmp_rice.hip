@@ -131,20 +131,18 @@ __device__ __forceinline__ uint32_t group8_last(uint32_t x, int) {
   return (uint32_t)__builtin_amdgcn_update_dpp(b, (int)x, 0x157, 0xf, 0x3, false);  // row_newbcast:7, lanes 0-7
 }
 
-// sum over the group (every lane of the group ends with it)
-__device__ __forceinline__ uint32_t group8_sum(uint32_t v, int j) {
+// sum / minimum over the group (every lane of the group ends with it): the quad's by two quad_perm
+// steps, then the other quad's by row_half_mirror (lane i of a half row reads lane 7 - i, which lies
+// in the other quad of the same group) -- three DPP operations, no select
+__device__ __forceinline__ uint32_t group8_sum(uint32_t v, int) {
   v += dpp<0xB1>(v);
   v += dpp<0x4E>(v);
-  const uint32_t up = dpp<0x104>(v), dn = dpp<0x114>(v);
-  return v + ((j & 4) ? dn : up);
+  return v + dpp<0x141>(v);
 }
-
-// minimum over the group (every lane of the group ends with it)
-__device__ __forceinline__ uint32_t group8_min(uint32_t v, int j) {
+__device__ __forceinline__ uint32_t group8_min(uint32_t v, int) {
   v = min(v, dpp<0xB1>(v));
   v = min(v, dpp<0x4E>(v));
-  const uint32_t up = dpp<0x104>(v), dn = dpp<0x114>(v);
-  return min(v, (j & 4) ? dn : up);
+  return min(v, dpp<0x141>(v));
 }
 
 // inclusive prefix over the block's 8 lanes: the inclusive scan over the row of 16 (row_shr 1, 2,
