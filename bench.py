@@ -203,6 +203,49 @@ def load_traffic(workload, padding, kernel):
     return entry['hbm_bytes'] if entry else None
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_command(n, port, argv, script=None):
+    """The command that starts ``n`` rank processes of this script (one per GPU) with the same
+    arguments: torch.distributed.run on one node, rendezvous on 127.0.0.1."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+            '--master-addr', '127.0.0.1', '--master-port', str(port),
+            script or os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus, env):
+    """Under a launcher (``WORLD_SIZE`` set) the rank count must equal ``--gpus``; returns True when
+    this process must launch the ranks itself (``--gpus N > 1`` and no launcher)."""
+    ws = env.get('WORLD_SIZE')
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f'bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks')
+        return False
+    if gpus < 1:
+        raise SystemExit(f'bench.py: --gpus must be >= 1, got {gpus}')
+    return gpus > 1
+
+
+def maybe_launch(args):
+    """``python bench.py --gpus N`` with N > 1 and no external launcher: start N ranks here, before
+    this process makes any GPU call (``torch.cuda.device_count`` does not initialise the device on
+    this image), and return their exit status; None when this process is a rank itself."""
+    if not check_world(args.gpus, os.environ):
+        return None
+    backend = os.environ.get('KMP_BENCH_BACKEND', 'nccl')
+    have = torch.cuda.device_count()
+    if backend == 'nccl' and have < args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL, '
+                         f'{have} visible (KMP_BENCH_BACKEND=gloo rehearses N ranks on fewer)')
+    import subprocess
+    return subprocess.call(launch_command(args.gpus, free_port(), sys.argv[1:]))
+
+
 def init_dist():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -218,10 +261,20 @@ def init_dist():
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev_id))
         else:
             dist.init_process_group(backend)
+        seen = dist.get_world_size()
+        assert seen == world, f'process group has {seen} ranks, WORLD_SIZE is {world}'
     else:
         dist = None
         torch.cuda.set_device(0)
     return world, rank, dist
+
+
+def dist_info(dist, world):
+    """What the job actually ran on: the rank count the process group reports after init."""
+    if not dist:
+        return {'world_size_seen': 1, 'backend': None, 'launcher': 'none (single process)'}
+    return {'world_size_seen': dist.get_world_size(), 'backend': dist.get_backend(),
+            'launcher': 'torch.distributed.run (one rank per GPU)'}
 
 
 def timed_steps(run_enc, run_dec, steps, dist):
@@ -340,6 +393,9 @@ def c4_strong(kom, hi, predictor, ndim, dist, world, ws, reps=10):
 
 def main():
     args = parse()
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.workload == 'stream':
         return main_stream(args)
     spec = WORKLOADS[args.workload]
@@ -429,6 +485,7 @@ def main():
                        'value_is': 'whole-job aggregate: raw highres bytes coded by all ranks / wall time '
                                    '(weak scaling: every rank codes its own full batch; value_per_gpu = value / n_gpus)'},
             'ms_encode': round(t_enc * 1e3, 5), 'ms_decode': round(t_dec * 1e3, 5),
+            'dist': dist_info(dist, world),
             'launch': 'hipGraph replay (one graph per direction)' if args.graph else 'eager (one ctypes launch per direction)',
             'roofline': {'bound': 'hbm', 'kernel': f'{kernel_name(ndim, args.padding, dominant, spec["dtype"] == np.uint8)} {dominant}',
                          'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -573,6 +630,7 @@ def main_stream(args):
                          'algorithmic_bytes_per_launch': 2 * kraw,
                          'device_resident_ms': {'encode': round(k_enc * 1e3, 4), 'decode': round(k_dec * 1e3, 4),
                                                 'chunks': k}},
+            'dist': dist_info(dist, world),
             'link': {'h2d_plus_d2h_bytes_per_step': 4 * raw,
                      'note': 'each direction moves the raw volume host->device and its coded form back'},
             'cpu_baseline': base,

@@ -6,6 +6,7 @@ arithmetic on the hot path runs in ``libkompressor_hip.so``.
 
 import os
 import threading
+import weakref
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -90,6 +91,11 @@ _SMALL = 4 << 20  # below this a plain .cpu() costs less than the hand-off
 RING_CHUNK = 16 << 20
 RING_SLOTS = 4
 _STAGING_CAP = 64 << 20  # pinned_staging buffers above this are not kept
+# page-locked result bytes alive at once (to_host): past it results go through the ring into pageable
+# memory, so a caller holding many results (a data loader) cannot pin an unbounded share of the host
+PINNED_LIVE_MAX = int(os.environ.get('KMP_PINNED_RESULTS_MAX', 2 << 30))
+_pinned_live = [0]
+_pinned_lock = threading.Lock()
 PINNED_OUT_MAX = 512 << 20  # to_host results up to this size are pinned arrays (kept in torch's host cache once freed, up to the peak in use; release_pinned() returns them)
 
 
@@ -137,11 +143,19 @@ class PinnedRing:
         self.events[i % RING_SLOTS].synchronize()
 
 
-def ring(name='d2h'):
-    r = getattr(_TLS, 'ring_' + name, None)
+def ring(name='d2h', device=None):
+    """This thread's ring for ``name`` on ``device`` (a CUDA event belongs to the device it is first
+    recorded on, so each device has its own ring)."""
+    idx = torch.cuda.current_device() if device is None else (device.index if isinstance(device, torch.device)
+                                                              else int(device))
+    if idx is None:
+        idx = torch.cuda.current_device()
+    key = f'ring_{name}_{idx}'
+    r = getattr(_TLS, key, None)
     if r is None or r.chunk != RING_CHUNK:
-        r = PinnedRing()
-        setattr(_TLS, 'ring_' + name, r)
+        with torch.cuda.device(idx):
+            r = PinnedRing()
+        setattr(_TLS, key, r)
     return r
 
 
@@ -151,7 +165,7 @@ def d2h_stream(src, sink, stream=None):
     pieces are in flight on ``stream`` (default: the current stream of ``src``'s device)."""
     n = src.numel()
     s = stream or torch.cuda.current_stream(src.device)
-    r = ring('d2h')
+    r = ring('d2h', src.device)
     nch = -(-n // RING_CHUNK)
 
     def issue(i):
@@ -178,7 +192,7 @@ def h2d_stream(dst, source, stream=None):
     filled (short when ``source`` came up short)."""
     n = dst.numel()
     s = stream or torch.cuda.current_stream(dst.device)
-    r = ring('h2d')
+    r = ring('h2d', dst.device)
     for i in range(-(-n // RING_CHUNK)):
         r.wait(i)  # the slot's previous upload (this call's chunk i - RING_SLOTS, or an earlier call's) landed
         lo = i * RING_CHUNK
@@ -244,19 +258,39 @@ def parallel_copy(dst, src):
     list(pool.map(lambda i: np.copyto(dst[i * step:(i + 1) * step], src[i * step:(i + 1) * step]), range(k)))
 
 
+def _pin_result(nbytes):
+    with _pinned_lock:
+        if _pinned_live[0] + nbytes > PINNED_LIVE_MAX:
+            return False
+        _pinned_live[0] += nbytes
+        return True
+
+
+def _unpin_result(nbytes):
+    with _pinned_lock:
+        _pinned_live[0] -= nbytes
+
+
+def pinned_result_bytes():
+    """Page-locked bytes held by live ``to_host`` results."""
+    return _pinned_live[0]
+
+
 def to_host(t):
     """A device tensor as a new numpy array, ordered after the work queued on the current stream of
     ``t``'s device.  Up to ``PINNED_OUT_MAX`` bytes the array lives in pinned host memory from
     torch's caching host allocator (one D2H at the link rate, ~57 GB/s, straight into the result;
-    the block returns to torch's cache when the array is freed); larger tensors stream through the
+    the block returns to torch's cache when the array is freed) while the live pinned results stay
+    within ``PINNED_LIVE_MAX``; larger tensors, and results past that cap, stream through the
     pinned chunk ring, each chunk copied out (in parallel) into ordinary pageable memory while the
     next ones cross the link."""
     nbytes = t.numel() * t.element_size()
     if nbytes < _SMALL:
         return t.cpu().numpy()
     t = t.contiguous()
-    if nbytes <= PINNED_OUT_MAX:
+    if nbytes <= PINNED_OUT_MAX and _pin_result(nbytes):
         host = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+        weakref.finalize(host, _unpin_result, nbytes)  # the numpy view keeps ``host`` alive
         with torch.cuda.device(t.device):
             s = torch.cuda.current_stream(t.device)
             with torch.cuda.stream(s):

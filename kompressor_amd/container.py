@@ -37,13 +37,13 @@ import torch
 from . import _device as dev
 from . import _nd, packing
 from ._lib import check, lib
-from .predictors import LinearPredictor, MeanPredictor
+from .predictors import ARITH_REV, LinearPredictor, MeanPredictor
 
 # wall-time split (seconds) of the last compress / decompress / save / load of this process
 last_timing = {}
 
 MAGIC = b'KMPF'
-VERSION = 2  # 2: rice payloads are v2 bundles (packing.py)
+VERSION = 3  # 2: rice payloads are v2 bundles (packing.py); 3: a LinearPredictor's arith_rev recorded
 _HEAD = struct.Struct('<4sHHQ')
 _NP_NAME = {torch.uint8: 'uint8', torch.uint16: 'uint16', torch.int32: 'int32', torch.uint32: 'uint32',
             torch.float32: 'float32'}
@@ -56,7 +56,7 @@ def _predictor_meta(predictor, padding, ndim, dtype):
         return {'kind': 'mean', 'padding': predictor.padding, 'ndim': predictor.ndim}
     if isinstance(predictor, LinearPredictor):
         return {'kind': 'linear', 'padding': predictor.padding, 'ndim': predictor.ndim,
-                'arith': predictor.arith_for(dtype),
+                'arith': predictor.arith_for(dtype), 'arith_rev': ARITH_REV[predictor.arith_for(dtype)],
                 'weights': predictor.weights.tolist(), 'bias': predictor.bias.tolist()}
     # an opaque predictions_fn: recorded by name; decoding needs the caller to pass it again
     return {'kind': 'external', 'padding': padding, 'ndim': ndim,
@@ -69,9 +69,29 @@ def predictor_from_meta(meta):
     if p['kind'] == 'mean':
         return MeanPredictor(p['padding'], p['ndim'])
     if p['kind'] == 'linear':
+        _check_arith_rev(meta)
         return LinearPredictor(np.asarray(p['weights'], np.float32), np.asarray(p['bias'], np.float32),
                                p['padding'], p['ndim'], p.get('arith', 'f32'))
     return None
+
+
+def _check_arith_rev(meta, path='file'):
+    """A LinearPredictor file decodes only under the arithmetic revision it was coded with
+    (predictors.ARITH_REV): a different revision rounds some predictions differently and would
+    return wrong samples.  Files before container version 3 carry no revision; their f32 chain is
+    revision 1, their bf16x2 data is ambiguous (round 4 and round 5 builds wrote it with different
+    accumulation orders) and is refused."""
+    p = meta.get('predictor') or {}
+    if p.get('kind') != 'linear':
+        return
+    arith = p.get('arith', 'f32')
+    rev = p.get('arith_rev', 1 if arith == 'f32' else None)
+    if arith not in ARITH_REV:
+        raise ValueError(f"{path}: unknown LinearPredictor arithmetic {arith!r}")
+    if rev != ARITH_REV[arith]:
+        raise ValueError(f"{path}: coded with arith={arith!r} revision {rev if rev is not None else 'unrecorded'}; "
+                         f"this build evaluates revision {ARITH_REV[arith]}, whose rounding differs -- decode it "
+                         f"with the build that wrote it")
 
 
 def _device_crc(blob, n_max, n_dev=None):
@@ -174,7 +194,7 @@ def _read(path):
         if len(head) < _HEAD.size:
             raise ValueError(f'{path}: not a kompressor_amd file (too short)')
         magic, version, _, mlen = _HEAD.unpack(head)
-        if magic != MAGIC or version not in (1, VERSION) or mlen > (1 << 26):
+        if magic != MAGIC or version not in (1, 2, VERSION) or mlen > (1 << 26):
             raise ValueError(f'{path}: not a kompressor_amd file (magic {magic!r}, version {version})')
         try:
             meta = json.loads(f.read(mlen).decode())
@@ -285,7 +305,10 @@ def decompress(path, predictor=None, as_numpy=True):
         raise AssertionError(f'{path} was coded with padding {padding}; the predictor passed has {pred.padding}')
     if isinstance(pred, LinearPredictor) and meta['predictor'] and meta['predictor'].get('kind') == 'linear':
         # the two arithmetics are not bit-equal: decoding with the other one returns wrong samples
+        _check_arith_rev(meta, path)
         arith = meta['predictor'].get('arith', 'f32')
+        if pred.arith == 'auto':  # a default-constructed predictor takes the file's arithmetic
+            pred = LinearPredictor(pred.weights, pred.bias, pred.padding, pred.ndim, arith=arith)
         if pred.arith_for(lowres.dtype) != arith:
             raise AssertionError(f"{path} was coded with arith='{arith}'; the predictor passed evaluates with "
                                  f"arith='{pred.arith_for(lowres.dtype)}'")

@@ -296,6 +296,9 @@ __global__ void __launch_bounds__(64 * kEncWaves) __attribute__((amdgpu_waves_pe
   uint8_t* const pside = params + blk0 + g8;
   uint8_t* const wside = bw + blk0 + g8;
   uint32_t* const wl = stage[wv];
+  // the stage holds 8 S UMAX words per wave = S UMAX / 16 rounds of 64 lanes x 8 bytes: exact only
+  // when S UMAX is a multiple of 16, or the tail words would keep stale bits under the unary ORs
+  static_assert((S * UMAX) % 16 == 0, "stage zeroing must cover the whole stage");
 #pragma unroll
   for (int t = 0; t < S * UMAX / 16; ++t) ((uint2*)wl)[lane + 64 * t] = make_uint2(0u, 0u);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

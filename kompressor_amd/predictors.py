@@ -54,6 +54,15 @@ class MeanPredictor:
 
 ARITHS = ('auto', 'f32', 'bf16x2')
 
+# Revision of each arithmetic's rounding behaviour.  A revision changes whenever the bits an
+# arithmetic produces change (e.g. the order in which the matrix-core form accumulates its
+# products), so data coded under one revision is never decoded under another: files record it
+# (container.py) and a reader refuses a mismatch instead of returning wrong samples.
+#   f32 1     the k-ordered fma chain from the bias (unchanged since round 1)
+#   bf16x2 1  round 4: one MFMA per 8 consecutive features
+#   bf16x2 2  round 5: one MFMA per node row of a plane pair (kmp_bf16x2.h step_feature)
+ARITH_REV = {'f32': 1, 'bf16x2': 2}
+
 
 def resolve_arith(arith, padding, ndim, dtype):
     """The arithmetic a LinearPredictor evaluates with for samples of ``dtype``: ``'auto'`` is the

@@ -283,3 +283,95 @@ def test_pinned_results_are_released(kom):
     st = torch.cuda.host_memory_stats()
     assert st.get('reserved_bytes.current', st.get('segment.current', 0)) < (48 << 20)
     assert np.array_equal(dev.to_host(t[:5 << 20]), np.full(5 << 20, 7, np.uint8))
+
+
+def _rewrite_meta(src, dst, version=None, **pred_changes):
+    """Copy a file with its metadata's predictor entry changed (keys set to None are removed)."""
+    import json
+    import struct
+    raw = open(src, 'rb').read()
+    magic, ver, z, mlen = struct.unpack('<4sHHQ', raw[:16])
+    meta = json.loads(raw[16:16 + mlen].decode())
+    for k, v in pred_changes.items():
+        if v is None:
+            meta['predictor'].pop(k, None)
+        else:
+            meta['predictor'][k] = v
+    js = json.dumps(meta).encode()
+    js += b' ' * (-len(js) % 8)
+    open(dst, 'wb').write(struct.pack('<4sHHQ', magic, ver if version is None else version, z, len(js)) + js
+                          + raw[16 + mlen:])
+
+
+@pytest.mark.gpu
+def test_arith_revision_recorded_and_enforced(kom, tmp_path):
+    """Files record the LinearPredictor arithmetic's revision; a bf16x2 file of another revision (or
+    a version-2 file, whose bf16x2 order is ambiguous) raises ValueError instead of decoding into wrong
+    samples, while a version-2 f32 file still decodes."""
+    from kompressor_amd.predictors import ARITH_REV
+    rng = np.random.default_rng(4)
+    w = (1 / 64 + rng.standard_normal((64, 19)) * 0.005).astype(np.float32)
+    b = np.zeros(19, np.float32)
+    x = structured((2, 32, 32, 32, 1), np.uint16, 2.0)
+    for arith in ('bf16x2', 'f32'):
+        path = str(tmp_path / f'{arith}.kmp')
+        kom.container.compress(path, x, kom.LinearPredictor(w, b, 1, 3, arith=arith))
+        meta = kom.container.load(path)[2]
+        assert meta['predictor']['arith'] == arith and meta['predictor']['arith_rev'] == ARITH_REV[arith]
+        assert np.array_equal(kom.container.decompress(path), x)
+        old = str(tmp_path / f'{arith}_v2.kmp')
+        _rewrite_meta(path, old, version=2, arith_rev=None)
+        if arith == 'f32':
+            assert np.array_equal(kom.container.decompress(old), x)
+        else:
+            with pytest.raises(ValueError, match='unrecorded'):
+                kom.container.decompress(old)
+        other = str(tmp_path / f'{arith}_rev.kmp')
+        _rewrite_meta(path, other, arith_rev=ARITH_REV[arith] + 1)
+        with pytest.raises(ValueError, match='revision'):
+            kom.container.decompress(other)
+        with pytest.raises(ValueError, match='revision'):
+            kom.container.decompress(other, predictor=kom.LinearPredictor(w, b, 1, 3, arith=arith))
+
+
+@pytest.mark.gpu
+def test_default_predictor_takes_the_files_arith(kom, tmp_path):
+    """A default-constructed LinearPredictor (arith='auto') passed to decompress evaluates with the
+    arithmetic the file records -- a u16 p = 1 file written with arith='f32' (the pre-round-5
+    default) decodes with it, although 'auto' would resolve to bf16x2 there."""
+    rng = np.random.default_rng(5)
+    w = (1 / 64 + rng.standard_normal((64, 19)) * 0.005).astype(np.float32)
+    b = np.zeros(19, np.float32)
+    x = structured((1, 32, 32, 32, 1), np.uint16, 2.0)
+    path = str(tmp_path / 'f32.kmp')
+    kom.container.compress(path, x, kom.LinearPredictor(w, b, 1, 3, arith='f32'))
+    auto = kom.LinearPredictor(w, b, 1, 3)
+    assert auto.arith_for(torch.uint16) == 'bf16x2'
+    assert np.array_equal(kom.container.decompress(path, predictor=auto), x)
+    with pytest.raises(AssertionError):  # an explicit mismatch still raises
+        kom.container.decompress(path, predictor=kom.LinearPredictor(w, b, 1, 3, arith='bf16x2'))
+
+
+@pytest.mark.gpu
+def test_pinned_results_are_capped(kom, monkeypatch):
+    """to_host pins results only while the live pinned bytes stay within PINNED_LIVE_MAX; past it
+    results are pageable (ring path), and freeing a pinned result returns its bytes to the budget."""
+    from kompressor_amd import _device as dev
+    import gc
+    gc.collect()
+    base = dev.pinned_result_bytes()
+    monkeypatch.setattr(dev, 'PINNED_LIVE_MAX', base + (12 << 20))
+    t = torch.arange(8 << 20, dtype=torch.int32, device='cuda').to(torch.uint8)  # 8 MiB
+    a = dev.to_host(t)
+    assert dev.pinned_result_bytes() == base + (8 << 20)
+    b = dev.to_host(t)       # would exceed the cap: pageable, not counted
+    assert dev.pinned_result_bytes() == base + (8 << 20)
+    assert np.array_equal(a, b) and np.array_equal(a, t.cpu().numpy())
+    del a
+    gc.collect()
+    assert dev.pinned_result_bytes() == base
+    c = dev.to_host(t)       # the budget is back
+    assert dev.pinned_result_bytes() == base + (8 << 20) and np.array_equal(c, b)
+    del b, c
+    gc.collect()
+    assert dev.pinned_result_bytes() == base

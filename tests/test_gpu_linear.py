@@ -306,3 +306,100 @@ def test_linear_auto_arith(kom, tmp_path, ndim, p, shape, dtype, want):
         if dtype == np.uint16:
             with pytest.raises(AssertionError):
                 kom.container.decompress(path, predictor=kom.LinearPredictor(w, b, p, ndim, arith=other))
+
+
+# ---- the default p = 1 arithmetic against the f32 oracle: flip-bounded ----
+
+def _smooth_c3(n, seed):
+    """C3-geometry u16 tiles of smooth data (planes + noise): the predictor's realistic regime."""
+    rng = np.random.default_rng(seed)
+    z, y, x = np.meshgrid(np.arange(64), np.arange(64), np.arange(64), indexing='ij')
+    hi = np.empty((n, 64, 64, 64, 1), np.uint16)
+    for t in range(n):
+        a = rng.uniform(-60, 60, 3)
+        hi[t, ..., 0] = np.clip(30000 + a[0] * z + a[1] * y + a[2] * x + rng.normal(0, 30, z.shape), 0, 65535)
+    return hi
+
+
+FLIP_CASES = ['golden:vol_tile64_p1', 'smooth_c3', 'golden:vol_ramp_even_p1', 'golden:vol_rand_mixed_p1',
+              'golden:vol_tile_small_p1', 'golden:vol_ramp_odd_p1']
+
+
+@pytest.mark.parametrize('case', FLIP_CASES)
+def test_linear_auto_p1_flips_vs_f32_oracle(kom, case):
+    """The default arithmetic for u16 volumes at padding 1 (arith='auto' -> bf16x2, the matrix cores)
+    against the oracle's f32 fma chain, on the C3 tile and the golden p = 1 inputs:
+      * a cell prediction differs only by +-1, and only where the float64 value lies within the north
+        star's 1e-5 (relative to sum|f w| + |b|) of the integer boundary the two truncations straddle;
+      * a residual differs from the oracle's f32 residual only by +-1 mod 2^16, and only at a position
+        whose aggregation (maps_from_predictions) takes a flipped cell;
+      * the mismatch rates are printed (run with -s), and the round trip is lossless."""
+    from conftest import GOLDEN
+    V, OV = kom.volume, oracle.volume
+    if case.startswith('golden:'):
+        hi = np.load(f'{GOLDEN}/{case[7:]}.npz')['highres']
+    else:
+        hi = _smooth_c3(2, 31)
+    w, b = _weights(3, 1, 21, np.uint16)
+    auto = kom.LinearPredictor(w, b, 1, 3)
+    assert auto.arith_for(torch.uint16) == 'bf16x2'
+    lo, (maps, dims) = V.encode(auto, V.encode_values_uint16, hi, padding=1)
+    if hi.shape[1:] == (64, 64, 64, 1):
+        assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_encode'
+    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
+                                                padding=1)
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    # cells
+    window = OV.pad_neighborhood(OV.lowres_from_highres(OV.pad_highres(hi)[0]), 1)
+    feats = OV.features_from_lowres(window, 1)
+    o_cells = OP.cast_from_f32(OP.linear_fma_chain(feats, w, b), np.uint16)
+    h_cells, h_f32 = auto.predict_cells(window, with_f32=True)
+    f64, _ = OP.linear_predictions(feats, w, b, np.uint16)
+    scale = np.tensordot(np.moveaxis(np.abs(feats.astype(np.float64)), 4, -1), np.abs(w.astype(np.float64)),
+                         axes=([-1], [0]))
+    scale = np.moveaxis(scale, -1, 4) + np.abs(b).reshape(-1, 1)
+    flips = h_cells != o_cells
+    d = h_cells.astype(np.int64) - o_cells.astype(np.int64)
+    assert np.all(np.abs(d[flips]) == 1), np.unique(d[flips])
+    boundary = np.maximum(h_cells, o_cells).astype(np.float64)
+    dist = np.abs(f64 - boundary)
+    assert np.all(dist[flips] <= 1e-5 * scale[flips]), np.max(dist[flips] / scale[flips]) if flips.any() else 0
+    # residuals
+    touched = OV.trim_maps(OV.maps_from_predictions(flips.astype(np.float32)), dims)
+    nbad = ntot = 0
+    for i, (a, c, t) in enumerate(zip(maps, want_maps, touched)):
+        bad = a != c
+        dd = (a.astype(np.int64) - c.astype(np.int64)) % 65536
+        assert np.all((dd[bad] == 1) | (dd[bad] == 65535)), f'map {i}: {np.unique(dd[bad])}'
+        assert np.all(t[bad] > 0), f'map {i}: a residual mismatch with no flipped cell in its aggregation'
+        nbad += int(bad.sum())
+        ntot += bad.size
+    print(f'\n[flip-rate {case}] cells {int(flips.sum())} / {flips.size} = {flips.mean():.3e}; '
+          f'residuals {nbad} / {ntot} = {nbad / ntot:.3e}')
+    assert np.array_equal(V.decode(auto, V.decode_values_uint16, lo, (maps, dims), padding=1), hi)
+
+
+def test_linear_bf16x2_golden(kom):
+    """The bf16x2 arithmetic's exact bits at the current revision (predictors.ARITH_REV), pinned by
+    GPU-generated fixtures (tests/golden/make_bf16x2_golden.py): any change of how the products are
+    grouped into MFMAs changes maps / cell values and fails here, so it must come with a revision
+    bump (files record the revision and refuse a mismatch)."""
+    import importlib.util
+    from conftest import GOLDEN
+    from kompressor_amd.predictors import ARITH_REV
+    spec = importlib.util.spec_from_file_location('make_bf16x2_golden', f'{GOLDEN}/make_bf16x2_golden.py')
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    rev = ARITH_REV['bf16x2']
+    with np.load(f'{GOLDEN}/bf16x2_r{rev}.npz', allow_pickle=False) as g:
+        assert int(g['arith_rev']) == rev
+        for i, (name, ndim, p, shape, dtype) in enumerate(mk.CASES):
+            # the default dispatch (fused kernels where they apply) and the generic MFMA kernel
+            for generic in (0, 1):
+                with kom._lib.option('KMP_DISABLE_LINEAR_FUSED', generic):
+                    dims, maps, sha, launch = mk.run_case(kom, ndim, p, shape, dtype, 500 + i)
+                assert np.array_equal(dims, g[f'{name}/dims'])
+                for j, m in enumerate(maps):
+                    want = g[f'{name}/map{j}']
+                    assert np.array_equal(m, want), f'{name} ({launch}) map {j}: {np.count_nonzero(m != want)} mismatches'
+                assert sha == str(g[f'{name}/cells_sha256']), f'{name}: f32 cell values changed'

@@ -259,3 +259,26 @@ def test_release_pinned_exported():
     from kompressor_amd import _device
     assert kom.release_pinned is _device.release_pinned
     assert _device.PINNED_OUT_MAX == 512 << 20
+
+
+def test_arith_revision_check():
+    """LinearPredictor files carry the arithmetic's revision (predictors.ARITH_REV); a file coded
+    under another revision -- or a pre-version-3 bf16x2 file, whose accumulation order is
+    ambiguous -- is refused with ValueError, never decoded into wrong samples."""
+    from kompressor_amd.container import _check_arith_rev
+    from kompressor_amd.predictors import ARITH_REV
+    lin = lambda **kw: {'predictor': dict({'kind': 'linear'}, **kw)}  # noqa: E731
+    _check_arith_rev({'predictor': {'kind': 'mean'}})
+    _check_arith_rev({'predictor': None})
+    _check_arith_rev(lin(arith='f32'))                      # version-2 f32 file: the chain is revision 1
+    _check_arith_rev(lin())                                 # round-3 file: no arith at all = f32
+    for a, r in ARITH_REV.items():
+        _check_arith_rev(lin(arith=a, arith_rev=r))
+        with pytest.raises(ValueError, match='revision'):
+            _check_arith_rev(lin(arith=a, arith_rev=r + 1))
+    with pytest.raises(ValueError, match='unrecorded'):
+        _check_arith_rev(lin(arith='bf16x2'))               # version-2 bf16x2: round 4 or round 5 order
+    with pytest.raises(ValueError):
+        _check_arith_rev(lin(arith='bf16x2', arith_rev=1))  # the round-4 accumulation order
+    with pytest.raises(ValueError, match='unknown'):
+        _check_arith_rev(lin(arith='tf32', arith_rev=1))

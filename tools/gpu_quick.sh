@@ -14,7 +14,7 @@ step bench 400 python bench.py && \
 step bench_image 300 python bench.py --workload image && \
 step bench_stream 400 python bench.py --workload stream && \
 step debug_parity 600 env KMP_DEBUG=1 python -u -m pytest tests/test_gpu_codec.py tests/test_packing.py -m gpu -x -q --timeout 120 --timeout-method thread && \
-step bench_n2_gloo 300 env KMP_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-e2e
+step bench_n2_gloo 300 env KMP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --no-e2e
 rc=$?
 tail -3 $O/pytest_gpu.log; tail -1 $O/bench.log; tail -1 $O/bench_image.log; tail -1 $O/bench_stream.log; tail -2 $O/debug_parity.log; tail -1 $O/bench_n2_gloo.log
 exit $rc
