@@ -94,6 +94,61 @@ __host__ __device__ constexpr int slot_of(int k, int q) {
   return s[k] + (s[k] >= 14 ? 5 * q : 0);
 }
 
+// Per-lane global segments of the sample dtype T (a lane owns VX = 4 cells of a row for either
+// dtype): a highres row segment is the 8 samples of its cells' two highres columns (16 B for u16,
+// 8 B for u8), a lowres / map segment the 4 cells (8 B / 4 B).  The channel table holds u16 either
+// way (u8 predictions saturate at 255 before they are stored).
+template <typename T> using HSeg = typename std::conditional<sizeof(T) == 2, uint4, uint2>::type;
+template <typename T> using MSeg = typename std::conditional<sizeof(T) == 2, uint2, uint32_t>::type;
+template <typename T> __device__ __forceinline__ HSeg<T> ldH(const T* p) {
+  if constexpr (sizeof(T) == 2) return ld16(p);
+  else return ld8(p);
+}
+template <typename T> __device__ __forceinline__ HSeg<T> ldHc(const T* p) {
+  if constexpr (sizeof(T) == 2) return ld16c(p);
+  else return ld8c(p);
+}
+template <typename T> __device__ __forceinline__ MSeg<T> ldM(const T* p) {
+  if constexpr (sizeof(T) == 2) return ld8(p);
+  else return __builtin_nontemporal_load((const uint32_t*)p);
+}
+template <typename T> __device__ __forceinline__ MSeg<T> ldMc(const T* p) {
+  if constexpr (sizeof(T) == 2) return ld8c(p);
+  else return *(const uint32_t*)p;
+}
+template <typename T> __device__ __forceinline__ void stH(T* p, const HSeg<T>& v) {
+  if constexpr (sizeof(T) == 2) st16(p, v);
+  else st8(p, v);
+}
+template <typename T> __device__ __forceinline__ void stM(T* p, const MSeg<T>& v) {
+  if constexpr (sizeof(T) == 2) st8(p, v);
+  else __builtin_nontemporal_store(v, (uint32_t*)p);
+}
+template <typename T> __device__ __forceinline__ uint32_t elH(const HSeg<T>& v, int e) {  // sample e < 8
+  if constexpr (sizeof(T) == 2) return el16<T>(v, e);
+  else return el8<T>(v, e);
+}
+template <typename T> __device__ __forceinline__ uint32_t elM(const MSeg<T>& v, int i) {  // cell i < 4
+  if constexpr (sizeof(T) == 2) return el8<T>(v, i);
+  else return (v >> (8 * i)) & 0xffu;
+}
+template <typename T> __device__ __forceinline__ MSeg<T> packM(const uint32_t (&v)[4]) {
+  if constexpr (sizeof(T) == 2) return pack8<T, 4>(v);
+  else return (v[0] & 0xffu) | ((v[1] & 0xffu) << 8) | ((v[2] & 0xffu) << 16) | (v[3] << 24);
+}
+template <typename T> __device__ __forceinline__ HSeg<T> packH(const uint32_t (&ev)[4], const uint32_t (&od)[4]) {
+  if constexpr (sizeof(T) == 2) return pack16<T, 4>(ev, od);
+  else
+    return make_uint2((ev[0] & 0xffu) | ((od[0] & 0xffu) << 8) | ((ev[1] & 0xffu) << 16) | (od[1] << 24),
+                      (ev[2] & 0xffu) | ((od[2] & 0xffu) << 8) | ((ev[3] & 0xffu) << 16) | (od[3] << 24));
+}
+// an MFMA result's 4 cells cast to T (XLA astype) as the table's packed u16; ``late``: the u16
+// form without the hazard pad (see kmp_bf16x2.h), for a caller with >= 8 MFMAs in between
+template <typename T, bool LATE> __device__ __forceinline__ uint2 cast_cells(const bx::f32x4& v) {
+  if constexpr (sizeof(T) == 2) return LATE ? bx::cast_pack4_u16_late(v) : bx::cast_pack4_u16(v);
+  else return bx::cast_pack4<uint16_t>(v, 255.0f);
+}
+
 // The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
 // biases, built once per call into the workspace instead of in every wave (64 bf16 splits a lane)
 __global__ void __launch_bounds__(64) fragments_kernel(const float* __restrict__ W, const float* __restrict__ bias,
@@ -113,10 +168,10 @@ constexpr size_t kFragBytes = 3 * 8 * 64 * sizeof(bx::u32x4) + 3 * 64 * sizeof(f
 // + the dummy store slots (8 u16 per lane) after the fragments
 constexpr size_t kWsBytes = kFragBytes + 64 * 8 * sizeof(uint16_t);
 
-template <bool DEC, int EX, int EY>
+template <typename T, bool DEC, int EX, int EY>
 __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_waves_per_eu(2, 2))) linear3pm_kernel(PM a) {
-  typedef uint16_t T;
-  constexpr int VX = 4;               // u16 cells per lane
+  typedef uint16_t CT_T;              // channel table entries
+  constexpr int VX = 4;               // cells per lane
   constexpr int TXN = EX / VX;        // lanes per row
   constexpr int ROWS = 64 / TXN;      // rows per wave
   constexpr int NW = EY / ROWS;       // waves
@@ -137,12 +192,12 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   constexpr int DMY = DPAD + 4 * 15 + 4 * 3 + (ROWS - 1) * EX + EX / 2 + 4;
   constexpr int CT = kSlots * CS + DMY;
   static_assert(CS % 64 == 4, "bank layout");
-  constexpr uint32_t MASK = 0xffffu;
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   static_assert(EX % 16 == 0 && ROWS % 2 == 0 && NW * ROWS == EY && NW <= 4, "geometry");
-  using V = typename std::conditional<DEC, uint2, uint4>::type;
+  using V = typename std::conditional<DEC, MSeg<T>, HSeg<T>>::type;
 
   __shared__ __attribute__((aligned(16))) uint32_t st[NPL * NR * PITCH];  // ring of 4 node planes
-  __shared__ __attribute__((aligned(16))) T ct[NW * CT];
+  __shared__ __attribute__((aligned(16))) CT_T ct[NW * CT];
 
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -185,14 +240,14 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   // the lane's node row of node plane q (any q within one reflection of the axis)
   auto node_row = [&](int q) -> V {
     const int sz = lsrc1(q, a.Lz, a.Ez);
-    if constexpr (DEC) return ld8c(lin + sz * lplane + lo_own);
-    else return ld16c(hin + 2 * sz * hplane + ho_own);
+    if constexpr (DEC) return ldMc<T>(lin + sz * lplane + lo_own);
+    else return ldHc<T>(hin + 2 * sz * hplane + ho_own);
   };
   // the rows an output plane's coder reads besides its nodes: the maps (decode) / the highres
   // rows of the odd positions (encode)
   struct Streams {
-    uint2 mv[7];
-    uint4 e1, o0, o1;
+    MSeg<T> mv[7];
+    HSeg<T> e1, o0, o1;
   };
   auto load_streams = [&](int c, Streams& sv) {
     // unconditional: a plane past an odd-sized z axis (c >= Lcz) re-reads the one before, its
@@ -203,27 +258,27 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
       for (int k = 0; k < 7; ++k) {
         int par[3];
         map_parity(3, k, par);
-        sv.mv[k] = ld8(mbase[k] + (((!par[0] || vz1) ? c : c - 1) * lplane + lo_own));
+        sv.mv[k] = ldM<T>(mbase[k] + (((!par[0] || vz1) ? c : c - 1) * lplane + lo_own));
       }
     } else {
       const T* p = hin + 2 * c * hplane;
       const int o = vz1 ? hplane : 0;
-      sv.e1 = ld16(p + ho_own + a.W_);
-      sv.o0 = ld16(p + o + ho_own);
-      sv.o1 = ld16(p + o + ho_own + a.W_);
+      sv.e1 = ldH<T>(p + ho_own + a.W_);
+      sv.o0 = ldH<T>(p + o + ho_own);
+      sv.o1 = ldH<T>(p + o + ho_own + a.W_);
     }
   };
 
   const int chC = kCch[m], chQ = kQch[m];
-  T* const ctw = ct + w * CT;
+  CT_T* const ctw = ct + w * CT;
   // the lane's column of the channel table (its C / Q channel, 4 cells from x0 + 4g), or its dummy slot
   // dummy addresses mimic the bank pair of a slot (mod 16) the tile's real columns do not take:
   // C: slots 14, 15; Q of parity 0 (slots 14 .. 18, banks of slots 14, 15, 0, 1, 2): slots 3 .. 13;
   // Q of parity 1 (slots 19 .. 23, banks of slots 3 .. 7): slots 8 .. 15, 0 .. 2
-  T* const dmy = ctw + kSlots * CS + DPAD + 4 * g;
-  T* const ctC = m < 14 ? ctw + m * CS + 4 * g : dmy + 4 * m;
-  T* const ctQ0 = m < 5 ? ctw + (14 + m) * CS + 4 * g : dmy + 4 * (m - 2);
-  T* const ctQ1 = m < 5 ? ctw + (19 + m) * CS + 4 * g : dmy + 4 * ((m + 3) & 15);
+  CT_T* const dmy = ctw + kSlots * CS + DPAD + 4 * g;
+  CT_T* const ctC = m < 14 ? ctw + m * CS + 4 * g : dmy + 4 * m;
+  CT_T* const ctQ0 = m < 5 ? ctw + (14 + m) * CS + 4 * g : dmy + 4 * (m - 2);
+  CT_T* const ctQ1 = m < 5 ? ctw + (19 + m) * CS + 4 * g : dmy + 4 * ((m + 3) & 15);
   // the lane's A-fragment origin: ring slot 0, node row Y0 + (g & 1), node column m
   const lds_cptr fl = (lds_cptr)st + Y0 * PITCH + m;
 
@@ -235,7 +290,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     uint32_t v[VX];
 #pragma unroll
     for (int i = 0; i < VX; ++i)
-      v[i] = bx::feature_dword(DEC ? el8<T>(*(const uint2*)&own, i) : el16<T>(*(const uint4*)&own, 2 * i));
+      v[i] = bx::feature_dword(DEC ? elM<T>(*(const MSeg<T>*)&own, i) : elH<T>(*(const HSeg<T>*)&own, 2 * i));
     auto put_row = [&](int ry) __attribute__((always_inline)) {
       uint32_t* row = st + (slot * NR + ry) * PITCH + P + X;
 #pragma unroll
@@ -271,7 +326,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
   // MFMA groups in program order
   auto channels = [&](int c, bool withC, const bx::u32x4 (&bC)[8], const bx::u32x4 (&bQ)[8], float biasC,
                       float biasQ, auto&& hook) {
-    T* const ctQ = (c & 1) ? ctQ1 : ctQ0;
+    CT_T* const ctQ = (c & 1) ? ctQ1 : ctQ0;
     constexpr int NJ = ROWS + 3;
     // A fragment: node plane c - 1 + t (ring slot (c - 1 + t) mod 4), staged rows Y0 + ry + (g & 1),
     // cells x0 + m: one base per slot and half of the wave's rows, the rest immediate offsets
@@ -339,11 +394,11 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
           for (int rr = j - 2; rr <= j; ++rr) after += (rr < ROWS) ? (withC ? 4 : 2) : 0;
           if (KMP_L3PM_DY0 && after >= 8) {
             __builtin_amdgcn_sched_barrier(0);
-            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16_late(aC[row & 3]);
-            *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16_late(aQ[row & 3]);
+            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = cast_cells<T, true>(aC[row & 3]);
+            *(uint2*)(ctQ + row * EX + 16 * xt) = cast_cells<T, true>(aQ[row & 3]);
           } else {
-            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = bx::cast_pack4_u16(aC[row & 3]);
-            *(uint2*)(ctQ + row * EX + 16 * xt) = bx::cast_pack4_u16(aQ[row & 3]);
+            if (withC) *(uint2*)(ctC + row * EX + 16 * xt) = cast_cells<T, false>(aC[row & 3]);
+            *(uint2*)(ctQ + row * EX + 16 * xt) = cast_cells<T, false>(aQ[row & 3]);
           }
         }
         hook(st);
@@ -360,7 +415,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     }
   };
 
-  const T* const upt = (r > 0 ? ctw + (r - 1) * EX : w > 0 ? ctw - CT + (ROWS - 1) * EX : ctw) + X;
+  const CT_T* const upt = (r > 0 ? ctw + (r - 1) * EX : w > 0 ? ctw - CT + (ROWS - 1) * EX : ctw) + X;
   const uint32_t upm = Y > 0 ? 0xffffffffu : 0u;
   // the channels the coder of one output plane reads: the lane's 4 cells of all 19 channels (slot
   // order) and the 5 row-above channels (3, 9, 10, 16, 17; this wave's row r - 1, the wave above's
@@ -395,11 +450,11 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     const bool vz1 = c < a.Lcz, vz0 = c >= 1;
     auto rd = [&](int k, uint32_t (&v)[VX + 1]) {
 #pragma unroll
-      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(ch.v[k], i);
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<CT_T>(ch.v[k], i);
     };
     auto rd_up = [&](int j, uint32_t (&v)[VX + 1]) {
 #pragma unroll
-      for (int i = 0; i < VX; ++i) v[i + 1] = el8<T>(ch.up[j], i);
+      for (int i = 0; i < VX; ++i) v[i + 1] = el8<CT_T>(ch.up[j], i);
     };
     uint32_t A3[VX + 1], A9[VX + 1], A10[VX + 1], A16[VX + 1], QA17[VX + 1];
     rd_up(0, A3);
@@ -420,21 +475,21 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
     auto put8 = [&](int k, const uint32_t (&res)[VX]) {
       int par[3];
       map_parity(3, k, par);
-      st8((!par[0] || vz1) ? mbase[k] + (c * lplane + lo_own) : dummy, pack8<T, VX>(res));
+      stM<T>((!par[0] || vz1) ? mbase[k] + (c * lplane + lo_own) : dummy, packM<T>(res));
     };
-    const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own;
+    const HSeg<T> e0 = DEC ? HSeg<T>{} : *(const HSeg<T>*)&own;
     T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
     uint32_t ownv[VX];
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own, i);
-      else ownv[i] = el16<T>(e0, 2 * i);
+      if constexpr (DEC) ownv[i] = elM<T>(*(const MSeg<T>*)&own, i);
+      else ownv[i] = elH<T>(e0, 2 * i);
     }
-    auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
+    auto code = [&](int k, const uint32_t (&pred)[VX], const HSeg<T>& src, int odd, uint32_t (&outv)[VX]) {
 #pragma unroll
       for (int i = 0; i < VX; ++i) {
-        if constexpr (DEC) outv[i] = (pred[i] + el8<T>(sv.mv[k], i)) & MASK;
-        else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+        if constexpr (DEC) outv[i] = (pred[i] + elM<T>(sv.mv[k], i)) & MASK;
+        else outv[i] = (elH<T>(src, 2 * i + odd) - pred[i]) & MASK;
       }
     };
 
@@ -447,9 +502,9 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
       for (int i = 0; i < VX; ++i) pred[i] = (P15[i + 1] + A16[i + 1] + QA17[i + 1] + Q18[i + 1]) >> ((nz * ny) >> 1);
       code(6, pred, e0, 1, outv);
       if constexpr (DEC) {
-        st16(h0, pack16<T, VX>(ownv, outv));
+        stH<T>(h0, packH<T>(ownv, outv));
       } else {
-        st8(lout + c * lplane + lo_own, pack8<T, VX>(ownv));
+        stM<T>(lout + c * lplane + lo_own, packM<T>(ownv));
         put8(6, outv);
       }
     }
@@ -473,7 +528,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
 #pragma unroll
       for (int i = 0; i < VX; ++i) pU[i] = (P2[i + 1] + A3[i + 1]) >> (ny >> 1);
       code(1, pU, sv.o0, 1, oU);
-      if constexpr (DEC) st16(vz1 ? h0 + hplane : dummy, pack16<T, VX>(keep, oU));
+      if constexpr (DEC) stH<T>(vz1 ? h0 + hplane : dummy, packH<T>(keep, oU));
       else put8(1, oU);
     }
     // Y map (0,1,0): ch11 (z,x) ch12 (z,x-1) ch13 (z-1,x-1) ch14 (z-1,x);  FB (0,1,1): ch4, ch5
@@ -500,7 +555,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
 #pragma unroll
       for (int i = 0; i < VX; ++i) pF[i] = (P4[i + 1] + Q5[i + 1]) >> (nz >> 1);
       code(2, pF, sv.e1, 1, oF);
-      if constexpr (DEC) st16(h0 + a.W_, pack16<T, VX>(keep, oF));
+      if constexpr (DEC) stH<T>(h0 + a.W_, packH<T>(keep, oF));
       else put8(2, oF);
     }
     // LR map (1,1,0): ch0 (x), ch1 (x-1);  C (1,1,1): ch6
@@ -523,7 +578,7 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
 #pragma unroll
       for (int i = 0; i < VX; ++i) pC[i] = P6[i + 1];
       code(3, pC, sv.o1, 1, oC);
-      if constexpr (DEC) st16(vz1 ? h0 + hplane + a.W_ : dummy, pack16<T, VX>(keep, oC));
+      if constexpr (DEC) stH<T>(vz1 ? h0 + hplane + a.W_ : dummy, packH<T>(keep, oC));
       else put8(3, oC);
     }
   };
@@ -591,19 +646,19 @@ __global__ void __launch_bounds__(64 * (EY / (256 / EX))) __attribute__((amdgpu_
 
 }  // namespace l3q
 
-// u16 FULL tiles (Lcy == Ey, Lcx == Ex) with Ex, Ey in {16, 32}; anything else is served by the
+// u8 / u16 FULL tiles (Lcy == Ey, Lcx == Ex) with Ex, Ey in {16, 32}; anything else is served by the
 // generic path with kmp_linear.hip's kernel of the same predictor kind (bit-identical arithmetic)
 template <typename T>
 static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
                                const kmp_region* region, l3q::PM& a, dim3& grid, dim3& block) {
   constexpr int P = l3q::P;
-  if (!std::is_same<T, uint16_t>::value) return false;
+  if (!std::is_same<T, uint16_t>::value && !std::is_same<T, uint8_t>::value) return false;
   if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR_MFMA || pred->padding != P || !pred->weights || !pred->bias) return false;
   if (g.E[2] != 16 && g.E[2] != 32) return false;
   if (g.E[1] != 16 && g.E[1] != 32) return false;
   if (g.Lc[1] != g.E[1] || g.Lc[2] != g.E[2] || g.Lc[0] < 1) return false;
-  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[2] % 8 != 0) return false;  // 8-sample highres row segments, aligned
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
   // one reflection covers every halo index (lsrc1): L >= P + 2 on each axis
   if (g.L[0] < P + 2 || g.L[1] < P + 2 || g.L[2] < P + 2) return false;
@@ -634,9 +689,9 @@ static bool linear3pm_geometry(const Geo& g, int64_t B, int64_t C, const kmp_pre
   return nblk < ((int64_t)1 << 31);
 }
 
-template <bool DEC>
+template <typename T, bool DEC>
 static void launch_linear3pm(const l3q::PM& a, dim3 grid, dim3 block, hipStream_t stream) {
-#define KMP_L3Q(EX, EY) l3q::linear3pm_kernel<DEC, EX, EY><<<grid, block, 0, stream>>>(a)
+#define KMP_L3Q(EX, EY) l3q::linear3pm_kernel<T, DEC, EX, EY><<<grid, block, 0, stream>>>(a)
   if (a.Ex == 32) {
     if (a.Ey == 32) KMP_L3Q(32, 32);
     else KMP_L3Q(32, 16);
@@ -651,13 +706,14 @@ template <typename T>
 int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                          const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes,
                          hipStream_t stream) {
-  if constexpr (std::is_same<T, uint16_t>::value) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     l3q::PM a{};
     dim3 grid, block;
     if (!linear3pm_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
-    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    constexpr uintptr_t HA = 8 * sizeof(T) - 1, MA = 4 * sizeof(T) - 1;  // segment alignments
+    if (((uintptr_t)hi & HA) || ((uintptr_t)lowres & MA)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
-      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      if ((uintptr_t)maps.p[k] & MA) return KMP_ERR_UNSUPPORTED;
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
@@ -666,7 +722,7 @@ int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
     l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
-    launch_linear3pm<false>(a, grid, block, stream);
+    launch_linear3pm<T, false>(a, grid, block, stream);
     return check_launch("linear3pm_encode");
   }
   return KMP_ERR_UNSUPPORTED;
@@ -676,13 +732,14 @@ template <typename T>
 int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
                          const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
                          hipStream_t stream) {
-  if constexpr (std::is_same<T, uint16_t>::value) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     l3q::PM a{};
     dim3 grid, block;
     if (!linear3pm_geometry<T>(g, B, C, pred, region, a, grid, block)) return KMP_ERR_UNSUPPORTED;
-    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    constexpr uintptr_t HA = 8 * sizeof(T) - 1, MA = 4 * sizeof(T) - 1;
+    if (((uintptr_t)hi & HA) || ((uintptr_t)lowres & MA)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
-      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      if ((uintptr_t)maps.p[k] & MA) return KMP_ERR_UNSUPPORTED;
       a.maps.p[k] = (void*)maps.p[k];
     }
     a.hi_out = hi;
@@ -692,7 +749,7 @@ int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
     l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
-    launch_linear3pm<true>(a, grid, block, stream);
+    launch_linear3pm<T, true>(a, grid, block, stream);
     return check_launch("linear3pm_decode");
   }
   return KMP_ERR_UNSUPPORTED;

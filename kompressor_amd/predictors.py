@@ -66,15 +66,16 @@ ARITH_REV = {'f32': 1, 'bf16x2': 2}
 
 def resolve_arith(arith, padding, ndim, dtype):
     """The arithmetic a LinearPredictor evaluates with for samples of ``dtype``: ``'auto'`` is the
-    matrix-core form (``'bf16x2'``) for volumes with padding 1 and uint16 samples -- the learned-
-    predictor configuration SURVEY.md §8d prices, where the fused ``linear3pm`` kernel codes a C3
-    direction in about half the f32 chain's time (profiles/round5/rows_linear_auto_r5a1.log) -- and the
-    f32 chain everywhere else (padding 0, where the f32 kernel is the faster one; images; 8- and
-    32-bit samples).  A function of the predictor and the sample dtype only, so encode, decode,
-    chunked and whole-volume calls, and a file's reader all resolve it the same way."""
+    matrix-core form (``'bf16x2'``) for volumes with padding 1 and 8- or 16-bit samples -- the
+    learned-predictor configuration SURVEY.md §8d prices, where the fused ``linear3pm`` kernel codes a
+    C3 direction in about half the f32 chain's time (profiles/round5/rows_linear_auto_r5a1.log; uint8
+    since round 6) -- and the f32 chain everywhere else (padding 0, where the f32 kernel is the faster
+    one; images; 32-bit samples, which bf16x2 cannot split exactly).  A function of the predictor and
+    the sample dtype only, so encode, decode, chunked and whole-volume calls, and a file's reader all
+    resolve it the same way."""
     if arith != 'auto':
         return arith
-    return 'bf16x2' if ndim == 3 and padding == 1 and dtype == torch.uint16 else 'f32'
+    return 'bf16x2' if ndim == 3 and padding == 1 and dtype in (torch.uint16, torch.uint8) else 'f32'
 
 
 class LinearPredictor:
@@ -91,7 +92,10 @@ class LinearPredictor:
       star's 1e-5 (relative to sum|f w| + |b|) of the float64 value rather than equal to the f32
       chain.  uint8 / uint16 samples;
     * ``'auto'`` (default): ``'bf16x2'`` where the matrix cores are the fast path (volumes, padding 1,
-      uint16 samples), ``'f32'`` elsewhere (:func:`resolve_arith`)."""
+      uint8 / uint16 samples), ``'f32'`` elsewhere (:func:`resolve_arith`).  Breaking change (round 5,
+      uint8 in round 6): the default was ``'f32'``; in-memory encodings made with the old default must
+      be decoded with ``arith='f32'`` (files record their arithmetic, and ``container.decompress``
+      takes it from the file for a default-constructed predictor)."""
 
     def __init__(self, weights, bias, padding=0, ndim=3, arith='auto'):
         if ndim not in (2, 3):

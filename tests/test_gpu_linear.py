@@ -159,7 +159,10 @@ BF_CASES = [(3, 0, (4, 64, 64, 64, 1), np.uint16), (3, 0, (2, 16, 32, 32, 1), np
             (3, 1, (2, 12, 64, 64, 1), np.uint16), (3, 1, (1, 10, 32, 32, 1), np.uint16),
             (3, 1, (1, 8, 32, 64, 1), np.uint16), (3, 1, (1, 7, 64, 32, 1), np.uint16),
             (3, 1, (1, 8, 32, 64, 1), np.uint8),
-            (3, 1, (1, 6, 32, 32, 1), np.uint16)]  # a small volume: the workspace still holds the fragments
+            (3, 1, (1, 6, 32, 32, 1), np.uint16),  # a small volume: the workspace still holds the fragments
+            # p = 1 u8 on linear3pm (round 6): every row width / plane height, C3 tiles, an odd depth
+            (3, 1, (2, 12, 64, 64, 1), np.uint8), (3, 1, (1, 10, 32, 32, 1), np.uint8),
+            (3, 1, (1, 7, 64, 32, 1), np.uint8), (3, 1, (4, 64, 64, 64, 1), np.uint8)]
 
 
 @pytest.mark.parametrize('ndim,p,shape,dtype', BF_CASES)
@@ -199,8 +202,8 @@ def test_linear_bf16x2_codec_paths_agree(kom, ndim, p, shape, dtype):
     rows = 64 // max(1, ex // vx)
     fused = (ndim == 3 and p == 0 and shape[2] % 2 == 0 and shape[3] % 2 == 0 and ex in (16, 32)
              and ey % rows == 0 and ey // rows in (1, 2, 4))
-    # p = 1: u16 FULL volumes with 16 / 32-wide rows and 16 / 32 rows a plane
-    fused1 = (ndim == 3 and p == 1 and dtype == np.uint16 and shape[2] % 2 == 0 and shape[3] % 2 == 0
+    # p = 1: u8 / u16 FULL volumes with 16 / 32-wide rows and 16 / 32 rows a plane
+    fused1 = (ndim == 3 and p == 1 and shape[2] % 2 == 0 and shape[3] % 2 == 0
               and ex in (16, 32) and ey in (16, 32))
     want_kernel = 'linear3m_encode' if fused else 'linear3pm_encode' if fused1 else 'encode_generic'
     assert kom._lib.lib.kmp_last_launch().decode() == want_kernel
@@ -230,8 +233,9 @@ def test_linear_bf16x2_rejects_32bit_samples(kom):
         kom.volume.encode(pred, kom.volume.encode_values_raw, hi)
 
 
-def test_linear_bf16x2_p1_fused_sweep(kom):
-    """Seeded sweep of fused-eligible p = 1 volumes (u16, 16 / 32-wide rows and planes, any depth,
+@pytest.mark.parametrize('dtype', [np.uint16, np.uint8])
+def test_linear_bf16x2_p1_fused_sweep(kom, dtype):
+    """Seeded sweep of fused-eligible p = 1 volumes (u8 / u16, 16 / 32-wide rows and planes, any depth,
     batch sizes that do and do not take the XCD order, smooth and full-range data, chunked regions):
     linear3pm's lowres + maps equal the generic bf16x2 path's bit for bit (KMP_DISABLE_LINEAR_FUSED),
     and the round trip is lossless."""
@@ -241,35 +245,41 @@ def test_linear_bf16x2_p1_fused_sweep(kom):
         B = int(rng.choice([1, 2, 3, 8]))
         D = int(rng.integers(6, 24))
         H, W = int(rng.choice([32, 64])), int(rng.choice([32, 64]))
-        hi = _data((B, D, H, W, 1), np.uint16, 100 + case)
+        hi = _data((B, D, H, W, 1), dtype, 100 + case)
         if case % 2:  # smooth data: small residuals, the predictor's realistic regime
             z, y, x = np.meshgrid(np.arange(D), np.arange(H), np.arange(W), indexing='ij')
-            hi = ((1000 + 40 * z + 25 * y + 10 * x)[None, ..., None] + rng.integers(0, 9, (B, D, H, W, 1))).astype(np.uint16)
-        w, b = _weights(3, 1, 200 + case, np.uint16)
+            sc = 1 if dtype == np.uint16 else 0.1
+            hi = ((1000 + 40 * z + 25 * y + 10 * x)[None, ..., None] * sc + rng.integers(0, 9, (B, D, H, W, 1))
+                  ).astype(np.int64) % (np.iinfo(dtype).max + 1)
+            hi = hi.astype(dtype)
+        w, b = _weights(3, 1, 200 + case, dtype)
         pred = kom.LinearPredictor(w, b, 1, 3, arith='bf16x2')
         hi_t = torch.from_numpy(hi).cuda()
-        lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, hi_t, padding=1)
+        enc, dec = ((V.encode_values_uint16, V.decode_values_uint16) if dtype == np.uint16
+                    else (V.encode_values_uint8, V.decode_values_uint8))
+        lo, (maps, dims) = V.encode(pred, enc, hi_t, padding=1)
         assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_encode', (B, D, H, W)
         chunk = int(rng.integers(4, 12))
-        lo_c, (maps_c, _) = V.encode_chunks(pred, V.encode_values_uint16, hi_t, chunk=chunk, padding=1)
+        lo_c, (maps_c, _) = V.encode_chunks(pred, enc, hi_t, chunk=chunk, padding=1)
         with kom._lib.option('KMP_DISABLE_LINEAR_FUSED', 1):
-            lo_g, (maps_g, _) = V.encode(pred, V.encode_values_uint16, hi_t, padding=1)
+            lo_g, (maps_g, _) = V.encode(pred, enc, hi_t, padding=1)
             assert kom._lib.lib.kmp_last_launch().decode() == 'encode_generic'
         assert torch.equal(lo, lo_g) and torch.equal(lo_c, lo_g)
         for i, (a, c, g) in enumerate(zip(maps, maps_c, maps_g)):
             assert torch.equal(a, g), f'case {case} map {i}: {int((a != g).sum())} mismatches'
             assert torch.equal(c, g), f'case {case} chunked map {i}'
-        rec = V.decode(pred, V.decode_values_uint16, lo, (maps, dims), padding=1)
+        rec = V.decode(pred, dec, lo, (maps, dims), padding=1)
         assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_decode'
         assert torch.equal(rec, hi_t)
-        rec_c = V.decode_chunks(pred, V.decode_values_uint16, lo, (maps, dims), chunk=chunk, padding=1)
+        rec_c = V.decode_chunks(pred, dec, lo, (maps, dims), chunk=chunk, padding=1)
         assert torch.equal(rec_c, hi_t)
 
 
 # ---- arith='auto' (the default) ----
 
 AUTO_CASES = [(3, 1, (2, 32, 32, 32, 1), np.uint16, 'bf16x2'), (3, 1, (1, 17, 30, 16, 1), np.uint16, 'bf16x2'),
-              (3, 0, (2, 32, 32, 32, 1), np.uint16, 'f32'), (3, 1, (2, 32, 32, 32, 1), np.uint8, 'f32'),
+              (3, 0, (2, 32, 32, 32, 1), np.uint16, 'f32'), (3, 1, (2, 32, 32, 32, 1), np.uint8, 'bf16x2'),
+              (3, 1, (1, 13, 22, 32, 1), np.uint8, 'bf16x2'), (3, 0, (1, 16, 32, 32, 1), np.uint8, 'f32'),
               (2, 1, (2, 64, 64, 1), np.uint16, 'f32')]
 
 

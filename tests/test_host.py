@@ -245,7 +245,9 @@ def test_linear_auto_arith_rule():
     import torch
     from kompressor_amd.predictors import resolve_arith
     assert resolve_arith('auto', 1, 3, torch.uint16) == 'bf16x2'
-    for p, nd, dt in ((0, 3, torch.uint16), (2, 3, torch.uint16), (1, 3, torch.uint8), (1, 2, torch.uint16),
+    assert resolve_arith('auto', 1, 3, torch.uint8) == 'bf16x2'
+    for p, nd, dt in ((0, 3, torch.uint16), (2, 3, torch.uint16), (0, 3, torch.uint8), (1, 2, torch.uint16),
+                      (1, 2, torch.uint8),
                       (1, 3, torch.int32), (1, 3, torch.uint32)):
         assert resolve_arith('auto', p, nd, dt) == 'f32'
     for a in ('f32', 'bf16x2'):

@@ -136,6 +136,18 @@ def main():
         codec_rows(f'volume_linear_bf16x2_p{p}', V, OV, vol, vol_h, kom.LinearPredictor(w, b, p, 3, arith='bf16x2'),
                    None, V.encode_values_uint16, V.decode_values_uint16, None, None, p, raw_v, 3, with_cpu=False)
 
+    # uint8 volumes at C3 geometry (512 tiles of 64^3), p = 1: the f32 chain vs the matrix cores
+    # (linear3pm's u8 form, the 'auto' default since round 6)
+    if not want or want & {'volume_linear_u8_p1', 'volume_linear_bf16x2_u8_p1'}:
+        vol8_h = rand((512, 64, 64, 64, 1), np.uint8)
+        vol8 = torch.from_numpy(vol8_h).cuda()
+        w = (1.0 / 64 + np.random.default_rng(2).standard_normal((64, 19)) * (0.3 / 64)).astype(np.float32)
+        b = np.zeros(19, np.float32)
+        for tag, ar in (('volume_linear_u8_p1', 'f32'), ('volume_linear_bf16x2_u8_p1', 'bf16x2')):
+            codec_rows(tag, V, OV, vol8, vol8_h, kom.LinearPredictor(w, b, 1, 3, arith=ar), None,
+                       V.encode_values_uint8, V.decode_values_uint8, None, None, 1, vol8.numel(), 3, with_cpu=False)
+        del vol8
+
     for p in (0,):
         n = (2 * p + 2) ** 2
         w = (1.0 / n + rng.standard_normal((n, 5)) * (0.3 / n)).astype(np.float32)

@@ -41,6 +41,8 @@ if wl == 'rice':  # Rice bundle encode + decode of 8 C3-sized u16 maps of N(0, s
     sys.exit(0)
 ndim = 3 if wl == 'volume' else 2
 shape, dt = ((512, 64, 64, 64, 1), np.uint16) if ndim == 3 else ((1024, 256, 256, 1), np.uint8)
+if os.environ.get('KMP_KT_U8') == '1' and ndim == 3:  # uint8 volumes at C3 geometry
+    dt = np.uint8
 host = np.random.default_rng(0).integers(0, np.iinfo(dt).max + 1, size=shape, dtype=np.int64).astype(dt)
 hi = torch.from_numpy(host).cuda()
 if len(sys.argv) > 4 and sys.argv[4] in ('linear', 'linearmx'):
