@@ -290,13 +290,16 @@ def to_host(t):
     t = t.contiguous()
     if nbytes <= PINNED_OUT_MAX and _pin_result(nbytes):
         host = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
-        weakref.finalize(host, _unpin_result, nbytes)  # the numpy view keeps ``host`` alive
         with torch.cuda.device(t.device):
             s = torch.cuda.current_stream(t.device)
             with torch.cuda.stream(s):
                 host.copy_(t, non_blocking=True)
             s.synchronize()
-        return host.numpy()
+        arr = host.numpy()
+        # the array (and any view of it, whose base it is) holds the pinned storage; the Python
+        # tensor object may go away first, so the budget follows the array
+        weakref.finalize(arr, _unpin_result, nbytes)
+        return arr
     out = np.empty(tuple(t.shape), dtype=torch.empty(0, dtype=t.dtype).numpy().dtype)
     dst = out.reshape(-1).view(np.uint8)
     with torch.cuda.device(t.device):
