@@ -145,11 +145,11 @@ __device__ __forceinline__ void sweep(const float* st, const L3P& a, int Yc, int
 // kernel's FULL body, kmp_codec_linear3d.hip)
 template <typename T, bool DEC, int P, bool FULL>
 __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
-  constexpr int VX = 4;  // u16: 4 outputs per lane
-  static_assert(sizeof(T) == 2, "u16");
-  constexpr uint32_t MASK = 0xffffu;
+  constexpr int VX = 4;  // 4 outputs per lane (u8 and u16: kmp_wave.h's 4-cell segments)
+  static_assert(sizeof(T) <= 2, "u8 / u16");
+  constexpr uint32_t MASK = sizeof(T) == 2 ? 0xffffu : 0xffu;
   constexpr int NPL = 2 * P + 3;  // staged node planes c-1-P .. c+P+1
-  using V = typename std::conditional<DEC, uint2, uint4>::type;
+  using V = typename std::conditional<DEC, MSeg<T>, HSeg<T>>::type;
   // LDS: staged node planes [NPL][nr][pitch] f32, then the exchange rows [wave][kXch][Ex]
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   float* st = (float*)smem;
@@ -207,27 +207,27 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   for (int t = 0; t < NPL; ++t) {
     const int sz = lsrc1(c - 1 - P + t, a.Lz, a.Ez);
     if constexpr (DEC) {
-      if (live) own[t] = ld8c(lin + sz * lplane + lo_own);
+      if (live) own[t] = ldMc<T>(lin + sz * lplane + lo_own);
     } else {
-      if (live) own[t] = ld16c(hin + 2 * sz * hplane + ho_own);
+      if (live) own[t] = ldHc<T>(hin + 2 * sz * hplane + ho_own);
     }
   }
-  uint4 e1 = make_uint4(0, 0, 0, 0), o0 = e1, o1 = e1;
-  uint2 mv[7];
+  HSeg<T> e1{}, o0{}, o1{};
+  MSeg<T> mv[7];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) mv[k] = make_uint2(0, 0);
+  for (int k = 0; k < 7; ++k) mv[k] = MSeg<T>{};
   if constexpr (DEC) {
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       int par[3];
       map_parity(3, k, par);
-      if (mok_y[k] && (!par[0] || vz1)) mv[k] = ld8(mbase[k] + c * mplane[k]);
+      if (mok_y[k] && (!par[0] || vz1)) mv[k] = ldM<T>(mbase[k] + c * mplane[k]);
     }
   } else {
     const T* p = hin + 2 * c * hplane;
-    if (live && vy1) e1 = ld16(p + ho_own + a.W_);
-    if (live && vz1) o0 = ld16(p + hplane + ho_own);
-    if (live && vz1 && vy1) o1 = ld16(p + hplane + ho_own + a.W_);
+    if (live && vy1) e1 = ldH<T>(p + ho_own + a.W_);
+    if (live && vz1) o0 = ldH<T>(p + hplane + ho_own);
+    if (live && vz1 && vy1) o1 = ldH<T>(p + hplane + ho_own + a.W_);
   }
 
   // ---- stage: every lane writes its 4 nodes of each plane, plus the mirrored halo columns /
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
       float v[VX];
 #pragma unroll
       for (int i = 0; i < VX; ++i)
-        v[i] = (float)(DEC ? el8<T>(*(const uint2*)&own[t], i) : el16<T>(*(const uint4*)&own[t], 2 * i));
+        v[i] = (float)(DEC ? elM<T>(*(const MSeg<T>*)&own[t], i) : elH<T>(*(const HSeg<T>*)&own[t], 2 * i));
       auto put_row = [&](int ry) __attribute__((always_inline)) {
         float* row = st + (t * a.nr + ry) * a.pitch + P + X;
 #pragma unroll
@@ -333,22 +333,22 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
   auto put8 = [&](int k, const uint32_t (&res)[VX]) {
     int par[3];
     map_parity(3, k, par);
-    if (mok_y[k] && (!par[0] || vz1)) st8((T*)mbase[k] + c * mplane[k], pack8<T, VX>(res));
+    if (mok_y[k] && (!par[0] || vz1)) stM<T>((T*)mbase[k] + c * mplane[k], packM<T>(res));
   };
   const int tc = 1 + P;  // staged plane index of node plane c
-  const uint4 e0 = DEC ? uint4{} : *(const uint4*)&own[tc];
+  const HSeg<T> e0 = DEC ? HSeg<T>{} : *(const HSeg<T>*)&own[tc];
   T* h0 = DEC ? hout + 2 * c * hplane + ho_own : nullptr;
   uint32_t ownv[VX];
 #pragma unroll
   for (int i = 0; i < VX; ++i) {
-    if constexpr (DEC) ownv[i] = el8<T>(*(const uint2*)&own[tc], i);
-    else ownv[i] = el16<T>(e0, 2 * i);
+    if constexpr (DEC) ownv[i] = elM<T>(*(const MSeg<T>*)&own[tc], i);
+    else ownv[i] = elH<T>(e0, 2 * i);
   }
-  auto code = [&](int k, const uint32_t (&pred)[VX], const uint4& src, int odd, uint32_t (&outv)[VX]) {
+  auto code = [&](int k, const uint32_t (&pred)[VX], const HSeg<T>& src, int odd, uint32_t (&outv)[VX]) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
-      if constexpr (DEC) outv[i] = (pred[i] + el8<T>(mv[k], i)) & MASK;
-      else outv[i] = (el16<T>(src, 2 * i + odd) - pred[i]) & MASK;
+      if constexpr (DEC) outv[i] = (pred[i] + elM<T>(mv[k], i)) & MASK;
+      else outv[i] = (elH<T>(src, 2 * i + odd) - pred[i]) & MASK;
     }
   };
 
@@ -360,9 +360,9 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
                  m(Q18, i + 1, vz0, vy1)) >> ((nz * ny) >> 1);
     code(6, pred, e0, 1, outv);
     if constexpr (DEC) {
-      st16(h0, pack16<T, VX>(ownv, outv));
+      stH<T>(h0, packH<T>(ownv, outv));
     } else {
-      st8((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, pack8<T, VX>(ownv));
+      stM<T>((T*)a.lo_out + b * (int64_t)a.Ez * lplane + c * lplane + lo_own, packM<T>(ownv));
       put8(6, outv);
     }
   }
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
     code(5, pY, e1, 0, oY);
     code(2, pF, e1, 1, oF);
     if constexpr (DEC) {
-      if (vy1) st16(h0 + a.W_, pack16<T, VX>(oY, oF));
+      if (vy1) stH<T>(h0 + a.W_, packH<T>(oY, oF));
     } else {
       put8(5, oY);
       put8(2, oF);
@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
     code(4, pZ, o0, 0, oZ);
     code(1, pU, o0, 1, oU);
     if constexpr (DEC) {
-      if (vz1) st16(h0 + hplane, pack16<T, VX>(oZ, oU));
+      if (vz1) stH<T>(h0 + hplane, packH<T>(oZ, oU));
     } else {
       put8(4, oZ);
       put8(1, oU);
@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(256) linear3dp_kernel(L3P a) {
     code(0, pL, o1, 0, oL);
     code(3, pC, o1, 1, oC);
     if constexpr (DEC) {
-      if (vz1 && vy1) st16(h0 + hplane + a.W_, pack16<T, VX>(oL, oC));
+      if (vz1 && vy1) stH<T>(h0 + hplane + a.W_, packH<T>(oL, oC));
     } else {
       put8(0, oL);
       put8(3, oC);
@@ -431,11 +431,11 @@ template <typename T>
 static bool linear3dp_geometry(const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred,
                                const kmp_region* region, l3p::L3P& a, dim3& grid, dim3& block, size_t& lds) {
   constexpr int VX = 4;
-  if (!std::is_same<T, uint16_t>::value) return false;
+  if (!std::is_same<T, uint16_t>::value && !std::is_same<T, uint8_t>::value) return false;
   if (opt(OPT_DISABLE_FAST, 0) || opt(OPT_DISABLE_LINEAR_FUSED, 0)) return false;
   if (C != 1 || pred->kind != KMP_PRED_LINEAR || pred->padding != 1 || !pred->weights || !pred->bias) return false;
   const int P = pred->padding;
-  if (g.n[2] % 2 != 0 || (g.n[2] * (int64_t)sizeof(T)) % 16 != 0) return false;
+  if (g.n[2] % 8 != 0) return false;  // 8-sample highres row segments, aligned
   if (g.n[0] * g.n[1] * g.n[2] >= ((int64_t)1 << 31)) return false;
   const int64_t txn = g.E[2] / VX;
   if (txn * VX != g.E[2] || txn < 1 || txn > 32 || (txn & (txn - 1)) != 0) return false;
@@ -475,14 +475,15 @@ template <typename T>
 int try_linear3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const kmp_predictor* pred, T* lowres,
                          const MapPtrs& maps, const kmp_region* region, void* ws, size_t ws_bytes,
                          hipStream_t stream) {
-  if constexpr (std::is_same<T, uint16_t>::value) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
     if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
-    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    constexpr uintptr_t HA = 8 * sizeof(T) - 1, MA = 4 * sizeof(T) - 1;  // segment alignments
+    if (((uintptr_t)hi & HA) || ((uintptr_t)lowres & MA)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k)
-      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      if ((uintptr_t)maps.p[k] & MA) return KMP_ERR_UNSUPPORTED;
     a.hi_in = hi;
     a.lo_out = lowres;
     a.maps = maps;
@@ -502,14 +503,15 @@ template <typename T>
 int try_linear3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int64_t B, int64_t C,
                          const kmp_predictor* pred, T* hi, const kmp_region* region, void* ws, size_t ws_bytes,
                          hipStream_t stream) {
-  if constexpr (std::is_same<T, uint16_t>::value) {
+  if constexpr (std::is_same<T, uint16_t>::value || std::is_same<T, uint8_t>::value) {
     l3p::L3P a{};
     dim3 grid, block;
     size_t lds = 0;
     if (!linear3dp_geometry<T>(g, B, C, pred, region, a, grid, block, lds)) return KMP_ERR_UNSUPPORTED;
-    if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
+    constexpr uintptr_t HA = 8 * sizeof(T) - 1, MA = 4 * sizeof(T) - 1;
+    if (((uintptr_t)hi & HA) || ((uintptr_t)lowres & MA)) return KMP_ERR_UNSUPPORTED;
     for (int k = 0; k < 7; ++k) {
-      if ((uintptr_t)maps.p[k] & 7) return KMP_ERR_UNSUPPORTED;
+      if ((uintptr_t)maps.p[k] & MA) return KMP_ERR_UNSUPPORTED;
       a.maps.p[k] = (void*)maps.p[k];
     }
     a.hi_out = hi;

@@ -94,54 +94,8 @@ __host__ __device__ constexpr int slot_of(int k, int q) {
   return s[k] + (s[k] >= 14 ? 5 * q : 0);
 }
 
-// Per-lane global segments of the sample dtype T (a lane owns VX = 4 cells of a row for either
-// dtype): a highres row segment is the 8 samples of its cells' two highres columns (16 B for u16,
-// 8 B for u8), a lowres / map segment the 4 cells (8 B / 4 B).  The channel table holds u16 either
-// way (u8 predictions saturate at 255 before they are stored).
-template <typename T> using HSeg = typename std::conditional<sizeof(T) == 2, uint4, uint2>::type;
-template <typename T> using MSeg = typename std::conditional<sizeof(T) == 2, uint2, uint32_t>::type;
-template <typename T> __device__ __forceinline__ HSeg<T> ldH(const T* p) {
-  if constexpr (sizeof(T) == 2) return ld16(p);
-  else return ld8(p);
-}
-template <typename T> __device__ __forceinline__ HSeg<T> ldHc(const T* p) {
-  if constexpr (sizeof(T) == 2) return ld16c(p);
-  else return ld8c(p);
-}
-template <typename T> __device__ __forceinline__ MSeg<T> ldM(const T* p) {
-  if constexpr (sizeof(T) == 2) return ld8(p);
-  else return __builtin_nontemporal_load((const uint32_t*)p);
-}
-template <typename T> __device__ __forceinline__ MSeg<T> ldMc(const T* p) {
-  if constexpr (sizeof(T) == 2) return ld8c(p);
-  else return *(const uint32_t*)p;
-}
-template <typename T> __device__ __forceinline__ void stH(T* p, const HSeg<T>& v) {
-  if constexpr (sizeof(T) == 2) st16(p, v);
-  else st8(p, v);
-}
-template <typename T> __device__ __forceinline__ void stM(T* p, const MSeg<T>& v) {
-  if constexpr (sizeof(T) == 2) st8(p, v);
-  else __builtin_nontemporal_store(v, (uint32_t*)p);
-}
-template <typename T> __device__ __forceinline__ uint32_t elH(const HSeg<T>& v, int e) {  // sample e < 8
-  if constexpr (sizeof(T) == 2) return el16<T>(v, e);
-  else return el8<T>(v, e);
-}
-template <typename T> __device__ __forceinline__ uint32_t elM(const MSeg<T>& v, int i) {  // cell i < 4
-  if constexpr (sizeof(T) == 2) return el8<T>(v, i);
-  else return (v >> (8 * i)) & 0xffu;
-}
-template <typename T> __device__ __forceinline__ MSeg<T> packM(const uint32_t (&v)[4]) {
-  if constexpr (sizeof(T) == 2) return pack8<T, 4>(v);
-  else return (v[0] & 0xffu) | ((v[1] & 0xffu) << 8) | ((v[2] & 0xffu) << 16) | (v[3] << 24);
-}
-template <typename T> __device__ __forceinline__ HSeg<T> packH(const uint32_t (&ev)[4], const uint32_t (&od)[4]) {
-  if constexpr (sizeof(T) == 2) return pack16<T, 4>(ev, od);
-  else
-    return make_uint2((ev[0] & 0xffu) | ((od[0] & 0xffu) << 8) | ((ev[1] & 0xffu) << 16) | (od[1] << 24),
-                      (ev[2] & 0xffu) | ((od[2] & 0xffu) << 8) | ((ev[3] & 0xffu) << 16) | (od[3] << 24));
-}
+// (the 4-cell segments of either sample dtype: kmp_wave.h's HSeg / MSeg helpers; the channel table
+// holds u16 either way, u8 predictions saturating at 255 before they are stored)
 // an MFMA result's 4 cells cast to T (XLA astype) as the table's packed u16; ``late``: the u16
 // form without the hazard pad (see kmp_bf16x2.h), for a caller with >= 8 MFMAs in between
 template <typename T, bool LATE> __device__ __forceinline__ uint2 cast_cells(const bx::f32x4& v) {

@@ -83,27 +83,29 @@ def test_linear_chunks(kom):
         assert np.array_equal(rec, hi)
 
 
+@pytest.mark.parametrize('dtype', [np.uint16, np.uint8])
 @pytest.mark.parametrize('shape', [(8, 64, 64, 64, 1), (2, 17, 30, 16, 1), (1, 9, 14, 128, 1), (2, 12, 33, 32, 1),
                                    (1, 6, 8, 8, 1), (1, 10, 40, 32, 1), (2, 9, 32, 128, 1)])
-def test_linear_fused_p1(kom, shape):
-    """The fused LinearPredictor p = 1 volume kernel (kmp_codec_linear3dp.hip, packed-FMA chain):
-    residuals and lowres bit-exact to the oracle's fma chain + aggregation, lossless, z-region
-    (chunked) launches, over lowres widths 4 .. 64 and partial last waves."""
-    hi = _data(shape, np.uint16, 7)
-    w, b = _weights(3, 1, 8, np.uint16)
+def test_linear_fused_p1(kom, shape, dtype):
+    """The fused LinearPredictor p = 1 volume kernel (kmp_codec_linear3dp.hip, packed-FMA chain; 8-bit
+    samples since round 6): residuals and lowres bit-exact to the oracle's fma chain + aggregation,
+    lossless, z-region (chunked) launches, over lowres widths 4 .. 64 and partial last waves."""
+    hi = _data(shape, dtype, 7)
+    w, b = _weights(3, 1, 8, dtype)
     pred = kom.LinearPredictor(w, b, 1, 3, arith='f32')
     V, OV = kom.volume, oracle.volume
-    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
-                                                padding=1)
-    lo, (maps, dims) = V.encode(pred, V.encode_values_uint16, hi, padding=1)
+    enc, dec, oenc = ((V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16) if dtype == np.uint16
+                      else (V.encode_values_uint8, V.decode_values_uint8, OV.encode_values_uint8))
+    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), oenc, hi, padding=1)
+    lo, (maps, dims) = V.encode(pred, enc, hi, padding=1)
     assert kom._lib.lib.kmp_last_launch().decode() == 'linear3dp_encode'
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     for i, (a, c) in enumerate(zip(maps, want_maps)):
         bad = np.argwhere(a != c)
         assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
-    assert np.array_equal(V.decode(pred, V.decode_values_uint16, lo, (maps, dims), padding=1), hi)
+    assert np.array_equal(V.decode(pred, dec, lo, (maps, dims), padding=1), hi)
     assert kom._lib.lib.kmp_last_launch().decode() == 'linear3dp_decode'
-    lo2, (maps2, _) = V.encode_chunks(pred, V.encode_values_uint16, hi, chunk=5, padding=1)
+    lo2, (maps2, _) = V.encode_chunks(pred, enc, hi, chunk=5, padding=1)
     assert np.array_equal(lo2, want_lo) and all(np.array_equal(a, c) for a, c in zip(maps2, want_maps))
 
 
