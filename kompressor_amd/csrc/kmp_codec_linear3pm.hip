@@ -104,19 +104,17 @@ template <typename T, bool LATE> __device__ __forceinline__ uint2 cast_cells(con
 }
 
 // The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
-// biases, built once per call into the workspace instead of in every wave (64 bf16 splits a lane)
+// biases, built once per call into the workspace instead of in every wave: one workgroup per
+// (tile, step), a lane one fragment (a single wave building all 24 serialised their weight loads:
+// 22 us per call, as long as a tenth of the codec kernel)
+constexpr int kFragBlocks = 3 * 8;
 __global__ void __launch_bounds__(64) fragments_kernel(const float* __restrict__ W, const float* __restrict__ bias,
                                                        bx::u32x4* __restrict__ frag) {
   const int lane = threadIdx.x, m = lane & 15, g = lane >> 4;
-  float* fb = (float*)(frag + 3 * 8 * 64);
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {  // C, Q, and a zero tile (the channels of a cell plane outside the tile)
-    const int ch = t == 0 ? kCch[m] : t == 1 ? kQch[m] : -1;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      frag[(t * 8 + q) * 64 + lane] = bx::b_fragment(W + (ch >= 0 ? ch : 0), 19, 64, 3, 1, q, g, ch >= 0);
-    fb[t * 64 + lane] = ch >= 0 ? bias[ch] : 0.0f;
-  }
+  const int t = blockIdx.x / 8, q = blockIdx.x % 8;  // C, Q, and a zero tile (a cell plane outside the tile)
+  const int ch = t == 0 ? kCch[m] : t == 1 ? kQch[m] : -1;
+  frag[(t * 8 + q) * 64 + lane] = bx::b_fragment(W + (ch >= 0 ? ch : 0), 19, 64, 3, 1, q, g, ch >= 0);
+  if (q == 0) ((float*)(frag + 3 * 8 * 64))[t * 64 + lane] = ch >= 0 ? bias[ch] : 0.0f;
 }
 constexpr size_t kFragBytes = 3 * 8 * 64 * sizeof(bx::u32x4) + 3 * 64 * sizeof(float);
 // + the dummy store slots (8 u16 per lane) after the fragments
@@ -675,7 +673,7 @@ int try_linear3pm_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const 
     a.b = pred->bias;
     if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
-    l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
+    l3q::fragments_kernel<<<l3q::kFragBlocks, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
     launch_linear3pm<T, false>(a, grid, block, stream);
     return check_launch("linear3pm_encode");
   }
@@ -702,7 +700,7 @@ int try_linear3pm_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, in
     a.b = pred->bias;
     if (!ws || ws_bytes < l3q::kWsBytes || ((uintptr_t)ws & 15)) return KMP_ERR_UNSUPPORTED;
     a.frag = (const bx::u32x4*)ws;
-    l3q::fragments_kernel<<<1, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
+    l3q::fragments_kernel<<<l3q::kFragBlocks, 64, 0, stream>>>(pred->weights, pred->bias, (bx::u32x4*)ws);
     launch_linear3pm<T, true>(a, grid, block, stream);
     return check_launch("linear3pm_decode");
   }

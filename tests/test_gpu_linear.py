@@ -334,39 +334,48 @@ def _smooth_c3(n, seed):
 
 
 FLIP_CASES = ['golden:vol_tile64_p1', 'smooth_c3', 'golden:vol_ramp_even_p1', 'golden:vol_rand_mixed_p1',
-              'golden:vol_tile_small_p1', 'golden:vol_ramp_odd_p1']
+              'golden:vol_tile_small_p1', 'golden:vol_ramp_odd_p1',
+              # uint8 volumes (the default is bf16x2 there too since round 6)
+              'golden:vol_fast_u8_p1', 'golden:vol_rand_u8_c3_p1', 'smooth_c3_u8', 'rand_c3_u8']
 
 
 @pytest.mark.parametrize('case', FLIP_CASES)
 def test_linear_auto_p1_flips_vs_f32_oracle(kom, case):
-    """The default arithmetic for u16 volumes at padding 1 (arith='auto' -> bf16x2, the matrix cores)
-    against the oracle's f32 fma chain, on the C3 tile and the golden p = 1 inputs:
+    """The default arithmetic for u8 / u16 volumes at padding 1 (arith='auto' -> bf16x2, the matrix
+    cores) against the oracle's f32 fma chain, on C3 tiles and the golden p = 1 inputs:
       * a cell prediction differs only by +-1, and only where the float64 value lies within the north
         star's 1e-5 (relative to sum|f w| + |b|) of the integer boundary the two truncations straddle;
-      * a residual differs from the oracle's f32 residual only by +-1 mod 2^16, and only at a position
+      * a residual differs from the oracle's f32 residual only by +-1 mod 2^bits, and only at a position
         whose aggregation (maps_from_predictions) takes a flipped cell;
       * the mismatch rates are printed (run with -s), and the round trip is lossless."""
     from conftest import GOLDEN
     V, OV = kom.volume, oracle.volume
     if case.startswith('golden:'):
         hi = np.load(f'{GOLDEN}/{case[7:]}.npz')['highres']
-    else:
+    elif case == 'smooth_c3':
         hi = _smooth_c3(2, 31)
-    w, b = _weights(3, 1, 21, np.uint16)
+    elif case == 'smooth_c3_u8':
+        hi = (_smooth_c3(2, 32) >> 8).astype(np.uint8)
+    else:
+        hi = _data((2, 64, 64, 64, 1), np.uint8, 33)
+    dt = hi.dtype.type
+    mod = np.iinfo(dt).max + 1
+    w, b = _weights(3, 1, 21, dt)
     auto = kom.LinearPredictor(w, b, 1, 3)
-    assert auto.arith_for(torch.uint16) == 'bf16x2'
-    lo, (maps, dims) = V.encode(auto, V.encode_values_uint16, hi, padding=1)
+    assert auto.arith_for(torch.from_numpy(hi[:0]).dtype) == 'bf16x2'
+    enc, dec, oenc = ((V.encode_values_uint16, V.decode_values_uint16, OV.encode_values_uint16) if dt == np.uint16
+                      else (V.encode_values_uint8, V.decode_values_uint8, OV.encode_values_uint8))
+    lo, (maps, dims) = V.encode(auto, enc, hi, padding=1)
     if hi.shape[1:] == (64, 64, 64, 1):
         assert kom._lib.lib.kmp_last_launch().decode() == 'linear3pm_encode'
-    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), OV.encode_values_uint16, hi,
-                                                padding=1)
+    want_lo, (want_maps, want_dims) = OV.encode(OP.linear_predictions_fn(1, w, b, 3), oenc, hi, padding=1)
     assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
     # cells
     window = OV.pad_neighborhood(OV.lowres_from_highres(OV.pad_highres(hi)[0]), 1)
     feats = OV.features_from_lowres(window, 1)
-    o_cells = OP.cast_from_f32(OP.linear_fma_chain(feats, w, b), np.uint16)
+    o_cells = OP.cast_from_f32(OP.linear_fma_chain(feats, w, b), dt)
     h_cells, h_f32 = auto.predict_cells(window, with_f32=True)
-    f64, _ = OP.linear_predictions(feats, w, b, np.uint16)
+    f64, _ = OP.linear_predictions(feats, w, b, dt)
     scale = np.tensordot(np.moveaxis(np.abs(feats.astype(np.float64)), 4, -1), np.abs(w.astype(np.float64)),
                          axes=([-1], [0]))
     scale = np.moveaxis(scale, -1, 4) + np.abs(b).reshape(-1, 1)
@@ -381,14 +390,14 @@ def test_linear_auto_p1_flips_vs_f32_oracle(kom, case):
     nbad = ntot = 0
     for i, (a, c, t) in enumerate(zip(maps, want_maps, touched)):
         bad = a != c
-        dd = (a.astype(np.int64) - c.astype(np.int64)) % 65536
-        assert np.all((dd[bad] == 1) | (dd[bad] == 65535)), f'map {i}: {np.unique(dd[bad])}'
+        dd = (a.astype(np.int64) - c.astype(np.int64)) % mod
+        assert np.all((dd[bad] == 1) | (dd[bad] == mod - 1)), f'map {i}: {np.unique(dd[bad])}'
         assert np.all(t[bad] > 0), f'map {i}: a residual mismatch with no flipped cell in its aggregation'
         nbad += int(bad.sum())
         ntot += bad.size
     print(f'\n[flip-rate {case}] cells {int(flips.sum())} / {flips.size} = {flips.mean():.3e}; '
           f'residuals {nbad} / {ntot} = {nbad / ntot:.3e}')
-    assert np.array_equal(V.decode(auto, V.decode_values_uint16, lo, (maps, dims), padding=1), hi)
+    assert np.array_equal(V.decode(auto, dec, lo, (maps, dims), padding=1), hi)
 
 
 def test_linear_bf16x2_golden(kom):
