@@ -100,7 +100,7 @@ __host__ __device__ constexpr int slot_of(int k, int q) {
 // form without the hazard pad (see kmp_bf16x2.h), for a caller with >= 8 MFMAs in between
 template <typename T, bool LATE> __device__ __forceinline__ uint2 cast_cells(const bx::f32x4& v) {
   if constexpr (sizeof(T) == 2) return LATE ? bx::cast_pack4_u16_late(v) : bx::cast_pack4_u16(v);
-  else return bx::cast_pack4<uint16_t>(v, 255.0f);
+  else return LATE ? bx::cast_pack4_u8_late(v) : bx::cast_pack4_u8(v);
 }
 
 // The weights' B fragments of both column tiles (kmp_bf16x2.h's b_fragment) and the per-column
