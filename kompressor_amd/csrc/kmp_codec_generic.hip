@@ -15,6 +15,8 @@
 // (pad_neighborhood volume/utils.py:213-218).  Costs ~1.25x the HBM bytes of the one-pass
 // fast kernels (kmp_codec_fast3d.hip); used whenever those are not eligible.
 #include "kmp_codec.h"
+#include "kmp_aggregate.h"
+#include "kmp_wave.h"
 
 namespace kmp {
 
@@ -30,108 +32,240 @@ struct Src {
   int32_t mult;  // 2 (encode: lowres node j <- highres 2j) or 1 (decode)
 };
 
-template <typename T>
-__device__ __forceinline__ T lowres_node(const T* __restrict__ src, const Src& s, const Geo& g, int64_t b, int64_t c,
-                                         int64_t C, int64_t jz, int64_t jy, int64_t jx) {
-  const int64_t z = s.mult * sym_index(sym_index(jz, g.L[0]), g.E[0]);
-  const int64_t y = s.mult * sym_index(sym_index(jy, g.L[1]), g.E[1]);
-  const int64_t x = s.mult * sym_index(sym_index(jx, g.L[2]), g.E[2]);
-  return src[(((b * s.S[0] + z) * s.S[1] + y) * s.S[2] + x) * C + c];
-}
-
 // Cell mean, float32 sum in feature order (z-major, y, x) / N, XLA cast (the reference test
 // predictor).  Exact (order-independent) for uint8 with p <= 4 and uint16 with p <= 2.
 struct Frame {
   int64_t begin[3], ext[3];
 };
 
-// ``cf`` is the box of cells to compute (a region launch needs cells [begin-1, end) only);
-// results land at their global position in ``cells`` [B, Lc..., C].
-template <typename T>
-__global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restrict__ src, Src s, Geo g, int nsp,
-                                                            int64_t B, int64_t C, int p, Frame cf,
-                                                            T* __restrict__ cells, int64_t total) {
-  const int k = 2 * p + 2;
-  const int kz = nsp == 3 ? k : 1;
-  const float inv_n = (float)(kz * k * k);
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b, cz, cy, cx, c;
-    unflat5(t, cf.ext[0], cf.ext[1], cf.ext[2], C, b, cz, cy, cx, c);
-    cz += cf.begin[0];
-    cy += cf.begin[1];
-    cx += cf.begin[2];
-    const int pz = nsp == 3 ? p : 0;
-    float sum = 0.0f;
-    for (int dz = 0; dz < kz; ++dz)
-      for (int dy = 0; dy < k; ++dy)
-        for (int dx = 0; dx < k; ++dx)
-          sum += (float)lowres_node(src, s, g, b, c, C, cz - pz + dz, cy - p + dy, cx - p + dx);
-    cells[(((b * g.Lc[0] + cz) * g.Lc[1] + cy) * g.Lc[2] + cx) * C + c] = cast_f32<T>(sum / inv_n);
+// Unsigned 32-bit division by a runtime constant as multiply-high + add + shift (the host computes
+// the magic number): n / d for n < 2^31.  The generic kernels' per-element index split was four
+// integer divisions (~40 VALU each, emulated); this is 3 VALU per division.
+struct FDiv {
+  uint32_t d, m, s;
+};
+static inline FDiv fdiv(int64_t d64) {
+  const uint32_t d = (uint32_t)(d64 < 1 ? 1 : d64);
+  uint32_t s = 0;
+  while (s < 32 && (1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FDiv{d, (uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv_q(uint32_t n, const FDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// The index space of a frame: t -> (b, i0, i1, i2, c), c fastest (as unflat5)
+struct Flat {
+  FDiv dC, d2, d1, d0;
+};
+static inline Flat make_flat(const int64_t (&ext)[3], int64_t C) {
+  return Flat{fdiv(C), fdiv(ext[2]), fdiv(ext[1]), fdiv(ext[0])};
+}
+template <typename I>
+__device__ __forceinline__ void unflat_i(int64_t t, const Flat& F, const int64_t (&ext)[3], int64_t C, I& b, I& i0,
+                                         I& i1, I& i2, I& c) {
+  if constexpr (sizeof(I) == 4) {  // t < 2^31 (the host's choice of I)
+    uint32_t u = (uint32_t)t, q;
+    q = fdiv_q(u, F.dC); c = (I)(u - q * F.dC.d); u = q;
+    q = fdiv_q(u, F.d2); i2 = (I)(u - q * F.d2.d); u = q;
+    q = fdiv_q(u, F.d1); i1 = (I)(u - q * F.d1.d); u = q;
+    q = fdiv_q(u, F.d0); i0 = (I)(u - q * F.d0.d); b = (I)q;
+  } else {
+    int64_t bb, z, y, x, cc;
+    unflat5(t, ext[0], ext[1], ext[2], C, bb, z, y, x, cc);
+    b = bb; i0 = z; i1 = y; i2 = x; c = cc;
   }
 }
 
-template <typename T, int CODER, bool PERCH>
-__global__ void __launch_bounds__(kGThreads) encode_generic_kernel(const T* __restrict__ hi, Geo g, int nsp, int64_t B,
+// astype(T) of the aggregation / mean: the saturating hardware conversion for 8- / 16-bit samples
+// (cvt_sat, kmp_wave.h), the exact restatement otherwise
+template <typename T>
+__device__ __forceinline__ T gcast(float v) {
+  if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) return (T)wv::cvt_sat<T>(v);
+  else return cast_f32<T>(v);
+}
+
+// the 7 (3) maps' lattice parities (z, y, x) and contributions at compile time (kmp_aggregate.h)
+template <int NSP>
+__device__ __forceinline__ constexpr int gpar(int k, int a) {
+  constexpr int8_t t3[7][3] = {{1, 1, 0}, {1, 0, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  constexpr int8_t t2[3][3] = {{0, 1, 0}, {0, 0, 1}, {0, 1, 1}};
+  return NSP == 3 ? t3[k][a] : t2[k][a];
+}
+
+// Lowres node source index along an axis: mult * sym(sym(j, L), E) (even reflect pad, then the
+// neighbourhood's symmetric pad)
+__device__ __forceinline__ int64_t node_src(int64_t j, int64_t L, int64_t E, int mult) {
+  return mult * sym_index(sym_index(j, L), E);
+}
+
+// ``cf`` is the box of cells to compute (a region launch needs cells [begin-1, end) only);
+// results land at their global position in ``cells`` [B, Lc..., C].  KK = 2p + 2 at compile time
+// (p <= 2: the node offsets per axis in registers, the (2p+2)^d loads unrolled) or 0 (any p).
+template <typename T, int NSP, int KK, typename I>
+__global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restrict__ src, Src s, Geo g, int64_t B,
+                                                            int64_t C, int p, Frame cf, Flat F, T* __restrict__ cells,
+                                                            int64_t total) {
+  const int k = KK ? KK : 2 * p + 2;
+  const int kz = NSP == 3 ? k : 1;
+  const int pz = NSP == 3 ? p : 0;
+  const float inv_n = (float)(kz * k * k);
+  const I Cc = (I)C, sy = (I)s.S[2] * Cc, sz = (I)s.S[1] * sy, sb = (I)s.S[0] * sz;
+  const I cy = (I)g.Lc[2] * Cc, cz = (I)g.Lc[1] * cy, cb = (I)g.Lc[0] * cz;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    I b, z, y, x, c;
+    unflat_i<I>(t, F, cf.ext, C, b, z, y, x, c);
+    z += (I)cf.begin[0];
+    y += (I)cf.begin[1];
+    x += (I)cf.begin[2];
+    const I base = b * sb + c;
+    float sum = 0.0f;
+    if constexpr (KK > 0) {
+      I ox[KK], oy[KK];
+#pragma unroll
+      for (int d = 0; d < KK; ++d) {
+        ox[d] = (I)node_src(x - p + d, g.L[2], g.E[2], s.mult) * Cc;
+        oy[d] = (I)node_src(y - p + d, g.L[1], g.E[1], s.mult) * sy;
+      }
+#pragma unroll
+      for (int dz = 0; dz < (NSP == 3 ? KK : 1); ++dz) {
+        const I zo = base + (NSP == 3 ? (I)node_src(z - pz + dz, g.L[0], g.E[0], s.mult) * sz : 0);
+#pragma unroll
+        for (int dy = 0; dy < KK; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < KK; ++dx) sum += (float)src[zo + oy[dy] + ox[dx]];
+      }
+    } else {
+      for (int dz = 0; dz < kz; ++dz) {
+        const I zo = base + (NSP == 3 ? (I)node_src(z - pz + dz, g.L[0], g.E[0], s.mult) * sz : 0);
+        for (int dy = 0; dy < k; ++dy) {
+          const I yo = zo + (I)node_src(y - p + dy, g.L[1], g.E[1], s.mult) * sy;
+          for (int dx = 0; dx < k; ++dx) sum += (float)src[yo + (I)node_src(x - p + dx, g.L[2], g.E[2], s.mult) * Cc];
+        }
+      }
+    }
+    cells[b * cb + z * cz + y * cy + x * Cc + c] = gcast<T>(sum / inv_n);
+  }
+}
+
+// Per output position o (and channel): the lowres node and the 7 (3) maps.  The cell values the
+// maps aggregate are read once: the 2^d cells o - {0,1}^d (MeanPredictor: one value per cell), or
+// each contribution's channel (LinearPredictor: K per cell); missing cells (past the cell box)
+// are skipped exactly as maps_from_predictions does, in the reference's channel order.
+template <typename T, int NSP, bool PERCH, typename I>
+struct GenCells {
+  const T* cells;
+  I base, sx, sy, sz;  // cells[base - dz sz - dy sy - dx sx + ch C]
+  I C;
+  bool v[2][2][2];     // cell o - (dz, dy, dx) exists
+  T m[2][2][2];        // MeanPredictor: the cell means
+
+  __device__ __forceinline__ void init(const T* c_, I b, I oz, I oy, I ox, I c, const Geo& g, int K, I Cc) {
+    cells = c_;
+    C = Cc;
+    const I kc = (I)(PERCH ? K : 1) * Cc;
+    sx = kc;
+    sy = (I)g.Lc[2] * kc;
+    sz = (I)g.Lc[1] * sy;
+    base = b * ((I)g.Lc[0] * sz) + oz * sz + oy * sy + ox * sx + c;
+    const bool vz[2] = {oz < (I)g.Lc[0], oz >= 1}, vy[2] = {oy < (I)g.Lc[1], oy >= 1},
+               vx[2] = {ox < (I)g.Lc[2], ox >= 1};
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          v[dz][dy][dx] = (NSP == 3 || dz == 0) && vz[dz] && vy[dy] && vx[dx];
+          if (!PERCH) m[dz][dy][dx] = v[dz][dy][dx] ? cells[base - dz * sz - dy * sy - dx * sx] : T(0);
+        }
+  }
+  __device__ __forceinline__ T get(int dz, int dy, int dx, int ch) const {
+    if constexpr (PERCH) return cells[base - dz * sz - dy * sy - dx * sx + (I)ch * C];
+    else return m[dz][dy][dx];
+  }
+  // map k's prediction (maps_from_predictions for one element)
+  __device__ __forceinline__ T pred(int k) const {
+    Contrib c[4];
+    const int nc = map_contribs(NSP, k, c);
+    if (k == center_map(NSP)) return get(0, 0, 0, c[0].ch);
+    float s = 0.0f;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nc) break;
+      if (v[c[i].dz][c[i].dy][c[i].dx]) {
+        s += (float)get(c[i].dz, c[i].dy, c[i].dx, c[i].ch);
+        ++cnt;
+      }
+    }
+    if (cnt == 4) s *= 0.25f;
+    else if (cnt == 2) s *= 0.5f;
+    return gcast<T>(s);
+  }
+};
+
+template <typename T, int CODER, bool PERCH, int NSP, typename I>
+__global__ void __launch_bounds__(kGThreads) encode_generic_kernel(const T* __restrict__ hi, Geo g, int64_t B,
                                                                  int64_t C, const T* __restrict__ cells, int K,
-                                                                 T* __restrict__ lowres, MapPtrs maps, Frame f,
+                                                                 T* __restrict__ lowres, MapPtrs maps, Frame f, Flat F,
                                                                  int64_t total) {
   using TO = typename coder_out<CODER>::type;
-  const int nmaps = nsp == 3 ? 7 : 3;
+  constexpr int NM = NSP == 3 ? 7 : 3;
+  const I Cc = (I)C;
+  const I hy = (I)g.n[2] * Cc, hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
+  const I ly = (I)g.E[2] * Cc, lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b, oz, oy, ox, c;
-    unflat5(t, f.ext[0], f.ext[1], f.ext[2], C, b, oz, oy, ox, c);
-    oz += f.begin[0];
-    oy += f.begin[1];
-    ox += f.begin[2];
-    auto hv = [&](int pz, int py, int px) -> T {
-      return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
-    };
-    if (oz < g.E[0] && oy < g.E[1] && ox < g.E[2])
-      lowres[(((b * g.E[0] + oz) * g.E[1] + oy) * g.E[2] + ox) * C + c] = hv(0, 0, 0);
-    auto get = [&](int64_t z, int64_t y, int64_t x, int ch) -> T {
-      return cells[((((b * g.Lc[0] + z) * g.Lc[1] + y) * g.Lc[2] + x) * K + (PERCH ? ch : 0)) * C + c];
-    };
-    for (int k = 0; k < nmaps; ++k) {
-      int par[3];
-      map_parity(nsp, k, par);
-      const int64_t e0 = par[0] ? g.Lc[0] : g.E[0], e1 = par[1] ? g.Lc[1] : g.E[1], e2 = par[2] ? g.Lc[2] : g.E[2];
+    I b, oz, oy, ox, c;
+    unflat_i<I>(t, F, f.ext, C, b, oz, oy, ox, c);
+    oz += (I)f.begin[0];
+    oy += (I)f.begin[1];
+    ox += (I)f.begin[2];
+    const I h0 = b * hb + (2 * oz) * hz + (2 * oy) * hy + (2 * ox) * Cc + c;
+    if (oz < (I)g.E[0] && oy < (I)g.E[1] && ox < (I)g.E[2]) lowres[b * lb + oz * lz + oy * ly + ox * Cc + c] = hi[h0];
+    GenCells<T, NSP, PERCH, I> gc;
+    gc.init(cells, b, oz, oy, ox, c, g, K, Cc);
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
+      const I e0 = (I)(p0 ? g.Lc[0] : g.E[0]), e1 = (I)(p1 ? g.Lc[1] : g.E[1]), e2 = (I)(p2 ? g.Lc[2] : g.E[2]);
       if (oz >= e0 || oy >= e1 || ox >= e2) continue;
-      const T pred = aggregate_map<T>(nsp, k, oz, oy, ox, g.Lc[0], g.Lc[1], g.Lc[2], get);
-      const T gt = hv(par[0], par[1], par[2]);
-      ((TO*)maps.p[k])[(((b * e0 + oz) * e1 + oy) * e2 + ox) * C + c] = code_encode<CODER>(to_i32(pred), to_i32(gt));
+      const T pred = gc.pred(k);
+      const T gt = hi[h0 + p0 * hz + p1 * hy + p2 * Cc];
+      ((TO*)maps.p[k])[((b * e0 + oz) * e1 + oy) * e2 * Cc + ox * Cc + c] = code_encode<CODER>(to_i32(pred), to_i32(gt));
     }
   }
 }
 
-template <typename T, int CODER, bool PERCH>
+template <typename T, int CODER, bool PERCH, int NSP, typename I>
 __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __restrict__ lowres, CMapPtrs maps, Geo g,
-                                                                 int nsp, int64_t B, int64_t C,
-                                                                 const T* __restrict__ cells, int K,
-                                                                 T* __restrict__ hi, Frame f, int64_t total) {
+                                                                 int64_t B, int64_t C, const T* __restrict__ cells,
+                                                                 int K, T* __restrict__ hi, Frame f, Flat F,
+                                                                 int64_t total) {
   using TO = typename coder_out<CODER>::type;
-  const int nmaps = nsp == 3 ? 7 : 3;
+  constexpr int NM = NSP == 3 ? 7 : 3;
+  const I Cc = (I)C;
+  const I hy = (I)g.n[2] * Cc, hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
+  const I ly = (I)g.E[2] * Cc, lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b, oz, oy, ox, c;
-    unflat5(t, f.ext[0], f.ext[1], f.ext[2], C, b, oz, oy, ox, c);
-    oz += f.begin[0];
-    oy += f.begin[1];
-    ox += f.begin[2];
-    auto hout = [&](int pz, int py, int px) -> T& {
-      return hi[(((b * g.n[0] + 2 * oz + pz) * g.n[1] + 2 * oy + py) * g.n[2] + 2 * ox + px) * C + c];
-    };
-    if (oz < g.E[0] && oy < g.E[1] && ox < g.E[2])
-      hout(0, 0, 0) = lowres[(((b * g.E[0] + oz) * g.E[1] + oy) * g.E[2] + ox) * C + c];
-    auto get = [&](int64_t z, int64_t y, int64_t x, int ch) -> T {
-      return cells[((((b * g.Lc[0] + z) * g.Lc[1] + y) * g.Lc[2] + x) * K + (PERCH ? ch : 0)) * C + c];
-    };
-    for (int k = 0; k < nmaps; ++k) {
-      int par[3];
-      map_parity(nsp, k, par);
-      const int64_t e0 = par[0] ? g.Lc[0] : g.E[0], e1 = par[1] ? g.Lc[1] : g.E[1], e2 = par[2] ? g.Lc[2] : g.E[2];
+    I b, oz, oy, ox, c;
+    unflat_i<I>(t, F, f.ext, C, b, oz, oy, ox, c);
+    oz += (I)f.begin[0];
+    oy += (I)f.begin[1];
+    ox += (I)f.begin[2];
+    const I h0 = b * hb + (2 * oz) * hz + (2 * oy) * hy + (2 * ox) * Cc + c;
+    if (oz < (I)g.E[0] && oy < (I)g.E[1] && ox < (I)g.E[2]) hi[h0] = lowres[b * lb + oz * lz + oy * ly + ox * Cc + c];
+    GenCells<T, NSP, PERCH, I> gc;
+    gc.init(cells, b, oz, oy, ox, c, g, K, Cc);
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
+      const I e0 = (I)(p0 ? g.Lc[0] : g.E[0]), e1 = (I)(p1 ? g.Lc[1] : g.E[1]), e2 = (I)(p2 ? g.Lc[2] : g.E[2]);
       if (oz >= e0 || oy >= e1 || ox >= e2) continue;
-      const T pred = aggregate_map<T>(nsp, k, oz, oy, ox, g.Lc[0], g.Lc[1], g.Lc[2], get);
-      const TO enc = ((const TO*)maps.p[k])[(((b * e0 + oz) * e1 + oy) * e2 + ox) * C + c];
-      hout(par[0], par[1], par[2]) = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
+      const T pred = gc.pred(k);
+      const TO enc = ((const TO*)maps.p[k])[((b * e0 + oz) * e1 + oy) * e2 * Cc + ox * Cc + c];
+      hi[h0 + p0 * hz + p1 * hy + p2 * Cc] = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
     }
   }
 }
@@ -182,6 +316,15 @@ static Frame cell_frame(const Geo& g, const Frame& f) {
   return cf;
 }
 
+// 32-bit element indexing when every array the generic kernels address (highres, cells, lowres,
+// maps: all at most the padded highres size x K) and the index space stay below 2^31
+static bool fits32(const Geo& g, int64_t B, int64_t C, int K) {
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t hi = B * (g.n[0] + 1) * (g.n[1] + 1) * (g.n[2] + 1) * C;
+  const int64_t cells = B * g.L[0] * g.L[1] * g.L[2] * K * C;
+  return B > 0 && hi < lim && cells < lim;
+}
+
 template <typename T>
 static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int64_t B, int64_t C,
                          const kmp_predictor* pred, const Frame& f, T* cells, hipStream_t stream) {
@@ -189,11 +332,50 @@ static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int6
   const int64_t ncell = B * cf.ext[0] * cf.ext[1] * cf.ext[2] * C;
   if (ncell == 0) return KMP_OK;
   if (pred->kind == KMP_PRED_MEAN) {
-    cell_mean_kernel<T><<<ggrid(ncell), kGThreads, 0, stream>>>(src, s, g, nsp, B, C, pred->padding, cf, cells, ncell);
+    const Flat F = make_flat(cf.ext, C);
+    const bool i32 = fits32(g, B, C, 1);
+    auto go = [&](auto nsp_c, auto i_tag) {
+      constexpr int NSP = decltype(nsp_c)::value;
+      using I = decltype(i_tag);
+      const int p = pred->padding;
+#define KMP_CM(KK) cell_mean_kernel<T, NSP, KK, I><<<ggrid(ncell), kGThreads, 0, stream>>>(src, s, g, B, C, p, cf, F, cells, ncell)
+      if (p == 0) KMP_CM(2);
+      else if (p == 1) KMP_CM(4);
+      else if (p == 2) KMP_CM(6);
+      else KMP_CM(0);
+#undef KMP_CM
+    };
+    if (nsp == 3) {
+      if (i32) go(std::integral_constant<int, 3>{}, int32_t{});
+      else go(std::integral_constant<int, 3>{}, int64_t{});
+    } else {
+      if (i32) go(std::integral_constant<int, 2>{}, int32_t{});
+      else go(std::integral_constant<int, 2>{}, int64_t{});
+    }
     return check_launch("cell_mean");
   }
   const int64_t cbeg[3] = {cf.begin[0], cf.begin[1], cf.begin[2]}, cext[3] = {cf.ext[0], cf.ext[1], cf.ext[2]};
   return linear_cells<T>(src, s.S, s.mult, g, nsp, B, C, pred, cbeg, cext, cells, stream);
+}
+
+// the encode / decode kernel of (NSP, PERCH, I) for this call
+template <bool DEC, typename T, int CODER, typename Launch>
+static void gen_dispatch(int nsp, bool perch, bool i32, Launch&& launch) {
+  auto with_i = [&](auto nsp_c, auto perch_c) {
+    if (i32) launch(nsp_c, perch_c, int32_t{});
+    else launch(nsp_c, perch_c, int64_t{});
+  };
+  using N3 = std::integral_constant<int, 3>;
+  using N2 = std::integral_constant<int, 2>;
+  using PT = std::true_type;
+  using PF = std::false_type;
+  if (nsp == 3) {
+    if (perch) with_i(N3{}, PT{});
+    else with_i(N3{}, PF{});
+  } else {
+    if (perch) with_i(N2{}, PT{});
+    else with_i(N2{}, PF{});
+  }
 }
 
 template <typename T, int CODER>
@@ -209,12 +391,13 @@ static int encode_generic_t(const T* hi, const Geo& g, int nsp, int64_t B, int64
   if (int st = run_predictor<T>(hi, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   const int64_t total = B * f.ext[0] * f.ext[1] * f.ext[2] * C;
   if (total == 0) return KMP_OK;
-  if (pred->kind == KMP_PRED_MEAN)
-    encode_generic_kernel<T, CODER, false><<<ggrid(total), kGThreads, 0, stream>>>(hi, g, nsp, B, C, cells, 1, lowres,
-                                                                                  maps, f, total);
-  else
-    encode_generic_kernel<T, CODER, true><<<ggrid(total), kGThreads, 0, stream>>>(
-        hi, g, nsp, B, C, cells, nsp == 3 ? 19 : 5, lowres, maps, f, total);
+  const bool perch = pred->kind != KMP_PRED_MEAN;
+  const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
+  const Flat F = make_flat(f.ext, C);
+  gen_dispatch<false, T, CODER>(nsp, perch, fits32(g, B, C, K), [&](auto nsp_c, auto perch_c, auto i_tag) {
+    encode_generic_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, decltype(i_tag)>
+        <<<ggrid(total), kGThreads, 0, stream>>>(hi, g, B, C, cells, K, lowres, maps, f, F, total);
+  });
   return check_launch("encode_generic");
 }
 
@@ -231,12 +414,13 @@ static int decode_generic_t(const T* lowres, const CMapPtrs& maps, const Geo& g,
   if (int st = run_predictor<T>(lowres, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   const int64_t total = B * f.ext[0] * f.ext[1] * f.ext[2] * C;
   if (total == 0) return KMP_OK;
-  if (pred->kind == KMP_PRED_MEAN)
-    decode_generic_kernel<T, CODER, false><<<ggrid(total), kGThreads, 0, stream>>>(lowres, maps, g, nsp, B, C, cells, 1,
-                                                                                  hi, f, total);
-  else
-    decode_generic_kernel<T, CODER, true><<<ggrid(total), kGThreads, 0, stream>>>(
-        lowres, maps, g, nsp, B, C, cells, nsp == 3 ? 19 : 5, hi, f, total);
+  const bool perch = pred->kind != KMP_PRED_MEAN;
+  const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
+  const Flat F = make_flat(f.ext, C);
+  gen_dispatch<true, T, CODER>(nsp, perch, fits32(g, B, C, K), [&](auto nsp_c, auto perch_c, auto i_tag) {
+    decode_generic_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, decltype(i_tag)>
+        <<<ggrid(total), kGThreads, 0, stream>>>(lowres, maps, g, B, C, cells, K, hi, f, F, total);
+  });
   return check_launch("decode_generic");
 }
 
