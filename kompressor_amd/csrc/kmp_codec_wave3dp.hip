@@ -636,10 +636,13 @@ wave3dr_kernel(W3P a) {
 // ------------------------------------------------------------------------------------------
 // Output planes per workgroup and register budget, per (p, direction): the measured optimum at C3
 // (profiles/round1/w3p_sweep.log; 64^3 u16 tiles): p = 1 PL 2 (decode at 4 waves / SIMD),
-// p = 2 encode PL 1, decode PL 2 at 3 waves / SIMD.  KMP_W3P_PL overrides the planes.
-static void w3p_cfg(int P, bool dec, int& pl, int& wpe) {
-  pl = (P == 2 && !dec) ? 1 : 2;
-  wpe = dec ? (P == 1 ? 4 : 3) : 1;
+// p = 2 encode PL 1, decode PL 2 at 3 waves / SIMD.  8-bit samples (8 cells a lane) spill under
+// those decode budgets (100-508 bytes of scratch, decode 2.2x the encode's time): the compiler's
+// own budget there, and PL 1 at p = 2 (C3-geometry u8 decode p = 1 159 -> 73 us, p = 2 227 -> 106 us,
+// profiles/round6/w3p_u8_r6o.log).  KMP_W3P_PL overrides the planes.
+static void w3p_cfg(int P, bool dec, int bytes, int& pl, int& wpe) {
+  pl = (P == 2 && (!dec || bytes == 1)) ? 1 : 2;
+  wpe = dec && bytes == 2 ? (P == 1 ? 4 : 3) : 1;
   pl = opt(OPT_W3P_PL, pl) == 1 ? 1 : 2;
 }
 
@@ -740,7 +743,7 @@ int try_wave3dp_encode(const T* hi, const Geo& g, int64_t B, int64_t C, const km
     w3p::W3P a{};
     dim3 grid, block;
     int pl, wpe;
-    w3p_cfg(pred->padding, false, pl, wpe);
+    w3p_cfg(pred->padding, false, (int)sizeof(T), pl, wpe);
     const int zr = w3p_roll(pred->padding, (int)sizeof(T));
     if (!wave3dp_geometry<T>(g, B, C, pred, region, zr ? zr : pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
@@ -767,7 +770,7 @@ int try_wave3dp_decode(const T* lowres, const CMapPtrs& maps, const Geo& g, int6
     w3p::W3P a{};
     dim3 grid, block;
     int pl, wpe;
-    w3p_cfg(pred->padding, true, pl, wpe);
+    w3p_cfg(pred->padding, true, (int)sizeof(T), pl, wpe);
     const int zr = w3p_roll(pred->padding, (int)sizeof(T));
     if (!wave3dp_geometry<T>(g, B, C, pred, region, zr ? zr : pl, a, grid, block)) return KMP_ERR_UNSUPPORTED;
     if (((uintptr_t)hi & 15) || ((uintptr_t)lowres & 7)) return KMP_ERR_UNSUPPORTED;
