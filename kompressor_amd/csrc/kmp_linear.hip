@@ -52,10 +52,78 @@ __device__ __forceinline__ float lin_feature(const T* __restrict__ src, const Li
   return (float)src[(((b * s.S[0] + z) * s.S[1] + y) * s.S[2] + x) * C + c];
 }
 
+// A lane's cell neighbourhood as element offsets into the source, per axis (KK = 2p + 2 nodes
+// each): feature n = (dz, dy, dx) in the reference's order is src[base + oz[dz] + oy[dy] + ox[dx]]
+// -- the index arithmetic of lin_feature done once per cell instead of once per feature.
+template <int NSP, int KK, typename I>
+struct Nbhd {
+  I base, oz[NSP == 3 ? KK : 1], oy[KK], ox[KK];
+  __device__ __forceinline__ void init(const LinSrc& s, int p, int64_t C, I b, I c, I cz, I cy, I cx) {
+    const I Cc = (I)C, sy = (I)s.S[2] * Cc, sz = (I)s.S[1] * sy;
+    base = b * ((I)s.S[0] * sz) + c;
+    auto src = [&](int64_t j, int a) -> I {  // source index of padded node j along axis a
+      return (I)(s.mult == 0 ? j : s.mult * sym_index(sym_index(j, s.L[a]), s.E[a]));
+    };
+#pragma unroll
+    for (int d = 0; d < KK; ++d) {
+      ox[d] = src(cx - (s.mult ? p : 0) + d, 2) * Cc;
+      oy[d] = src(cy - (s.mult ? p : 0) + d, 1) * sy;
+      if constexpr (NSP == 3) oz[d] = src(cz - (s.mult ? p : 0) + d, 0) * sz;
+    }
+    if constexpr (NSP != 3) oz[0] = 0;
+  }
+  // feature n's offset (n compile-time after unrolling)
+  __device__ __forceinline__ I at(int n) const {
+    const int dz = NSP == 3 ? n / (KK * KK) : 0, dy = (n / KK) % KK, dx = n % KK;
+    return base + oz[dz] + oy[dy] + ox[dx];
+  }
+};
+
+// The row decomposition (b, cell in box, c) of the flattened rows, by multiply-high division
+struct LinFlat {
+  uint32_t dC_m, dC_s, d2_m, d2_s, d1_m, d1_s, d0_m, d0_s;
+  uint32_t C, e2, e1, e0;
+};
+static inline void lf_div(int64_t d64, uint32_t& m, uint32_t& sh) {
+  const uint32_t d = (uint32_t)(d64 < 1 ? 1 : d64);
+  uint32_t s = 0;
+  while (s < 32 && (1ull << s) < d) ++s;
+  m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  sh = s;
+}
+static inline LinFlat make_linflat(const LinSrc& s, int64_t C) {
+  LinFlat f{};
+  lf_div(C, f.dC_m, f.dC_s);
+  lf_div(s.cext[2], f.d2_m, f.d2_s);
+  lf_div(s.cext[1], f.d1_m, f.d1_s);
+  lf_div(s.cext[0], f.d0_m, f.d0_s);
+  f.C = (uint32_t)C; f.e2 = (uint32_t)s.cext[2]; f.e1 = (uint32_t)s.cext[1]; f.e0 = (uint32_t)s.cext[0];
+  return f;
+}
+template <typename I>
+__device__ __forceinline__ void lin_unflat(int64_t row, const LinFlat& f, const LinSrc& s, int64_t C, I& b, I& z, I& y,
+                                           I& x, I& c) {
+  if constexpr (sizeof(I) == 4) {
+    uint32_t u = (uint32_t)row, q;
+    q = (__umulhi(u, f.dC_m) + u) >> f.dC_s; c = (I)(u - q * f.C); u = q;
+    q = (__umulhi(u, f.d2_m) + u) >> f.d2_s; x = (I)(u - q * f.e2); u = q;
+    q = (__umulhi(u, f.d1_m) + u) >> f.d1_s; y = (I)(u - q * f.e1); u = q;
+    q = (__umulhi(u, f.d0_m) + u) >> f.d0_s; z = (I)(u - q * f.e0); b = (I)q;
+  } else {
+    int64_t bb, zz, yy, xx, cc;
+    unflat5(row, s.cext[0], s.cext[1], s.cext[2], C, bb, zz, yy, xx, cc);
+    b = bb; z = zz; y = yy; x = xx; c = cc;
+  }
+  z += (I)s.cbeg[0];
+  y += (I)s.cbeg[1];
+  x += (I)s.cbeg[2];
+}
+
 // One wave per 32-row tile; rows = (b, cell in box, c) flattened.  Writes preds[row-major
-// [B, Lc..., K, C]] in T and optionally the f32 values.
-template <typename T>
-__global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ src, LinSrc s, int nsp, int p,
+// [B, Lc..., K, C]] in T and optionally the f32 values.  KK = 2p + 2 at compile time (p <= 2:
+// the neighbourhood offsets per lane once, the N/2 steps unrolled) or 0 (any p: lin_feature).
+template <typename T, int NSP, int KK, typename I>
+__global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
                                                           int64_t B, int64_t C, const float* __restrict__ W,
                                                           const float* __restrict__ bias, int N, int K,
                                                           T* __restrict__ out, float* __restrict__ out_f32,
@@ -65,37 +133,56 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int j = lane & 31;  // output column this lane feeds (B operand) and holds (D)
   const int h = lane >> 5;  // k within the 2-wide step
+  const float bj = j < K ? bias[j] : 0.0f;
+  // the lane's weights of every step, loaded once for all its tiles when they fit in registers
+  constexpr int NN0 = KK > 0 ? (NSP == 3 ? KK * KK * KK : KK * KK) : 2;
+  constexpr bool WREG = KK > 0 && NN0 / 2 <= 32;
+  float wreg[WREG ? NN0 / 2 : 1];
+  if constexpr (WREG) {
+#pragma unroll
+    for (int st = 0; st < NN0 / 2; ++st) wreg[st] = j < K ? W[(2 * st + h) * K + j] : 0.0f;
+  }
   for (int64_t tile = wave; tile * 32 < rows; tile += nwaves) {
-    // decode this lane's A row (cell)
+    // this lane's A row (cell)
     const int64_t row = tile * 32 + (lane & 31);
     const bool row_ok = row < rows;
-    int64_t b, z, y, x, c;
-    unflat5(row_ok ? row : 0, s.cext[0], s.cext[1], s.cext[2], C, b, z, y, x, c);
-    z += s.cbeg[0];
-    y += s.cbeg[1];
-    x += s.cbeg[2];
+    I b, z, y, x, c;
+    lin_unflat<I>(row_ok ? row : 0, lf, s, C, b, z, y, x, c);
     f32x16 acc;
-    const float bj = j < K ? bias[j] : 0.0f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = bj;  // every row of column j starts at b[j]
-    for (int st = 0; st < N / 2; ++st) {
-      const int n = 2 * st + h;
-      const float a = row_ok ? lin_feature(src, s, nsp, p, b, c, C, z, y, x, n) : 0.0f;
-      const float w = j < K ? W[n * K + j] : 0.0f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+    if constexpr (KK > 0) {
+      Nbhd<NSP, KK, I> nb;
+      nb.init(s, p, C, b, c, z, y, x);
+      constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
+#pragma unroll
+      for (int st = 0; st < NN / 2; ++st) {
+        // features 2st and 2st + 1 share dz, dy (KK even): the lane's is 2st + h
+        const I o0 = nb.at(2 * st), o1 = nb.at(2 * st + 1);
+        const float a = row_ok ? (float)src[h ? o1 : o0] : 0.0f;
+        const float w = WREG ? wreg[WREG ? st : 0] : (j < K ? W[(2 * st + h) * K + j] : 0.0f);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+      }
+    } else {
+      const int64_t bz = b, zz = z, yy = y, xx = x, cc = c;
+      for (int st = 0; st < N / 2; ++st) {
+        const int n = 2 * st + h;
+        const float a = row_ok ? lin_feature(src, s, NSP, p, bz, cc, C, zz, yy, xx, n) : 0.0f;
+        const float w = j < K ? W[n * K + j] : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+      }
     }
-    if (j >= K) continue;
+    // the output offset of each row, held by the row's own lane: cell * K * C + c
+    const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
+    const int64_t obase = cell * K * C + c;
+    const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
+    // (the shuffles run with every lane active: a lane reading an inactive lane gets no value)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int64_t orow = tile * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      if (orow >= rows) continue;
-      int64_t ob, oz, oy, ox, oc;
-      unflat5(orow, s.cext[0], s.cext[1], s.cext[2], C, ob, oz, oy, ox, oc);
-      oz += s.cbeg[0];
-      oy += s.cbeg[1];
-      ox += s.cbeg[2];
-      const int64_t cell = ((ob * s.Lc[0] + oz) * s.Lc[1] + oy) * s.Lc[2] + ox;
-      const int64_t o = (cell * K + j) * C + oc;
+      const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
+      const int64_t ob = (int64_t)(uint32_t)__shfl(olo, r, 64) | ((int64_t)__shfl(ohi, r, 64) << 32);
+      if (j >= K || tile * 32 + r >= rows) continue;
+      const int64_t o = ob + (int64_t)j * C;
       out[o] = cast_f32<T>(acc[q]);
       if (out_f32) out_f32[o] = acc[q];
     }
@@ -104,9 +191,11 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
 
 // KMP_PRED_LINEAR_MFMA (kmp_bf16x2.h): one wave per 16-row tile (rows = (b, cell, c) as above),
 // the K outputs in column tiles of 16, per accumulation step (8 features, kmp_bf16x2.h
-// step_feature) one v_mfma_f32_16x16x32_bf16 per column tile.  u8 / u16 samples only (the byte split is exact for them).
-template <typename T>
-__global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict__ src, LinSrc s, int nsp, int p,
+// step_feature) one v_mfma_f32_16x16x32_bf16 per column tile.  u8 / u16 samples only (the byte
+// split is exact for them).  KK as linear_mfma_kernel's: the neighbourhood offsets once per cell,
+// the steps unrolled, each lane's 4 features of a step one select between the two lane groups'.
+template <typename T, int NSP, int KK, typename I>
+__global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
                                                             int64_t B, int64_t C, const float* __restrict__ W,
                                                             const float* __restrict__ bias, int N, int K,
                                                             T* __restrict__ out, float* __restrict__ out_f32,
@@ -116,41 +205,79 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int m = lane & 15, g = lane >> 4;
   const int nq = (N + 7) / 8, nct = (K + 15) / 16;
+  // the lane's B fragments of every (column tile, step), built once for all its tiles when they
+  // fit in 64 registers (the bf16 splits of 4 weights per fragment were redone per tile)
+  constexpr int NQ0 = KK > 0 ? ((NSP == 3 ? KK * KK * KK : KK * KK) + 7) / 8 : 1;
+  constexpr int NCT0 = NSP == 3 ? 2 : 1;
+  constexpr bool BREG = KK > 0 && NCT0 * NQ0 <= 16;
+  bx::u32x4 breg[BREG ? NCT0 : 1][BREG ? NQ0 : 1];
+  if constexpr (BREG) {
+#pragma unroll
+    for (int ct = 0; ct < NCT0; ++ct)
+#pragma unroll
+      for (int t = 0; t < NQ0; ++t) {
+        const int k = 16 * ct + m;
+        breg[ct][t] = bx::b_fragment(W + (k < K ? k : 0), K, N, NSP, p, t, g, k < K);
+      }
+  }
   for (int64_t tile = wave; tile * 16 < rows; tile += nwaves) {
     const int64_t row = tile * 16 + m;  // this lane's A row (cell)
     const bool row_ok = row < rows;
-    int64_t b, z, y, x, c;
-    unflat5(row_ok ? row : 0, s.cext[0], s.cext[1], s.cext[2], C, b, z, y, x, c);
-    z += s.cbeg[0];
-    y += s.cbeg[1];
-    x += s.cbeg[2];
+    I b, z, y, x, c;
+    lin_unflat<I>(row_ok ? row : 0, lf, s, C, b, z, y, x, c);
+    constexpr int NQ = KK > 0 ? ((NSP == 3 ? KK * KK * KK : KK * KK) + 7) / 8 : 1;
+    Nbhd<NSP, (KK > 0 ? KK : 2), I> nb;
+    if constexpr (KK > 0) nb.init(s, p, C, b, c, z, y, x);
+    const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
+    const int64_t obase = cell * K * C + c;
+    const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
     for (int ct = 0; ct < nct; ++ct) {
       const int k = 16 * ct + m;  // this lane's B / D column
       const bool col_ok = k < K;
       const float bk = col_ok ? bias[k] : 0.0f;
       bx::f32x4 acc = {bk, bk, bk, bk};
-      for (int t = 0; t < nq; ++t) {  // accumulation steps (kmp_bf16x2.h step_feature)
-        bx::u32x4 a;
+      if constexpr (KK > 0) {
+        constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = bx::step_feature(nsp, p, nq, t, g & 1, i);
-          const uint32_t v = (row_ok && n < N) ? (uint32_t)lin_feature(src, s, nsp, p, b, c, C, z, y, x, n) : 0u;
-          a[i] = bx::feature_dword(v);
+        for (int t = 0; t < NQ; ++t) {
+          bx::u32x4 a;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {  // the lane group's feature of the step: one select
+            const int n0 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 0, i);
+            const int n1 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 1, i);
+            const int n = (g & 1) ? n1 : n0;
+            const I o = (g & 1) ? nb.at(n1 < NN ? n1 : 0) : nb.at(n0 < NN ? n0 : 0);
+            a[i] = bx::feature_dword((row_ok && n < NN) ? (uint32_t)src[o] : 0u);
+          }
+          if constexpr (BREG) {
+            bx::u32x4 bf = breg[0][t];
+#pragma unroll
+            for (int c2 = 1; c2 < NCT0; ++c2) bf = ct == c2 ? breg[c2][t] : bf;
+            acc = bx::mfma(a, bf, acc);
+          } else {
+            acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, NSP, p, t, g, col_ok), acc);
+          }
         }
-        acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, nsp, p, t, g, col_ok), acc);
+      } else {
+        const int64_t bz = b, zz = z, yy = y, xx = x, cc = c;
+        for (int t = 0; t < nq; ++t) {  // accumulation steps (kmp_bf16x2.h step_feature)
+          bx::u32x4 a;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int n = bx::step_feature(NSP, p, nq, t, g & 1, i);
+            const uint32_t v = (row_ok && n < N) ? (uint32_t)lin_feature(src, s, NSP, p, bz, cc, C, zz, yy, xx, n) : 0u;
+            a[i] = bx::feature_dword(v);
+          }
+          acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, NSP, p, t, g, col_ok), acc);
+        }
       }
-      if (!col_ok) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t orow = tile * 16 + 4 * g + r;
-        if (orow >= rows) continue;
-        int64_t ob, oz, oy, ox, oc;
-        unflat5(orow, s.cext[0], s.cext[1], s.cext[2], C, ob, oz, oy, ox, oc);
-        oz += s.cbeg[0];
-        oy += s.cbeg[1];
-        ox += s.cbeg[2];
-        const int64_t cell = ((ob * s.Lc[0] + oz) * s.Lc[1] + oy) * s.Lc[2] + ox;
-        const int64_t o = (cell * K + k) * C + oc;
+        const int rr = 4 * g + r;
+        // (every lane active for the shuffle: see linear_mfma_kernel)
+        const int64_t ob = (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
+        if (!col_ok || tile * 16 + rr >= rows) continue;
+        const int64_t o = ob + (int64_t)k * C;
         out[o] = cast_f32<T>(acc[r]);
         if (out_f32) out_f32[o] = acc[r];
       }
@@ -170,8 +297,24 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
       int64_t blocks = ceil_div(ceil_div(rows, 16), 4);
       if (blocks > 65536) blocks = 65536;
-      linear_bf16x2_kernel<T><<<(unsigned)blocks, 256, 0, stream>>>(src, s, nsp, p, B, C, W, bias, N, K, out, out_f32,
-                                                                    rows);
+      const LinFlat lf = make_linflat(s, C);
+      const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
+      auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
+        linear_bf16x2_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
+            <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows);
+      };
+      auto with_kk = [&](auto nsp_c, auto i_tag) {
+        if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
+        else if (p == 1) go(nsp_c, std::integral_constant<int, 4>{}, i_tag);
+        else if (p == 2) go(nsp_c, std::integral_constant<int, 6>{}, i_tag);
+        else go(nsp_c, std::integral_constant<int, 0>{}, int64_t{});
+      };
+      auto with_i = [&](auto nsp_c) {
+        if (i32) with_kk(nsp_c, int32_t{});
+        else with_kk(nsp_c, int64_t{});
+      };
+      if (nsp == 3) with_i(std::integral_constant<int, 3>{});
+      else with_i(std::integral_constant<int, 2>{});
       return check_launch("linear_bf16x2");
     }
     return fail(KMP_ERR_UNSUPPORTED, "the matrix-core LinearPredictor (bf16x2) takes uint8 / uint16 samples");
@@ -179,7 +322,25 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
   int64_t waves = ceil_div(rows, 32);
   int64_t blocks = ceil_div(waves, 4);
   if (blocks > 65536) blocks = 65536;
-  linear_mfma_kernel<T><<<(unsigned)blocks, 256, 0, stream>>>(src, s, nsp, p, B, C, W, bias, N, K, out, out_f32, rows);
+  const LinFlat lf = make_linflat(s, C);
+  // 32-bit rows and source offsets when both stay below 2^31
+  const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
+  auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
+    linear_mfma_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
+        <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows);
+  };
+  auto with_kk = [&](auto nsp_c, auto i_tag) {
+    if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
+    else if (p == 1) go(nsp_c, std::integral_constant<int, 4>{}, i_tag);
+    else if (p == 2) go(nsp_c, std::integral_constant<int, 6>{}, i_tag);
+    else go(nsp_c, std::integral_constant<int, 0>{}, int64_t{});
+  };
+  auto with_i = [&](auto nsp_c) {
+    if (i32) with_kk(nsp_c, int32_t{});
+    else with_kk(nsp_c, int64_t{});
+  };
+  if (nsp == 3) with_i(std::integral_constant<int, 3>{});
+  else with_i(std::integral_constant<int, 2>{});
   return check_launch("linear_mfma");
 }
 
