@@ -2,7 +2,7 @@
 // integer dtype: two launches per direction.
 //
 //   1. predictor apply: one value per cell (MEAN) or K per cell (LINEAR) into a workspace
-//      [B, Lc..., K, C] -- the reference's features_from_lowres + mean/astype
+//      [K, B, Lc..., C] (channel planes) -- the reference's features_from_lowres + mean/astype
 //      (tests/volume/test_encode_decode.py:46-51) without materialising the features;
 //   2. residual pass: per output block position o, read the 2^d highres block at 2o, aggregate
 //      the cell predictions exactly as maps_from_predictions does (kmp_aggregate.h), apply the
@@ -151,22 +151,22 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restric
 
 // Per output position o (and channel): the lowres node and the 7 (3) maps.  The cell values the
 // maps aggregate are read once: the 2^d cells o - {0,1}^d (MeanPredictor: one value per cell), or
-// each contribution's channel (LinearPredictor: K per cell); missing cells (past the cell box)
-// are skipped exactly as maps_from_predictions does, in the reference's channel order.
+// each contribution's channel (LinearPredictor: K per cell, planar: channel ch of every cell in
+// plane ch, kmp_linear.hip launch_linear); missing cells (past the cell box) are skipped exactly as
+// maps_from_predictions does, in the reference's channel order.
 template <typename T, int NSP, bool PERCH, typename I>
 struct GenCells {
   const T* cells;
-  I base, sx, sy, sz;  // cells[base - dz sz - dy sy - dx sx + ch C]
-  I C;
+  I base, sx, sy, sz;  // cells[base - dz sz - dy sy - dx sx + ch kp]
+  I kp;                // LinearPredictor: the channel plane stride
   bool v[2][2][2];     // cell o - (dz, dy, dx) exists
   T m[2][2][2];        // MeanPredictor: the cell means
 
-  __device__ __forceinline__ void init(const T* c_, I b, I oz, I oy, I ox, I c, const Geo& g, int K, I Cc) {
+  __device__ __forceinline__ void init(const T* c_, I b, I oz, I oy, I ox, I c, const Geo& g, I Cc, I kp_) {
     cells = c_;
-    C = Cc;
-    const I kc = (I)(PERCH ? K : 1) * Cc;
-    sx = kc;
-    sy = (I)g.Lc[2] * kc;
+    kp = kp_;
+    sx = Cc;
+    sy = (I)g.Lc[2] * Cc;
     sz = (I)g.Lc[1] * sy;
     base = b * ((I)g.Lc[0] * sz) + oz * sz + oy * sy + ox * sx + c;
     const bool vz[2] = {oz < (I)g.Lc[0], oz >= 1}, vy[2] = {oy < (I)g.Lc[1], oy >= 1},
@@ -182,7 +182,7 @@ struct GenCells {
         }
   }
   __device__ __forceinline__ T get(int dz, int dy, int dx, int ch) const {
-    if constexpr (PERCH) return cells[base - dz * sz - dy * sy - dx * sx + (I)ch * C];
+    if constexpr (PERCH) return cells[base - dz * sz - dy * sy - dx * sx + (I)ch * kp];
     else return m[dz][dy][dx];
   }
   // map k's prediction (maps_from_predictions for one element)
@@ -216,6 +216,7 @@ __global__ void __launch_bounds__(kGThreads) encode_generic_kernel(const T* __re
   const I Cc = (I)C;
   const I hy = (I)g.n[2] * Cc, hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
   const I ly = (I)g.E[2] * Cc, lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
+  const I kp = (I)(B * g.Lc[0] * g.Lc[1] * g.Lc[2] * C);  // LinearPredictor: channel plane stride
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     I b, oz, oy, ox, c;
     unflat_i<I>(t, F, f.ext, C, b, oz, oy, ox, c);
@@ -225,7 +226,7 @@ __global__ void __launch_bounds__(kGThreads) encode_generic_kernel(const T* __re
     const I h0 = b * hb + (2 * oz) * hz + (2 * oy) * hy + (2 * ox) * Cc + c;
     if (oz < (I)g.E[0] && oy < (I)g.E[1] && ox < (I)g.E[2]) lowres[b * lb + oz * lz + oy * ly + ox * Cc + c] = hi[h0];
     GenCells<T, NSP, PERCH, I> gc;
-    gc.init(cells, b, oz, oy, ox, c, g, K, Cc);
+    gc.init(cells, b, oz, oy, ox, c, g, Cc, kp);
 #pragma unroll
     for (int k = 0; k < NM; ++k) {
       const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
@@ -248,6 +249,7 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
   const I Cc = (I)C;
   const I hy = (I)g.n[2] * Cc, hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
   const I ly = (I)g.E[2] * Cc, lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
+  const I kp = (I)(B * g.Lc[0] * g.Lc[1] * g.Lc[2] * C);  // LinearPredictor: channel plane stride
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     I b, oz, oy, ox, c;
     unflat_i<I>(t, F, f.ext, C, b, oz, oy, ox, c);
@@ -257,7 +259,7 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
     const I h0 = b * hb + (2 * oz) * hz + (2 * oy) * hy + (2 * ox) * Cc + c;
     if (oz < (I)g.E[0] && oy < (I)g.E[1] && ox < (I)g.E[2]) hi[h0] = lowres[b * lb + oz * lz + oy * ly + ox * Cc + c];
     GenCells<T, NSP, PERCH, I> gc;
-    gc.init(cells, b, oz, oy, ox, c, g, K, Cc);
+    gc.init(cells, b, oz, oy, ox, c, g, Cc, kp);
 #pragma unroll
     for (int k = 0; k < NM; ++k) {
       const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
@@ -266,6 +268,259 @@ __global__ void __launch_bounds__(kGThreads) decode_generic_kernel(const T* __re
       const T pred = gc.pred(k);
       const TO enc = ((const TO*)maps.p[k])[((b * e0 + oz) * e1 + oy) * e2 * Cc + ox * Cc + c];
       hi[h0 + p0 * hz + p1 * hy + p2 * Cc] = (T)code_decode<CODER>(to_i32(pred), to_i32(enc));
+    }
+  }
+}
+
+// ---- the generic codec with one channel: a thread owns 4 consecutive output columns of a row ----
+// The per-element kernels above move 2-byte values (u16) one per thread; with C == 1 (the common
+// case outside the one-pass kernels: odd or wide rows, p >= 3) a thread here reads the 8 highres
+// samples of each of its 2^d rows as one unaligned vector access (element-wise only in a row's
+// last partial group), the cells around its outputs once, and writes each map's 4 values together.
+typedef uint32_t g32x2a1 __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t g32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t g32a1 __attribute__((aligned(1)));
+typedef uint8_t g8x4 __attribute__((ext_vector_type(4)));
+typedef uint8_t g8x4a1 __attribute__((ext_vector_type(4), aligned(1)));
+
+template <typename T>
+__device__ __forceinline__ void g_load8(const T* p, uint32_t (&v)[8]) {  // 8 consecutive samples
+  if constexpr (sizeof(T) == 1) {
+    const g32x2a1 w = *(const g32x2a1*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
+  } else if constexpr (sizeof(T) == 2) {
+    const g32x4a1 w = *(const g32x4a1*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+  } else {
+    const g32x4a1 a = *(const g32x4a1*)p, b = *(const g32x4a1*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void g_store8(T* p, const uint32_t (&v)[8]) {
+  if constexpr (sizeof(T) == 1) {
+    uint32_t w[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e >> 2] |= (v[e] & 0xffu) << (8 * (e & 3));
+    *(g32x2a1*)p = g32x2a1{w[0], w[1]};
+  } else if constexpr (sizeof(T) == 2) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e >> 1] |= (v[e] & 0xffffu) << (16 * (e & 1));
+    *(g32x4a1*)p = g32x4a1{w[0], w[1], w[2], w[3]};
+  } else {
+    *(g32x4a1*)p = g32x4a1{v[0], v[1], v[2], v[3]};
+    *(g32x4a1*)(p + 4) = g32x4a1{v[4], v[5], v[6], v[7]};
+  }
+}
+template <typename T>
+__device__ __forceinline__ void g_store4(T* p, const uint32_t (&v)[4]) {  // 4 consecutive values
+  if constexpr (sizeof(T) == 1) {
+    *(g8x4a1*)p = g8x4{(uint8_t)v[0], (uint8_t)v[1], (uint8_t)v[2], (uint8_t)v[3]};
+  } else if constexpr (sizeof(T) == 2) {
+    *(g32x2a1*)p = g32x2a1{(v[0] & 0xffffu) | (v[1] << 16), (v[2] & 0xffffu) | (v[3] << 16)};
+  } else {
+    *(g32x4a1*)p = g32x4a1{v[0], v[1], v[2], v[3]};
+  }
+}
+template <typename T>
+__device__ __forceinline__ void g_load4(const T* p, uint32_t (&v)[4]) {
+  if constexpr (sizeof(T) == 1) {
+    const uint32_t w = *(const g32a1*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (w >> (8 * e)) & 0xffu;
+  } else if constexpr (sizeof(T) == 2) {
+    const g32x2a1 w = *(const g32x2a1*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+  } else {
+    const g32x4a1 w = *(const g32x4a1*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = w[e];
+  }
+}
+
+// (b, oz, oy, xq) of a flat thread index over B x ext0 x ext1 x nxq (xq: a group of 4 columns)
+struct Row4 {
+  FDiv dq, d1, d0;
+};
+
+template <typename T, int CODER, bool PERCH, int NSP, typename I, bool DEC>
+__global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restrict__ src, CMapPtrs imaps, Geo g,
+                                                             const T* __restrict__ cells, int64_t B, T* __restrict__ dst,
+                                                             MapPtrs omaps, Frame f, Row4 R, int64_t nxq,
+                                                             int64_t total) {
+  using TO = typename coder_out<CODER>::type;
+  constexpr int NM = NSP == 3 ? 7 : 3;
+  constexpr int NZ = NSP == 3 ? 2 : 1;
+  const I hy = (I)g.n[2], hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
+  const I ly = (I)g.E[2], lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
+  const I cy = (I)g.Lc[2], cz = (I)g.Lc[1] * cy, cb = (I)g.Lc[0] * cz;
+  const I kp = (I)B * cb;  // LinearPredictor: channel plane stride (planar cells)
+  const I end2 = (I)(f.begin[2] + f.ext[2]);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    I b, oz, oy, xq;
+    {
+      uint32_t u = (uint32_t)t, q;
+      q = fdiv_q(u, R.dq); xq = (I)(u - q * R.dq.d); u = q;
+      q = fdiv_q(u, R.d1); oy = (I)(u - q * R.d1.d); u = q;
+      q = fdiv_q(u, R.d0); oz = (I)(u - q * R.d0.d); b = (I)q;
+    }
+    oz += (I)f.begin[0];
+    oy += (I)f.begin[1];
+    const I ox0 = (I)f.begin[2] + 4 * xq;
+    const int nout = (int)(end2 - ox0 < 4 ? end2 - ox0 : 4);
+    // ---- the cells around the 4 outputs: (oz - dz, oy - dy, ox0 - 1 + j), j = 0..4 ----
+    const I cbase = b * cb + oz * cz + oy * cy + ox0;  // cell (oz, oy, ox0)
+    bool cv[2][2][5];
+    T cm[2][2][5];
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const bool rowok = (NSP == 3 || dz == 0) && oz - dz >= 0 && oz - dz < (I)g.Lc[0] && oy - dy >= 0 &&
+                           oy - dy < (I)g.Lc[1];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const I x = ox0 - 1 + j;
+          cv[dz][dy][j] = rowok && x >= 0 && x < (I)g.Lc[2];
+          if (!PERCH) cm[dz][dy][j] = cv[dz][dy][j] ? cells[cbase - dz * cz - dy * cy + (j - 1)] : T(0);
+        }
+      }
+    auto cell = [&](int i, int dz, int dy, int dx, int ch) -> T {
+      if constexpr (PERCH) return cells[cbase - dz * cz - dy * cy + (i - dx) + (I)ch * kp];
+      else return cm[dz][dy][i + 1 - dx];
+    };
+    auto pred = [&](int k, int i) -> uint32_t {
+      Contrib c[4];
+      const int nc = map_contribs(NSP, k, c);
+      if (k == center_map(NSP)) return (uint32_t)to_i32(cell(i, 0, 0, 0, c[0].ch));
+      float sacc = 0.0f;
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q >= nc) break;
+        if (cv[c[q].dz][c[q].dy][i + 1 - c[q].dx]) {
+          sacc += (float)cell(i, c[q].dz, c[q].dy, c[q].dx, c[q].ch);
+          ++cnt;
+        }
+      }
+      if (cnt == 4) sacc *= 0.25f;
+      else if (cnt == 2) sacc *= 0.5f;
+      return (uint32_t)to_i32(gcast<T>(sacc));
+    };
+    if constexpr (!DEC) {
+      // ---- encode: the 8 samples of each of the 2^d highres rows, then lowres + maps ----
+      uint32_t hv[NZ][2][8];
+#pragma unroll
+      for (int pz = 0; pz < NZ; ++pz)
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          const I hz_ = 2 * oz + pz, hy_ = 2 * oy + py;
+          const bool rowok = hz_ < (I)g.n[0] && hy_ < (I)g.n[1];
+          const T* rp = src + b * hb + hz_ * hz + hy_ * hy + 2 * ox0;
+          if (rowok && 2 * ox0 + 8 <= (I)g.n[2]) {
+            g_load8<T>(rp, hv[pz][py]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hv[pz][py][e] = (rowok && 2 * ox0 + e < (I)g.n[2]) ? (uint32_t)rp[e] : 0u;
+          }
+        }
+      if (oz < (I)g.E[0] && oy < (I)g.E[1]) {
+        uint32_t lv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lv[i] = hv[0][0][2 * i];
+        T* lp = dst + b * lb + oz * lz + oy * ly + ox0;
+        const int n = (int)((I)g.E[2] - ox0 < nout ? (I)g.E[2] - ox0 : nout);
+        if (n == 4) g_store4<T>(lp, lv);
+        else
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < n) lp[i] = (T)lv[i];
+      }
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
+        const I e0 = (I)(p0 ? g.Lc[0] : g.E[0]), e1 = (I)(p1 ? g.Lc[1] : g.E[1]), e2 = (I)(p2 ? g.Lc[2] : g.E[2]);
+        if (oz >= e0 || oy >= e1) continue;
+        const int n = (int)(e2 - ox0 < nout ? e2 - ox0 : nout);
+        if (n <= 0) continue;
+        uint32_t ov[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ov[i] = (uint32_t)code_encode<CODER>((int32_t)pred(k, i), to_i32((T)hv[NSP == 3 ? p0 : 0][p1][2 * i + p2]));
+        TO* mp = (TO*)omaps.p[k] + ((b * e0 + oz) * e1 + oy) * e2 + ox0;
+        if (n == 4) g_store4<TO>(mp, ov);
+        else
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < n) mp[i] = (TO)ov[i];
+      }
+    } else {
+      // ---- decode: lowres + maps into the 8 samples of each highres row ----
+      uint32_t hv[NZ][2][8];
+      bool hok[NZ][2][8];
+#pragma unroll
+      for (int pz = 0; pz < NZ; ++pz)
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            hv[pz][py][e] = 0u;
+            hok[pz][py][e] = false;
+          }
+      if (oz < (I)g.E[0] && oy < (I)g.E[1]) {
+        const T* lp = src + b * lb + oz * lz + oy * ly + ox0;
+        const int n = (int)((I)g.E[2] - ox0 < nout ? (I)g.E[2] - ox0 : nout);
+        uint32_t lv[4];
+        if (n == 4) g_load4<T>(lp, lv);
+        else
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lv[i] = i < n ? (uint32_t)lp[i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          hv[0][0][2 * i] = lv[i];
+          hok[0][0][2 * i] = i < n;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        const int p0 = gpar<NSP>(k, 0), p1 = gpar<NSP>(k, 1), p2 = gpar<NSP>(k, 2);
+        const I e0 = (I)(p0 ? g.Lc[0] : g.E[0]), e1 = (I)(p1 ? g.Lc[1] : g.E[1]), e2 = (I)(p2 ? g.Lc[2] : g.E[2]);
+        if (oz >= e0 || oy >= e1) continue;
+        const int n = (int)(e2 - ox0 < nout ? e2 - ox0 : nout);
+        if (n <= 0) continue;
+        const TO* mp = (const TO*)imaps.p[k] + ((b * e0 + oz) * e1 + oy) * e2 + ox0;
+        uint32_t mv[4];
+        if (n == 4) g_load4<TO>(mp, mv);
+        else
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mv[i] = i < n ? (uint32_t)mp[i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          hv[NSP == 3 ? p0 : 0][p1][2 * i + p2] = (uint32_t)(T)code_decode<CODER>((int32_t)pred(k, i), (int32_t)(TO)mv[i]);
+          hok[NSP == 3 ? p0 : 0][p1][2 * i + p2] = i < n;
+        }
+      }
+#pragma unroll
+      for (int pz = 0; pz < NZ; ++pz)
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          const I hz_ = 2 * oz + pz, hy_ = 2 * oy + py;
+          if (hz_ >= (I)g.n[0] || hy_ >= (I)g.n[1]) continue;
+          T* rp = dst + b * hb + hz_ * hz + hy_ * hy + 2 * ox0;
+          bool all = true;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) all = all && hok[pz][py][e];
+          if (all) g_store8<T>(rp, hv[pz][py]);
+          else
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (hok[pz][py][e]) rp[e] = (T)hv[pz][py][e];
+        }
     }
   }
 }
@@ -393,6 +648,15 @@ static int encode_generic_t(const T* hi, const Geo& g, int nsp, int64_t B, int64
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
+  if (C == 1 && fits32(g, B, C, K)) {  // one channel: 4 output columns a thread
+    const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
+    const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
+    gen_dispatch<false, T, CODER>(nsp, perch, true, [&](auto nsp_c, auto perch_c, auto) {
+      codec_row4_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, int32_t, false>
+          <<<ggrid(n4), kGThreads, 0, stream>>>(hi, CMapPtrs{}, g, cells, B, lowres, maps, f, R, nxq, n4);
+    });
+    return check_launch("encode_generic");
+  }
   const Flat F = make_flat(f.ext, C);
   gen_dispatch<false, T, CODER>(nsp, perch, fits32(g, B, C, K), [&](auto nsp_c, auto perch_c, auto i_tag) {
     encode_generic_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, decltype(i_tag)>
@@ -416,6 +680,15 @@ static int decode_generic_t(const T* lowres, const CMapPtrs& maps, const Geo& g,
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
+  if (C == 1 && fits32(g, B, C, K)) {  // one channel: 4 output columns a thread
+    const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
+    const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
+    gen_dispatch<true, T, CODER>(nsp, perch, true, [&](auto nsp_c, auto perch_c, auto) {
+      codec_row4_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, int32_t, true>
+          <<<ggrid(n4), kGThreads, 0, stream>>>(lowres, maps, g, cells, B, hi, MapPtrs{}, f, R, nxq, n4);
+    });
+    return check_launch("decode_generic");
+  }
   const Flat F = make_flat(f.ext, C);
   gen_dispatch<true, T, CODER>(nsp, perch, fits32(g, B, C, K), [&](auto nsp_c, auto perch_c, auto i_tag) {
     decode_generic_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, decltype(i_tag)>

@@ -119,15 +119,15 @@ __device__ __forceinline__ void lin_unflat(int64_t row, const LinFlat& f, const 
   x += (I)s.cbeg[2];
 }
 
-// One wave per 32-row tile; rows = (b, cell in box, c) flattened.  Writes preds[row-major
-// [B, Lc..., K, C]] in T and optionally the f32 values.  KK = 2p + 2 at compile time (p <= 2:
+// One wave per 32-row tile; rows = (b, cell in box, c) flattened.  Writes preds[cell * cst + k *
+// kst + c] (launch_linear: interleaved or planar) in T and optionally the f32 values.  KK = 2p + 2 at compile time (p <= 2:
 // the neighbourhood offsets per lane once, the N/2 steps unrolled) or 0 (any p: lin_feature).
 template <typename T, int NSP, int KK, typename I>
 __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
                                                           int64_t B, int64_t C, const float* __restrict__ W,
                                                           const float* __restrict__ bias, int N, int K,
                                                           T* __restrict__ out, float* __restrict__ out_f32,
-                                                          int64_t rows) {
+                                                          int64_t rows, int64_t cst, int64_t kst) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -172,9 +172,9 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
       }
     }
-    // the output offset of each row, held by the row's own lane: cell * K * C + c
+    // the output offset of each row, held by the row's own lane: cell * cst + c (+ k * kst)
     const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
-    const int64_t obase = cell * K * C + c;
+    const int64_t obase = cell * cst + c;
     const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
     // (the shuffles run with every lane active: a lane reading an inactive lane gets no value)
 #pragma unroll
@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
       const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
       const int64_t ob = (int64_t)(uint32_t)__shfl(olo, r, 64) | ((int64_t)__shfl(ohi, r, 64) << 32);
       if (j >= K || tile * 32 + r >= rows) continue;
-      const int64_t o = ob + (int64_t)j * C;
+      const int64_t o = ob + (int64_t)j * kst;
       out[o] = cast_f32<T>(acc[q]);
       if (out_f32) out_f32[o] = acc[q];
     }
@@ -193,13 +193,15 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
 // the K outputs in column tiles of 16, per accumulation step (8 features, kmp_bf16x2.h
 // step_feature) one v_mfma_f32_16x16x32_bf16 per column tile.  u8 / u16 samples only (the byte
 // split is exact for them).  KK as linear_mfma_kernel's: the neighbourhood offsets once per cell,
-// the steps unrolled, each lane's 4 features of a step one select between the two lane groups'.
+// the steps unrolled (step-outer: each A fragment feeds every column tile; per column tile the
+// accumulation order is unchanged, so the bits are), each lane's 4 features of a step one select
+// between the two lane groups'.
 template <typename T, int NSP, int KK, typename I>
 __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
                                                             int64_t B, int64_t C, const float* __restrict__ W,
                                                             const float* __restrict__ bias, int N, int K,
                                                             T* __restrict__ out, float* __restrict__ out_f32,
-                                                            int64_t rows) {
+                                                            int64_t rows, int64_t cst, int64_t kst) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -229,37 +231,85 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
     Nbhd<NSP, (KK > 0 ? KK : 2), I> nb;
     if constexpr (KK > 0) nb.init(s, p, C, b, c, z, y, x);
     const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
-    const int64_t obase = cell * K * C + c;
+    const int64_t obase = cell * cst + c;
     const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
-    for (int ct = 0; ct < nct; ++ct) {
-      const int k = 16 * ct + m;  // this lane's B / D column
-      const bool col_ok = k < K;
-      const float bk = col_ok ? bias[k] : 0.0f;
-      bx::f32x4 acc = {bk, bk, bk, bk};
-      if constexpr (KK > 0) {
-        constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
+    // the lane's output row offsets for the epilogue (every lane active for the shuffle: see
+    // linear_mfma_kernel)
+    auto store = [&](const bx::f32x4& acc, int k) {
 #pragma unroll
-        for (int t = 0; t < NQ; ++t) {
-          bx::u32x4 a;
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 4 * g + r;
+        const int64_t ob = (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
+        if (k >= K || tile * 16 + rr >= rows) continue;
+        const int64_t o = ob + (int64_t)k * kst;
+        out[o] = cast_f32<T>(acc[r]);
+        if (out_f32) out_f32[o] = acc[r];
+      }
+    };
+    if constexpr (KK > 0) {
+      constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
+      // The A fragment depends on (m, g & 1) only, so the two half-waves need the same values:
+      // per pair of steps the low half gathers step t, the high half step t + 1, and one
+      // permlane32 swap per dword gives every lane both (half the gathers of loading each step
+      // in both halves).  Each step's fragment then feeds both column tiles.
+      auto feat = [&](int t, int i, int& n) -> I {  // this lane's feature i of step t and its offset
+        const int n0 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 0, i);
+        const int n1 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 1, i);
+        n = (g & 1) ? n1 : n0;
+        return (g & 1) ? nb.at(n1 < NN ? n1 : 0) : nb.at(n0 < NN ? n0 : 0);
+      };
+      bx::f32x4 acc[NCT0];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {  // the lane group's feature of the step: one select
-            const int n0 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 0, i);
-            const int n1 = bx::step_feature(NSP, (KK - 2) / 2, NQ, t, 1, i);
-            const int n = (g & 1) ? n1 : n0;
-            const I o = (g & 1) ? nb.at(n1 < NN ? n1 : 0) : nb.at(n0 < NN ? n0 : 0);
-            a[i] = bx::feature_dword((row_ok && n < NN) ? (uint32_t)src[o] : 0u);
-          }
-          if constexpr (BREG) {
-            bx::u32x4 bf = breg[0][t];
+      for (int ct = 0; ct < NCT0; ++ct) {
+        const int k = 16 * ct + m;
+        const float bk = k < K ? bias[k] : 0.0f;
+        acc[ct] = bx::f32x4{bk, bk, bk, bk};
+      }
+      auto step = [&](const bx::u32x4& a, int t) {
 #pragma unroll
-            for (int c2 = 1; c2 < NCT0; ++c2) bf = ct == c2 ? breg[c2][t] : bf;
-            acc = bx::mfma(a, bf, acc);
-          } else {
-            acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, NSP, p, t, g, col_ok), acc);
-          }
+        for (int ct = 0; ct < NCT0; ++ct) {
+          const int k = 16 * ct + m;
+          if constexpr (BREG) acc[ct] = bx::mfma(a, breg[ct][t], acc[ct]);
+          else acc[ct] = bx::mfma(a, bx::b_fragment(W + (k < K ? k : 0), K, N, NSP, p, t, g, k < K), acc[ct]);
         }
-      } else {
-        const int64_t bz = b, zz = z, yy = y, xx = x, cc = c;
+      };
+      const bool up = g >= 2;
+#pragma unroll
+      for (int t = 0; t < NQ; t += 2) {
+        bx::u32x4 a0, a1;
+        if (t + 1 < NQ) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            int nl, nu;
+            const I ol = feat(t, i, nl), ou = feat(t + 1, i, nu);
+            const int n = up ? nu : nl;
+            const uint32_t v = bx::feature_dword((row_ok && n < NN) ? (uint32_t)src[up ? ou : ol] : 0u);
+            // lanes 32-63 of the first operand trade with lanes 0-31 of the second
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            a0[i] = r[0];
+            a1[i] = r[1];
+          }
+          step(a0, t);
+          step(a1, t + 1);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            int n;
+            const I o = feat(t, i, n);
+            a0[i] = bx::feature_dword((row_ok && n < NN) ? (uint32_t)src[o] : 0u);
+          }
+          step(a0, t);
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < NCT0; ++ct) store(acc[ct], 16 * ct + m);
+    } else {
+      const int64_t bz = b, zz = z, yy = y, xx = x, cc = c;
+      for (int ct = 0; ct < nct; ++ct) {
+        const int k = 16 * ct + m;  // this lane's B / D column
+        const bool col_ok = k < K;
+        const float bk = col_ok ? bias[k] : 0.0f;
+        bx::f32x4 acc = {bk, bk, bk, bk};
         for (int t = 0; t < nq; ++t) {  // accumulation steps (kmp_bf16x2.h step_feature)
           bx::u32x4 a;
 #pragma unroll
@@ -270,16 +320,7 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
           }
           acc = bx::mfma(a, bx::b_fragment(W + (col_ok ? k : 0), K, N, NSP, p, t, g, col_ok), acc);
         }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = 4 * g + r;
-        // (every lane active for the shuffle: see linear_mfma_kernel)
-        const int64_t ob = (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
-        if (!col_ok || tile * 16 + rr >= rows) continue;
-        const int64_t o = ob + (int64_t)k * C;
-        out[o] = cast_f32<T>(acc[r]);
-        if (out_f32) out_f32[o] = acc[r];
+        store(acc, k);
       }
     }
   }
@@ -287,12 +328,16 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
 
 template <typename T>
 static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t B, int64_t C, const float* W,
-                         const float* bias, T* out, float* out_f32, hipStream_t stream, int kind = KMP_PRED_LINEAR) {
+                         const float* bias, T* out, float* out_f32, hipStream_t stream, int kind = KMP_PRED_LINEAR,
+                         bool planar = false) {
   const int k = 2 * p + 2;
   const int N = nsp == 3 ? k * k * k : k * k;
   const int K = nsp == 3 ? 19 : 5;
   const int64_t rows = B * s.cext[0] * s.cext[1] * s.cext[2] * C;
   if (rows == 0) return KMP_OK;
+  // preds [B, Lc..., K, C] (kmp_linear_predict), or planar [K, B, Lc..., C] (the generic codec's
+  // cells: a map's channel of neighbouring cells is then contiguous)
+  const int64_t cst = planar ? C : K * C, kst = planar ? B * s.Lc[0] * s.Lc[1] * s.Lc[2] * C : C;
   if (kind == KMP_PRED_LINEAR_MFMA) {
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
       int64_t blocks = ceil_div(ceil_div(rows, 16), 4);
@@ -301,7 +346,7 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
       const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
       auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
         linear_bf16x2_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
-            <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows);
+            <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
       };
       auto with_kk = [&](auto nsp_c, auto i_tag) {
         if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
@@ -327,7 +372,7 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
   const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
   auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
     linear_mfma_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
-        <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows);
+        <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
   };
   auto with_kk = [&](auto nsp_c, auto i_tag) {
     if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
@@ -358,7 +403,7 @@ int linear_cells(const T* src, const int64_t* S, int mult, const Geo& g, int nsp
   }
   s.mult = mult;
   return launch_linear<T>(src, s, nsp, pred->padding, B, C, pred->weights, pred->bias, cells, nullptr, stream,
-                          pred->kind);
+                          pred->kind, true);
 }
 
 #define KMP_INSTL(T)                                                                                             \

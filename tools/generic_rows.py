@@ -71,3 +71,35 @@ row('img_lin_p1_u8', I2, np.uint8, kom.LinearPredictor(*w_b(16, 5), 1, 2), 2)
 row('img_lin_p1_u16', (512, 256, 256, 1), np.uint16, kom.LinearPredictor(*w_b(16, 5), 1, 2), 2)
 row('img_mean_p0_c3', (1024, 256, 256, 3), np.uint8, kom.MeanPredictor(0, 2), 2)
 row('vol_mean_p0_i32', (128, 64, 64, 64, 1), np.int32, kom.MeanPredictor(0, 3), 3)
+
+if len(sys.argv) > 2 and sys.argv[2] == 'more':
+    row('img_mean_p0_odd', (1024, 255, 255, 1), np.uint8, kom.MeanPredictor(0, 2), 2)
+    row('img_mean_p1_odd', (1024, 255, 255, 1), np.uint8, kom.MeanPredictor(1, 2), 2)
+    row('vol_mean_p1_odd', (512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(1, 3), 3)
+    row('vol_mean_p0_w100', (64, 128, 128, 100, 1), np.uint16, kom.MeanPredictor(0, 3), 3)
+    row('vol_mean_p0_big', (1, 512, 512, 1024, 1), np.uint16, kom.MeanPredictor(0, 3), 3)
+    row('vol_lin_p1_odd', (256, 63, 63, 63, 1), np.uint16, kom.LinearPredictor(*w_b(64, 19), 1, 3), 3)
+    # the callback path (an opaque predictions_fn) on an odd shape
+    V = kom.volume
+    hi = torch.from_numpy(np.random.default_rng(0).integers(0, 65536, size=(256, 63, 63, 63, 1), dtype=np.int64)
+                          .astype(np.uint16)).cuda()
+    inner = kom.MeanPredictor(0, 3)
+    cb = lambda x: inner(x)  # noqa: E731
+    lo, enc = V.encode(cb, V.encode_values_uint16, hi)
+    te = timed(lambda: V.encode(cb, V.encode_values_uint16, hi))
+    td = timed(lambda: V.decode(cb, V.decode_values_uint16, lo, enc))
+    raw = hi.numel() * 2
+    print(json.dumps({'row': 'vol_callback_p0_odd', 'us': [round(te, 1), round(td, 1)],
+                      'GBps': round(2 * raw / (te + td) / 1e3, 1)}), flush=True)
+    # categorical with class counts the vector kernel does not take
+    for L in (10, 255):
+        torch.manual_seed(0)
+        logits = torch.rand((1 << 18, L), device='cuda')
+        gt = torch.randint(0, L, (1 << 18,), device='cuda', dtype=torch.uint8)
+        enc_c = V.encode_categorical(logits, gt)
+        te = timed(lambda: V.encode_categorical(logits, gt))
+        td = timed(lambda: V.decode_categorical(logits, enc_c))
+        assert torch.equal(V.decode_categorical(logits, enc_c), gt)
+        nb = logits.numel() * 4
+        print(json.dumps({'row': f'categorical_L{L}', 'us': [round(te, 1), round(td, 1)],
+                          'GBps_read': [round(nb / te / 1e3, 1), round(nb / td / 1e3, 1)]}), flush=True)

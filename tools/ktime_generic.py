@@ -12,13 +12,18 @@ from kompressor_amd import _nd  # noqa: E402
 
 name = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+w64 = (1.0 / 64 + np.random.default_rng(1).standard_normal((64, 19)) * 0.005).astype(np.float32)
 w16 = (1.0 / 16 + np.random.default_rng(1).standard_normal((16, 5)) * 0.02).astype(np.float32)
 CFG = {'odd': ((512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(0, 3), 3),
        'odd1': ((512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(1, 3), 3),
        'c2': ((256, 64, 64, 64, 2), np.uint16, kom.MeanPredictor(0, 3), 3),
        'img_c3': ((1024, 256, 256, 3), np.uint8, kom.MeanPredictor(0, 2), 2),
        'img_odd': ((1024, 255, 255, 1), np.uint8, kom.MeanPredictor(0, 2), 2),
-       'img_lin1': ((1024, 256, 256, 1), np.uint8, kom.LinearPredictor(w16, np.zeros(5, np.float32), 1, 2), 2)}
+       'img_lin1': ((1024, 256, 256, 1), np.uint8, kom.LinearPredictor(w16, np.zeros(5, np.float32), 1, 2), 2),
+       'big': ((1, 512, 512, 1024, 1), np.uint16, kom.MeanPredictor(0, 3), 3),
+       'lin1_odd': ((256, 63, 63, 63, 1), np.uint16, kom.LinearPredictor(w64, np.zeros(19, np.float32), 1, 3), 3),
+       'lin1_odd_f32': ((256, 63, 63, 63, 1), np.uint16,
+                        kom.LinearPredictor(w64, np.zeros(19, np.float32), 1, 3, arith='f32'), 3)}
 shape, dt, pred, ndim = CFG[name]
 hi = torch.from_numpy(np.random.default_rng(0).integers(0, np.iinfo(dt).max + 1, size=shape,
                                                          dtype=np.int64).astype(dt)).cuda()
