@@ -24,6 +24,7 @@ struct LinSrc {
   int64_t L[3], E[3];
   int64_t cbeg[3], cext[3];  // box of cells to compute
   int64_t Lc[3];             // cells of the full grid (output indexing)
+  int32_t simple;            // every node index needs at most one reflection per sym (launch_linear)
 };
 
 template <typename T>
@@ -62,7 +63,17 @@ struct Nbhd {
     const I Cc = (I)C, sy = (I)s.S[2] * Cc, sz = (I)s.S[1] * sy;
     base = b * ((I)s.S[0] * sz) + c;
     auto src = [&](int64_t j, int a) -> I {  // source index of padded node j along axis a
-      return (I)(s.mult == 0 ? j : s.mult * sym_index(sym_index(j, s.L[a]), s.E[a]));
+      if (s.mult == 0) return (I)j;
+      if constexpr (sizeof(I) == 4) {
+        if (s.simple) {  // kernel argument: a uniform branch; 32-bit, select-only reflections
+          const int L = (int)s.L[a], E = (int)s.E[a];
+          int v = (int)j;
+          v = v < 0 ? -1 - v : (v >= L ? 2 * L - 1 - v : v);
+          v = v >= E ? 2 * E - 1 - v : v;
+          return (I)(s.mult * v);
+        }
+      }
+      return (I)(s.mult * sym_index(sym_index(j, s.L[a]), s.E[a]));
     };
 #pragma unroll
     for (int d = 0; d < KK; ++d) {
@@ -175,12 +186,13 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
     // the output offset of each row, held by the row's own lane: cell * cst + c (+ k * kst)
     const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
     const int64_t obase = cell * cst + c;
-    const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
+    const int olo = (int)(uint32_t)obase, ohi = sizeof(I) == 4 ? 0 : (int)(obase >> 32);
     // (the shuffles run with every lane active: a lane reading an inactive lane gets no value)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
-      const int64_t ob = (int64_t)(uint32_t)__shfl(olo, r, 64) | ((int64_t)__shfl(ohi, r, 64) << 32);
+      const int64_t ob = sizeof(I) == 4 ? (int64_t)__shfl(olo, r, 64)
+                                        : (int64_t)(uint32_t)__shfl(olo, r, 64) | ((int64_t)__shfl(ohi, r, 64) << 32);
       if (j >= K || tile * 32 + r >= rows) continue;
       const int64_t o = ob + (int64_t)j * kst;
       out[o] = cast_f32<T>(acc[q]);
@@ -222,6 +234,111 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
         breg[ct][t] = bx::b_fragment(W + (k < K ? k : 0), K, N, NSP, p, t, g, k < K);
       }
   }
+  constexpr int NQP = KK > 0 ? ((NSP == 3 ? KK * KK * KK : KK * KK) + 7) / 8 : 1;
+  if constexpr (KK > 0 && NQP <= 8) {
+    // p <= 1 (<= 8 steps): software-pipelined over the wave's tiles.  The gathers are the latency
+    // chain (offsets -> loads -> MFMAs -> stores, with ~3 waves a SIMD), so each iteration issues
+    // the next tile's gathers (16 raw values a lane at most) before the current tile's MFMAs and
+    // stores.  Same fragments, same MFMA order per column tile as the loop below: same bits.
+    constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
+    constexpr int NP = (NQP + 1) / 2;  // step pairs (the last one may be a single step)
+    const bool up = g >= 2;
+    struct In {
+      uint32_t raw[NP][4];
+      int olo, ohi;
+    };
+    auto fetch = [&](int64_t tile, In& in) {
+      const int64_t row = tile * 16 + m;
+      const bool row_ok = row < rows;
+      I b, z, y, x, c;
+      lin_unflat<I>(row_ok ? row : 0, lf, s, C, b, z, y, x, c);
+      Nbhd<NSP, KK, I> nb;
+      nb.init(s, p, C, b, c, z, y, x);
+      auto feat = [&](int t, int i, int& n) -> I {
+        const int n0 = bx::step_feature(NSP, (KK - 2) / 2, NQP, t, 0, i);
+        const int n1 = bx::step_feature(NSP, (KK - 2) / 2, NQP, t, 1, i);
+        n = (g & 1) ? n1 : n0;
+        return (g & 1) ? nb.at(n1 < NN ? n1 : 0) : nb.at(n0 < NN ? n0 : 0);
+      };
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int t = 2 * q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int nl, nu = 0;
+          const I ol = feat(t, i, nl);
+          I o = ol;
+          int n = nl;
+          if (t + 1 < NQP) {  // low half: step t, high half: step t + 1
+            const I ou = feat(t + 1, i, nu);
+            o = up ? ou : ol;
+            n = up ? nu : nl;
+          }
+          in.raw[q][i] = (row_ok && n < NN) ? (uint32_t)src[o] : 0u;
+        }
+      }
+      const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
+      const int64_t obase = cell * cst + c;
+      in.olo = (int)(uint32_t)obase;
+      in.ohi = sizeof(I) == 4 ? 0 : (int)(obase >> 32);
+    };
+    In cur, nxt;
+    int64_t tile = wave;
+    if (tile * 16 < rows) fetch(tile, cur);
+    for (; tile * 16 < rows; tile += nwaves) {
+      if ((tile + nwaves) * 16 < rows) fetch(tile + nwaves, nxt);
+      bx::f32x4 acc[NCT0];
+#pragma unroll
+      for (int ct = 0; ct < NCT0; ++ct) {
+        const int k = 16 * ct + m;
+        const float bk = k < K ? bias[k] : 0.0f;
+        acc[ct] = bx::f32x4{bk, bk, bk, bk};
+      }
+      auto step = [&](const bx::u32x4& a, int t) {
+#pragma unroll
+        for (int ct = 0; ct < NCT0; ++ct) {
+          const int k = 16 * ct + m;
+          if constexpr (BREG) acc[ct] = bx::mfma(a, breg[ct][t], acc[ct]);
+          else acc[ct] = bx::mfma(a, bx::b_fragment(W + (k < K ? k : 0), K, N, NSP, p, t, g, k < K), acc[ct]);
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int t = 2 * q;
+        bx::u32x4 a0, a1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t v = bx::feature_dword(cur.raw[q][i]);
+          if (t + 1 < NQP) {  // lanes 32-63 of the first operand trade with lanes 0-31 of the second
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            a0[i] = r[0];
+            a1[i] = r[1];
+          } else {
+            a0[i] = v;
+          }
+        }
+        step(a0, t);
+        if (t + 1 < NQP) step(a1, t + 1);
+      }
+#pragma unroll
+      for (int ct = 0; ct < NCT0; ++ct) {
+        const int k = 16 * ct + m;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = 4 * g + r;  // (every lane active for the shuffle)
+          const int64_t ob = sizeof(I) == 4
+                                 ? (int64_t)__shfl(cur.olo, rr, 64)
+                                 : (int64_t)(uint32_t)__shfl(cur.olo, rr, 64) | ((int64_t)__shfl(cur.ohi, rr, 64) << 32);
+          if (k >= K || tile * 16 + rr >= rows) continue;
+          const int64_t o = ob + (int64_t)k * kst;
+          out[o] = cast_f32<T>(acc[ct][r]);
+          if (out_f32) out_f32[o] = acc[ct][r];
+        }
+      }
+      cur = nxt;
+    }
+    return;
+  }
   for (int64_t tile = wave; tile * 16 < rows; tile += nwaves) {
     const int64_t row = tile * 16 + m;  // this lane's A row (cell)
     const bool row_ok = row < rows;
@@ -232,14 +349,15 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
     if constexpr (KK > 0) nb.init(s, p, C, b, c, z, y, x);
     const int64_t cell = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x;
     const int64_t obase = cell * cst + c;
-    const int olo = (int)(uint32_t)obase, ohi = (int)(obase >> 32);
+    const int olo = (int)(uint32_t)obase, ohi = sizeof(I) == 4 ? 0 : (int)(obase >> 32);
     // the lane's output row offsets for the epilogue (every lane active for the shuffle: see
     // linear_mfma_kernel)
     auto store = [&](const bx::f32x4& acc, int k) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = 4 * g + r;
-        const int64_t ob = (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
+        const int64_t ob = sizeof(I) == 4 ? (int64_t)__shfl(olo, rr, 64)
+                                          : (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
         if (k >= K || tile * 16 + rr >= rows) continue;
         const int64_t o = ob + (int64_t)k * kst;
         out[o] = cast_f32<T>(acc[r]);
@@ -338,15 +456,34 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
   // preds [B, Lc..., K, C] (kmp_linear_predict), or planar [K, B, Lc..., C] (the generic codec's
   // cells: a map's channel of neighbouring cells is then contiguous)
   const int64_t cst = planar ? C : K * C, kst = planar ? B * s.Lc[0] * s.Lc[1] * s.Lc[2] * C : C;
+  // 32-bit rows, source and output offsets when all stay below 2^31
+  const int64_t lim = (int64_t)1 << 31;
+  const bool i32 = rows < lim && B * s.S[0] * s.S[1] * s.S[2] * C < lim && B * s.Lc[0] * s.Lc[1] * s.Lc[2] * K * C < lim;
+  // one reflection per sym for every node index the box can touch: j in [cbeg - p, cbeg + cext + p]
+  // within [-L, 2L), and sym(., L) < L <= 2E (else the general sym_index)
+  LinSrc sv = s;
+  sv.simple = 1;
+  for (int a = 3 - nsp; a < 3; ++a)
+    if (!(s.cbeg[a] - p >= -s.L[a] && s.cbeg[a] + s.cext[a] + p < 2 * s.L[a] && s.L[a] <= 2 * s.E[a])) sv.simple = 0;
   if (kind == KMP_PRED_LINEAR_MFMA) {
     if constexpr (std::is_same<T, uint8_t>::value || std::is_same<T, uint16_t>::value) {
-      int64_t blocks = ceil_div(ceil_div(rows, 16), 4);
-      if (blocks > 65536) blocks = 65536;
+      // persistent waves, one resident round (the variant's occupancy x CUs): each wave builds its
+      // B fragments once (thousands of instructions, the bf16 splits of the weights), so one wave
+      // per tile or two spent most of the time there
+      const int64_t need = ceil_div(ceil_div(rows, 16), 4);
       const LinFlat lf = make_linflat(s, C);
-      const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
       auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
-        linear_bf16x2_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
-            <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
+        auto kern = linear_bf16x2_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>;
+        static int resident = 0;  // per variant: blocks per CU x CUs
+        if (resident == 0) {
+          int per_cu = 0, dev = 0, cus = 0;
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+          if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+          resident = per_cu * cus;
+        }
+        const int64_t blocks = need < resident ? need : resident;
+        kern<<<(unsigned)blocks, 256, 0, stream>>>(src, sv, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
       };
       auto with_kk = [&](auto nsp_c, auto i_tag) {
         if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
@@ -368,11 +505,9 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
   int64_t blocks = ceil_div(waves, 4);
   if (blocks > 65536) blocks = 65536;
   const LinFlat lf = make_linflat(s, C);
-  // 32-bit rows and source offsets when both stay below 2^31
-  const bool i32 = rows < ((int64_t)1 << 31) && B * s.S[0] * s.S[1] * s.S[2] * C < ((int64_t)1 << 31);
   auto go = [&](auto nsp_c, auto kk_c, auto i_tag) {
     linear_mfma_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value, decltype(i_tag)>
-        <<<(unsigned)blocks, 256, 0, stream>>>(src, s, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
+        <<<(unsigned)blocks, 256, 0, stream>>>(src, sv, lf, p, B, C, W, bias, N, K, out, out_f32, rows, cst, kst);
   };
   auto with_kk = [&](auto nsp_c, auto i_tag) {
     if (p == 0) go(nsp_c, std::integral_constant<int, 2>{}, i_tag);
