@@ -13,10 +13,20 @@
 // result row (cell) of accumulator register r is (r&3) + 8(r>>2) + 4(l>>5), column l&31.
 #include "kmp_bf16x2.h"
 #include "kmp_codec.h"
+#include "kmp_wave.h"
 
 namespace kmp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// astype(T) of an MFMA result: for 8- / 16-bit samples the clamp-then-convert form of the
+// saturating hardware conversion (kmp_wave.h cvt_sat_mfma: NaN -> 0, truncation, saturation --
+// cast_f32's semantics in 3 VALU instead of its f64 path with branches)
+template <typename T>
+__device__ __forceinline__ T lin_cast(float v) {
+  if constexpr (sizeof(T) <= 2) return (T)wv::cvt_sat_mfma<T>(v);
+  else return cast_f32<T>(v);
+}
 
 struct LinSrc {
   int64_t S[3];   // source spatial extents
@@ -166,13 +176,34 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
       Nbhd<NSP, KK, I> nb;
       nb.init(s, p, C, b, c, z, y, x);
       constexpr int NN = NSP == 3 ? KK * KK * KK : KK * KK;
+      if constexpr (NN / 2 > 32) {
+        // 3D p = 2 (108 steps): unrolled per z plane only -- fully unrolled, the compiler hoisted
+        // every gather (310 VGPRs, one wave a SIMD).  Same steps in the same order.
+        constexpr int PL = KK * KK / 2;  // steps per z plane
+#pragma unroll 1
+        for (int dz = 0; dz < KK; ++dz) {
+          I zo = nb.oz[0];
 #pragma unroll
-      for (int st = 0; st < NN / 2; ++st) {
-        // features 2st and 2st + 1 share dz, dy (KK even): the lane's is 2st + h
-        const I o0 = nb.at(2 * st), o1 = nb.at(2 * st + 1);
-        const float a = row_ok ? (float)src[h ? o1 : o0] : 0.0f;
-        const float w = WREG ? wreg[WREG ? st : 0] : (j < K ? W[(2 * st + h) * K + j] : 0.0f);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+          for (int d = 1; d < KK; ++d) zo = dz == d ? nb.oz[d] : zo;
+#pragma unroll
+          for (int q = 0; q < PL; ++q) {
+            const int dy = (2 * q) / KK, dx = (2 * q) % KK;  // features 2q, 2q + 1 of the plane
+            const I o = nb.base + zo + nb.oy[dy] + (h ? nb.ox[dx + 1] : nb.ox[dx]);
+            const float a = row_ok ? (float)src[o] : 0.0f;
+            const int st = dz * PL + q;
+            const float w = j < K ? W[(2 * st + h) * K + j] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < NN / 2; ++st) {
+          // features 2st and 2st + 1 share dz, dy (KK even): the lane's is 2st + h
+          const I o0 = nb.at(2 * st), o1 = nb.at(2 * st + 1);
+          const float a = row_ok ? (float)src[h ? o1 : o0] : 0.0f;
+          const float w = WREG ? wreg[WREG ? st : 0] : (j < K ? W[(2 * st + h) * K + j] : 0.0f);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+        }
       }
     } else {
       const int64_t bz = b, zz = z, yy = y, xx = x, cc = c;
@@ -195,7 +226,7 @@ __global__ void __launch_bounds__(256) linear_mfma_kernel(const T* __restrict__ 
                                         : (int64_t)(uint32_t)__shfl(olo, r, 64) | ((int64_t)__shfl(ohi, r, 64) << 32);
       if (j >= K || tile * 32 + r >= rows) continue;
       const int64_t o = ob + (int64_t)j * kst;
-      out[o] = cast_f32<T>(acc[q]);
+      out[o] = lin_cast<T>(acc[q]);
       if (out_f32) out_f32[o] = acc[q];
     }
   }
@@ -331,7 +362,7 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
                                  : (int64_t)(uint32_t)__shfl(cur.olo, rr, 64) | ((int64_t)__shfl(cur.ohi, rr, 64) << 32);
           if (k >= K || tile * 16 + rr >= rows) continue;
           const int64_t o = ob + (int64_t)k * kst;
-          out[o] = cast_f32<T>(acc[ct][r]);
+          out[o] = lin_cast<T>(acc[ct][r]);
           if (out_f32) out_f32[o] = acc[ct][r];
         }
       }
@@ -360,7 +391,7 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
                                           : (int64_t)(uint32_t)__shfl(olo, rr, 64) | ((int64_t)__shfl(ohi, rr, 64) << 32);
         if (k >= K || tile * 16 + rr >= rows) continue;
         const int64_t o = ob + (int64_t)k * kst;
-        out[o] = cast_f32<T>(acc[r]);
+        out[o] = lin_cast<T>(acc[r]);
         if (out_f32) out_f32[o] = acc[r];
       }
     };

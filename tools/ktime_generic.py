@@ -1,5 +1,5 @@
 """Launch one generic-path configuration N times per direction (for rocprofv3 --kernel-trace --stats).
-    python tools/ktime_generic.py NAME [reps]   (NAME: odd | c2 | img_c3 | img_lin1)"""
+    python tools/ktime_generic.py NAME [reps]   (NAME: a key of CFG)"""
 import os
 import sys
 
@@ -13,6 +13,7 @@ from kompressor_amd import _nd  # noqa: E402
 name = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 w64 = (1.0 / 64 + np.random.default_rng(1).standard_normal((64, 19)) * 0.005).astype(np.float32)
+w216 = (1.0 / 216 + np.random.default_rng(1).standard_normal((216, 19)) * 0.001).astype(np.float32)
 w16 = (1.0 / 16 + np.random.default_rng(1).standard_normal((16, 5)) * 0.02).astype(np.float32)
 CFG = {'odd': ((512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(0, 3), 3),
        'odd1': ((512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(1, 3), 3),
@@ -22,6 +23,7 @@ CFG = {'odd': ((512, 63, 63, 63, 1), np.uint16, kom.MeanPredictor(0, 3), 3),
        'img_lin1': ((1024, 256, 256, 1), np.uint8, kom.LinearPredictor(w16, np.zeros(5, np.float32), 1, 2), 2),
        'big': ((1, 512, 512, 1024, 1), np.uint16, kom.MeanPredictor(0, 3), 3),
        'lin1_odd': ((256, 63, 63, 63, 1), np.uint16, kom.LinearPredictor(w64, np.zeros(19, np.float32), 1, 3), 3),
+       'lin2': ((128, 64, 64, 64, 1), np.uint16, kom.LinearPredictor(w216, np.zeros(19, np.float32), 2, 3), 3),
        'lin1_odd_f32': ((256, 63, 63, 63, 1), np.uint16,
                         kom.LinearPredictor(w64, np.zeros(19, np.float32), 1, 3, arith='f32'), 3)}
 shape, dt, pred, ndim = CFG[name]
