@@ -53,7 +53,7 @@ __device__ __forceinline__ void dcheck_span(const T* base, const T* p, int64_t c
 enum Opt {
   OPT_DISABLE_WAVE, OPT_DISABLE_FAST, OPT_DISABLE_LINEAR_FUSED, OPT_DISABLE_ROWS, OPT_DISABLE_SWAR,
   OPT_W3_PL, OPT_W3P_PL, OPT_W3_XCD, OPT_W2_XCD, OPT_W3_ST_ENC, OPT_W3P_ST_ENC, OPT_W2_ST_ENC,
-  OPT_W2P_ST_ENC, OPT_L3Y, OPT_COUNT
+  OPT_W2P_ST_ENC, OPT_L3Y, OPT_LINEAR_F32_MFMA, OPT_COUNT
 };
 // the option's value, or ``dflt`` while it is unset
 int opt(Opt id, int dflt);

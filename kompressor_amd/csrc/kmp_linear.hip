@@ -475,6 +475,119 @@ __global__ void __launch_bounds__(256) linear_bf16x2_kernel(const T* __restrict_
   }
 }
 
+// KMP_PRED_LINEAR on the vector ALUs: each thread keeps R = 4 consecutive cells of a row and
+// runs the reference's chain for every (cell, k) literally -- acc = b[k]; acc = fmaf(f[n], W[n, k],
+// acc) for n = 0, 1, ... -- so it is the oracle's arithmetic by construction, as the f32 MFMA is.
+// The weights are staged in LDS per workgroup (broadcast reads); a (dz, dy) row of R + KK - 1
+// nodes is read once for the R cells.  The 32 x 32 f32 MFMA tile spent 64 cycles per 2 features x
+// 32 outputs (19 or 5 used) and ran latency-bound at ~1 wave of work per tile; this does K fmas per
+// feature and cell at 16 lanes a cycle with no fragment traffic.
+constexpr int kValuR = 4;
+
+template <typename I>
+__device__ __forceinline__ I node_off(const LinSrc& s, int64_t j, int a) {
+  if (s.mult == 0) return (I)j;
+  if constexpr (sizeof(I) == 4) {
+    if (s.simple) {  // one reflection per sym (launch_linear's check)
+      const int L = (int)s.L[a], E = (int)s.E[a];
+      int v = (int)j;
+      v = v < 0 ? -1 - v : (v >= L ? 2 * L - 1 - v : v);
+      v = v >= E ? 2 * E - 1 - v : v;
+      return (I)(s.mult * v);
+    }
+  }
+  return (I)(s.mult * sym_index(sym_index(j, s.L[a]), s.E[a]));
+}
+
+template <typename T, int NSP, int KK, int KO>
+__global__ void __launch_bounds__(256) linear_valu_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
+                                                          int64_t C, const float* __restrict__ W,
+                                                          const float* __restrict__ bias, T* __restrict__ out,
+                                                          float* __restrict__ out_f32, int64_t nthreads, int64_t nxq,
+                                                          int64_t cst, int64_t kst) {
+  constexpr int R = kValuR, NX = R + KK - 1;
+  using I = int32_t;
+  const I Cc = (I)C, sy = (I)s.S[2] * Cc, sz = (I)s.S[1] * sy;
+  const int sh = s.mult ? p : 0;
+  const int64_t xend = s.cbeg[2] + s.cext[2];        // cells [cbeg, xend) along x
+  const int64_t jmax = xend - 1 - sh + (KK - 1);     // the last node a valid cell reads
+  // the weights in LDS: every lane reads the same word (a broadcast); as scalar loads the compiler
+  // hoisted a row's KK x KO weights into SGPRs and spilled
+  constexpr int NW = (NSP == 3 ? KK * KK * KK : KK * KK) * KO;
+  __shared__ float wl[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) wl[i] = W[i];
+  __syncthreads();
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nthreads;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    // (b, z, y, xq, c), c fastest: the LinFlat of a box whose x extent is nxq groups
+    uint32_t u = (uint32_t)t, q;
+    q = (__umulhi(u, lf.dC_m) + u) >> lf.dC_s; const I c = (I)(u - q * lf.C); u = q;
+    q = (__umulhi(u, lf.d2_m) + u) >> lf.d2_s; const I xq = (I)(u - q * lf.e2); u = q;
+    q = (__umulhi(u, lf.d1_m) + u) >> lf.d1_s; const I y = (I)(u - q * lf.e1) + (I)s.cbeg[1]; u = q;
+    q = (__umulhi(u, lf.d0_m) + u) >> lf.d0_s; const I z = (I)(u - q * lf.e0) + (I)s.cbeg[0];
+    const I b = (I)q;
+    const I x0 = (I)s.cbeg[2] + R * xq;
+    const I base = b * ((I)s.S[0] * sz) + c;
+    I ox[NX], oy[KK], oz[NSP == 3 ? KK : 1];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      int64_t j = (int64_t)x0 - sh + i;
+      j = j > jmax ? jmax : j;  // past the box's last cell: any in-range node (not stored)
+      ox[i] = node_off<I>(s, j, 2) * Cc;
+    }
+#pragma unroll
+    for (int d = 0; d < KK; ++d) {
+      oy[d] = node_off<I>(s, (int64_t)y - sh + d, 1) * sy;
+      if constexpr (NSP == 3) oz[d] = node_off<I>(s, (int64_t)z - sh + d, 0) * sz;
+    }
+    float acc[R][KO];
+#pragma unroll
+    for (int k = 0; k < KO; ++k) {
+      const float bk = bias[k];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][k] = bk;
+    }
+    // one (dz, dy) row of nodes per iteration, in feature order (a runtime loop: the code stays
+    // small and the row's loads are the only ones in flight)
+    constexpr int NROW = (NSP == 3 ? KK : 1) * KK;
+#pragma unroll 1
+    for (int row = 0; row < NROW; ++row) {
+      const int dz = row / KK, dy = row - dz * KK;
+      I zo = NSP == 3 ? oz[0] : 0, yo = oy[0];
+#pragma unroll
+      for (int d = 1; d < KK; ++d) {
+        if constexpr (NSP == 3) zo = dz == d ? oz[d] : zo;
+        yo = dy == d ? oy[d] : yo;
+      }
+      const I rb = base + zo + yo;
+      float f[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) f[i] = (float)src[rb + ox[i]];
+      const float* wr = wl + row * KK * KO;
+#pragma unroll
+      for (int dx = 0; dx < KK; ++dx) {
+#pragma unroll
+        for (int k = 0; k < KO; ++k) {
+          const float w = wr[dx * KO + k];
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r][k] = __builtin_fmaf(f[r + dx], w, acc[r][k]);
+        }
+      }
+    }
+    const int64_t cell0 = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (x0 + r >= xend) break;
+      const int64_t ob = (cell0 + r) * cst + c;
+#pragma unroll
+      for (int k = 0; k < KO; ++k) {
+        out[ob + (int64_t)k * kst] = lin_cast<T>(acc[r][k]);
+        if (out_f32) out_f32[ob + (int64_t)k * kst] = acc[r][k];
+      }
+    }
+  }
+}
+
 template <typename T>
 static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t B, int64_t C, const float* W,
                          const float* bias, T* out, float* out_f32, hipStream_t stream, int kind = KMP_PRED_LINEAR,
@@ -531,6 +644,30 @@ static int launch_linear(const T* src, const LinSrc& s, int nsp, int p, int64_t 
       return check_launch("linear_bf16x2");
     }
     return fail(KMP_ERR_UNSUPPORTED, "the matrix-core LinearPredictor (bf16x2) takes uint8 / uint16 samples");
+  }
+  if (i32 && p <= 2 && !opt(OPT_LINEAR_F32_MFMA, 0)) {  // the fma-chain kernel (linear_valu_kernel)
+    const int64_t nxq = ceil_div(s.cext[2], (int64_t)kValuR);
+    const int64_t nthreads = B * s.cext[0] * s.cext[1] * nxq * C;
+    if (nthreads < ((int64_t)1 << 31)) {
+      LinSrc sq = s;
+      sq.cext[2] = nxq;
+      const LinFlat lf = make_linflat(sq, C);
+      int64_t blocks = ceil_div(nthreads, 256);
+      if (blocks > 65536) blocks = 65536;
+      auto go = [&](auto nsp_c, auto kk_c) {
+        constexpr int NSP_ = decltype(nsp_c)::value;
+        linear_valu_kernel<T, NSP_, decltype(kk_c)::value, NSP_ == 3 ? 19 : 5>
+            <<<(unsigned)blocks, 256, 0, stream>>>(src, sv, lf, p, C, W, bias, out, out_f32, nthreads, nxq, cst, kst);
+      };
+      auto with_kk = [&](auto nsp_c) {
+        if (p == 0) go(nsp_c, std::integral_constant<int, 2>{});
+        else if (p == 1) go(nsp_c, std::integral_constant<int, 4>{});
+        else go(nsp_c, std::integral_constant<int, 6>{});
+      };
+      if (nsp == 3) with_kk(std::integral_constant<int, 3>{});
+      else with_kk(std::integral_constant<int, 2>{});
+      return check_launch("linear_valu");
+    }
   }
   int64_t waves = ceil_div(rows, 32);
   int64_t blocks = ceil_div(waves, 4);

@@ -19,6 +19,7 @@ const char* const kNames[OPT_COUNT] = {
     "KMP_DISABLE_WAVE", "KMP_DISABLE_FAST", "KMP_DISABLE_LINEAR_FUSED", "KMP_DISABLE_ROWS", "KMP_DISABLE_SWAR",
     "KMP_W3_PL",        "KMP_W3P_PL",       "KMP_W3_XCD",               "KMP_W2_XCD",       "KMP_W3_ST_ENC",
     "KMP_W3P_ST_ENC",   "KMP_W2_ST_ENC",    "KMP_W2P_ST_ENC",           "KMP_L3Y",
+    "KMP_LINEAR_F32_MFMA",
 };
 
 struct Table {

@@ -34,18 +34,23 @@ def _data(shape, dtype, seed):
     return rng.integers(0, np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
 
 
+@pytest.mark.parametrize('kernel', ['valu', 'mfma'])
 @pytest.mark.parametrize('ndim,p,shape,dtype', CASES)
-def test_linear_cell_predictions(kom, ndim, p, shape, dtype):
+def test_linear_cell_predictions(kom, ndim, p, shape, dtype, kernel):
+    """Both f32 kernels (kmp_linear.hip: the per-thread fma chain, the default, and the f32 MFMA
+    under KMP_LINEAR_F32_MFMA=1) are the oracle's k-ordered chain, bit for bit."""
     ons = oracle.volume if ndim == 3 else oracle.image
     hi = _data(shape, dtype, 1)
     w, b = _weights(ndim, p, 2, dtype)
     window = ons.pad_neighborhood(ons.lowres_from_highres(ons.pad_highres(hi)[0]), p)
     pred = kom.LinearPredictor(w, b, p, ndim, arith='f32')
-    cells_t, cells_f = pred.predict_cells(window, with_f32=True)
+    with kom._lib.option('KMP_LINEAR_F32_MFMA', int(kernel == 'mfma')):
+        cells_t, cells_f = pred.predict_cells(window, with_f32=True)
+        assert kom._lib.lib.kmp_last_launch().decode() == 'linear_' + kernel
     feats = ons.features_from_lowres(window, p)
     exact = OP.linear_fma_chain(feats, w, b)
     assert cells_f.dtype == np.float32 and cells_f.shape == exact.shape
-    assert np.array_equal(cells_f.view(np.uint32), exact.view(np.uint32)), 'f32 MFMA != k-ordered fma chain'
+    assert np.array_equal(cells_f.view(np.uint32), exact.view(np.uint32)), f'f32 {kernel} != k-ordered fma chain'
     f64, _ = OP.linear_predictions(feats, w, b, dtype)
     scale = np.tensordot(np.abs(np.moveaxis(feats.astype(np.float64), ndim + 1, -1)), np.abs(w), axes=([-1], [0]))
     scale = np.moveaxis(scale, -1, ndim + 1) + np.abs(b).reshape(-1, 1)
