@@ -18,6 +18,7 @@
 namespace kmp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // astype(T) of an MFMA result: for 8- / 16-bit samples the clamp-then-convert form of the
 // saturating hardware conversion (kmp_wave.h cvt_sat_mfma: NaN -> 0, truncation, saturation --
@@ -499,6 +500,22 @@ __device__ __forceinline__ I node_off(const LinSrc& s, int64_t j, int a) {
   return (I)(s.mult * sym_index(sym_index(j, s.L[a]), s.E[a]));
 }
 
+// R consecutive samples as one (unaligned) store
+template <typename T, int R>
+__device__ __forceinline__ void store_run(T* p, const T (&v)[R]) {
+  static_assert(R == 4, "store_run: 4 samples");
+  if constexpr (sizeof(T) == 1) {
+    typedef uint32_t u32a1 __attribute__((aligned(1)));
+    *(u32a1*)p = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  } else if constexpr (sizeof(T) == 2) {
+    typedef uint32_t u32x2a1 __attribute__((ext_vector_type(2), aligned(1)));
+    *(u32x2a1*)p = u32x2a1{(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16)};
+  } else {
+    typedef uint32_t u32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
+    *(u32x4a1*)p = u32x4a1{(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
+  }
+}
+
 template <typename T, int NSP, int KK, int KO>
 __global__ void __launch_bounds__(256) linear_valu_kernel(const T* __restrict__ src, LinSrc s, LinFlat lf, int p,
                                                           int64_t C, const float* __restrict__ W,
@@ -540,12 +557,14 @@ __global__ void __launch_bounds__(256) linear_valu_kernel(const T* __restrict__ 
       oy[d] = node_off<I>(s, (int64_t)y - sh + d, 1) * sy;
       if constexpr (NSP == 3) oz[d] = node_off<I>(s, (int64_t)z - sh + d, 0) * sz;
     }
-    float acc[R][KO];
+    // accumulators as pairs of cells (2r, 2r + 1): one packed fma (v_pk_fma_f32, an IEEE fma per
+    // half) per pair, output and feature
+    f32x2 acc[R / 2][KO];
 #pragma unroll
     for (int k = 0; k < KO; ++k) {
       const float bk = bias[k];
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r][k] = bk;
+      for (int r = 0; r < R / 2; ++r) acc[r][k] = f32x2{bk, bk};
     }
     // one (dz, dy) row of nodes per iteration, in feature order (a runtime loop: the code stays
     // small and the row's loads are the only ones in flight)
@@ -563,6 +582,9 @@ __global__ void __launch_bounds__(256) linear_valu_kernel(const T* __restrict__ 
       float f[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) f[i] = (float)src[rb + ox[i]];
+      f32x2 fp[NX - 1];  // fp[i] = (f[i], f[i + 1]): cells 2r, 2r + 1 at offset dx read fp[2r + dx]
+#pragma unroll
+      for (int i = 0; i + 1 < NX; ++i) fp[i] = f32x2{f[i], f[i + 1]};
       const float* wr = wl + row * KK * KO;
 #pragma unroll
       for (int dx = 0; dx < KK; ++dx) {
@@ -570,19 +592,34 @@ __global__ void __launch_bounds__(256) linear_valu_kernel(const T* __restrict__ 
         for (int k = 0; k < KO; ++k) {
           const float w = wr[dx * KO + k];
 #pragma unroll
-          for (int r = 0; r < R; ++r) acc[r][k] = __builtin_fmaf(f[r + dx], w, acc[r][k]);
+          for (int r = 0; r < R / 2; ++r)
+            acc[r][k] = __builtin_elementwise_fma(fp[2 * r + dx], f32x2{w, w}, acc[r][k]);
         }
       }
     }
-    const int64_t cell0 = (((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (x0 + r >= xend) break;
-      const int64_t ob = (cell0 + r) * cst + c;
+    // 32-bit output offsets (launch_linear's i32 condition covers the output array)
+    const int ob0 = (int)((((int64_t)b * s.Lc[0] + z) * s.Lc[1] + y) * s.Lc[2] + x0) * (int)cst + c;
+    const int ks = (int)kst, cs = (int)cst;
+    const int nv = (int)(xend - x0 < R ? xend - x0 : R);  // valid cells of the group
+    if (out_f32 == nullptr && cs == 1 && nv == R) {
+      // planar, one channel: the R cells of an output are consecutive -- one store
 #pragma unroll
       for (int k = 0; k < KO; ++k) {
-        out[ob + (int64_t)k * kst] = lin_cast<T>(acc[r][k]);
-        if (out_f32) out_f32[ob + (int64_t)k * kst] = acc[r][k];
+        T v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = lin_cast<T>(acc[r / 2][k][r & 1]);
+        store_run<T, R>(out + ob0 + k * ks, v);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= nv) break;
+#pragma unroll
+        for (int k = 0; k < KO; ++k) {
+          const float v = acc[r / 2][k][r & 1];
+          out[ob0 + r * cs + k * ks] = lin_cast<T>(v);
+          if (out_f32) out_f32[ob0 + r * cs + k * ks] = v;
+        }
       }
     }
   }
