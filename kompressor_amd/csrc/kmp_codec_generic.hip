@@ -149,6 +149,79 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restric
   }
 }
 
+// The cell mean for 8- / 16-bit samples when the neighbourhood's sum is an exact float32 integer
+// (N x max sample < 2^24: u8 at p <= 4, u16 at p <= 2): the reference's in-order float sum is then
+// the integer sum, so it can be formed in any order.  A thread takes R = 4 consecutive cells of a
+// row and reads each (dz, dy) row of R + KK - 1 nodes once (28 loads for 4 cells at p = 1 instead
+// of 4 x 64), the 4 windowed sums by sliding.
+constexpr int kMeanR = 4;
+
+template <typename T, int NSP, int KK>
+__global__ void __launch_bounds__(kGThreads) cell_mean_row_kernel(const T* __restrict__ src, Src s, Geo g, int64_t C,
+                                                                int p, Frame cf, Flat F, T* __restrict__ cells,
+                                                                int64_t total) {
+  constexpr int R = kMeanR, NX = R + KK - 1;
+  using I = int32_t;
+  const float n_f = (float)((NSP == 3 ? KK : 1) * KK * KK);
+  const I Cc = (I)C, sy = (I)s.S[2] * Cc, sz = (I)s.S[1] * sy, sb = (I)s.S[0] * sz;
+  const I cy = (I)g.Lc[2] * Cc, cz = (I)g.Lc[1] * cy, cb = (I)g.Lc[0] * cz;
+  const int pz = NSP == 3 ? p : 0;
+  const I xend = (I)(cf.begin[2] + cf.ext[2]);
+  const int64_t jmax = xend - 1 - p + (KK - 1);  // the last node a valid cell reads
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ext_q[3] = {cf.ext[0], cf.ext[1], (cf.ext[2] + R - 1) / R};
+    I b, z, y, xq, c;
+    unflat_i<I>(t, F, ext_q, C, b, z, y, xq, c);
+    z += (I)cf.begin[0];
+    y += (I)cf.begin[1];
+    const I x0 = (I)cf.begin[2] + R * xq;
+    const I base = b * sb + c;
+    I ox[NX], oy[KK], oz[NSP == 3 ? KK : 1];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      int64_t j = (int64_t)x0 - p + i;
+      j = j > jmax ? jmax : j;
+      ox[i] = (I)node_src(j, g.L[2], g.E[2], s.mult) * Cc;
+    }
+#pragma unroll
+    for (int d = 0; d < KK; ++d) {
+      oy[d] = (I)node_src(y - p + d, g.L[1], g.E[1], s.mult) * sy;
+      if constexpr (NSP == 3) oz[d] = (I)node_src(z - pz + d, g.L[0], g.E[0], s.mult) * sz;
+    }
+    uint32_t sum[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) sum[r] = 0u;
+    constexpr int ZU = NSP == 3 && KK <= 4 ? KK : 1;  // 3D p = 2: a runtime z loop (all 324 loads
+                                                    // hoisted took 267 VGPRs)
+#pragma unroll ZU
+    for (int dz = 0; dz < (NSP == 3 ? KK : 1); ++dz) {
+      I zo = NSP == 3 ? oz[0] : 0;
+#pragma unroll
+      for (int d = 1; d < (NSP == 3 ? KK : 1); ++d) zo = dz == d ? oz[d] : zo;
+#pragma unroll
+      for (int dy = 0; dy < KK; ++dy) {
+        const I rb = base + zo + oy[dy];
+        uint32_t v[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) v[i] = (uint32_t)src[rb + ox[i]];
+        uint32_t w = 0u;
+#pragma unroll
+        for (int i = 0; i < KK; ++i) w += v[i];
+        sum[0] += w;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          w += v[r + KK - 1] - v[r - 1];
+          sum[r] += w;
+        }
+      }
+    }
+    const I ob = b * cb + z * cz + y * cy + x0 * Cc + c;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (x0 + r < xend) cells[ob + r * Cc] = gcast<T>((float)sum[r] / n_f);
+  }
+}
+
 // Per output position o (and channel): the lowres node and the 7 (3) maps.  The cell values the
 // maps aggregate are read once: the 2^d cells o - {0,1}^d (MeanPredictor: one value per cell), or
 // each contribution's channel (LinearPredictor: K per cell, planar: channel ch of every cell in
@@ -587,12 +660,31 @@ static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int6
   const int64_t ncell = B * cf.ext[0] * cf.ext[1] * cf.ext[2] * C;
   if (ncell == 0) return KMP_OK;
   if (pred->kind == KMP_PRED_MEAN) {
-    const Flat F = make_flat(cf.ext, C);
     const bool i32 = fits32(g, B, C, 1);
+    const int p = pred->padding, kk = 2 * p + 2;
+    const int64_t nn = (nsp == 3 ? kk : 1) * (int64_t)kk * kk;
+    const int64_t top = std::is_same<T, uint8_t>::value ? 255 : (std::is_same<T, uint16_t>::value ? 65535 : -1);
+    if (i32 && p <= 2 && top > 0 && nn * top < ((int64_t)1 << 24)) {  // exact integer sums: cell_mean_row_kernel
+      const int64_t ext_q[3] = {cf.ext[0], cf.ext[1], ceil_div(cf.ext[2], (int64_t)kMeanR)};
+      const Flat Fq = make_flat(ext_q, C);
+      const int64_t nq = B * ext_q[0] * ext_q[1] * ext_q[2] * C;
+      auto go = [&](auto nsp_c, auto kk_c) {
+        cell_mean_row_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value>
+            <<<ggrid(nq), kGThreads, 0, stream>>>(src, s, g, C, p, cf, Fq, cells, nq);
+      };
+      auto with_kk = [&](auto nsp_c) {
+        if (p == 0) go(nsp_c, std::integral_constant<int, 2>{});
+        else if (p == 1) go(nsp_c, std::integral_constant<int, 4>{});
+        else go(nsp_c, std::integral_constant<int, 6>{});
+      };
+      if (nsp == 3) with_kk(std::integral_constant<int, 3>{});
+      else with_kk(std::integral_constant<int, 2>{});
+      return check_launch("cell_mean");
+    }
+    const Flat F = make_flat(cf.ext, C);
     auto go = [&](auto nsp_c, auto i_tag) {
       constexpr int NSP = decltype(nsp_c)::value;
       using I = decltype(i_tag);
-      const int p = pred->padding;
 #define KMP_CM(KK) cell_mean_kernel<T, NSP, KK, I><<<ggrid(ncell), kGThreads, 0, stream>>>(src, s, g, B, C, p, cf, F, cells, ncell)
       if (p == 0) KMP_CM(2);
       else if (p == 1) KMP_CM(4);
