@@ -149,14 +149,14 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_kernel(const T* __restric
   }
 }
 
-// The cell mean for 8- / 16-bit samples when the neighbourhood's sum is an exact float32 integer
-// (N x max sample < 2^24: u8 at p <= 4, u16 at p <= 2): the reference's in-order float sum is then
-// the integer sum, so it can be formed in any order.  A thread takes R = 4 consecutive cells of a
-// row and reads each (dz, dy) row of R + KK - 1 nodes once (28 loads for 4 cells at p = 1 instead
-// of 4 x 64), the 4 windowed sums by sliding.
+// The cell mean, R = 4 consecutive cells of a row per thread: each (dz, dy) row of R + KK - 1 nodes
+// is read once for the 4 cells (28 loads for 4 cells at p = 1 instead of 4 x 64).  EXACT (8- /
+// 16-bit samples with N x max sample < 2^24: u8 at p <= 4, u16 at p <= 2): the reference's
+// in-order float sum is the integer sum, formed by sliding windows; otherwise each cell's float
+// sum is accumulated in the reference's feature order (z-major, y, x), exactly cell_mean_kernel's.
 constexpr int kMeanR = 4;
 
-template <typename T, int NSP, int KK>
+template <typename T, int NSP, int KK, bool EXACT>
 __global__ void __launch_bounds__(kGThreads) cell_mean_row_kernel(const T* __restrict__ src, Src s, Geo g, int64_t C,
                                                                 int p, Frame cf, Flat F, T* __restrict__ cells,
                                                                 int64_t total) {
@@ -189,8 +189,12 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_row_kernel(const T* __res
       if constexpr (NSP == 3) oz[d] = (I)node_src(z - pz + d, g.L[0], g.E[0], s.mult) * sz;
     }
     uint32_t sum[R];
+    float fsum[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) sum[r] = 0u;
+    for (int r = 0; r < R; ++r) {
+      sum[r] = 0u;
+      fsum[r] = 0.0f;
+    }
     constexpr int ZU = NSP == 3 && KK <= 4 ? KK : 1;  // 3D p = 2: a runtime z loop (all 324 loads
                                                     // hoisted took 267 VGPRs)
 #pragma unroll ZU
@@ -201,24 +205,34 @@ __global__ void __launch_bounds__(kGThreads) cell_mean_row_kernel(const T* __res
 #pragma unroll
       for (int dy = 0; dy < KK; ++dy) {
         const I rb = base + zo + oy[dy];
-        uint32_t v[NX];
+        if constexpr (EXACT) {
+          uint32_t v[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) v[i] = (uint32_t)src[rb + ox[i]];
-        uint32_t w = 0u;
+          for (int i = 0; i < NX; ++i) v[i] = (uint32_t)src[rb + ox[i]];
+          uint32_t w = 0u;
 #pragma unroll
-        for (int i = 0; i < KK; ++i) w += v[i];
-        sum[0] += w;
+          for (int i = 0; i < KK; ++i) w += v[i];
+          sum[0] += w;
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-          w += v[r + KK - 1] - v[r - 1];
-          sum[r] += w;
+          for (int r = 1; r < R; ++r) {
+            w += v[r + KK - 1] - v[r - 1];
+            sum[r] += w;
+          }
+        } else {
+          float v[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) v[i] = (float)src[rb + ox[i]];
+#pragma unroll
+          for (int dx = 0; dx < KK; ++dx)
+#pragma unroll
+            for (int r = 0; r < R; ++r) fsum[r] += v[r + dx];
         }
       }
     }
     const I ob = b * cb + z * cz + y * cy + x0 * Cc + c;
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      if (x0 + r < xend) cells[ob + r * Cc] = gcast<T>((float)sum[r] / n_f);
+      if (x0 + r < xend) cells[ob + r * Cc] = gcast<T>((EXACT ? (float)sum[r] : fsum[r]) / n_f);
   }
 }
 
@@ -664,18 +678,21 @@ static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int6
     const int p = pred->padding, kk = 2 * p + 2;
     const int64_t nn = (nsp == 3 ? kk : 1) * (int64_t)kk * kk;
     const int64_t top = std::is_same<T, uint8_t>::value ? 255 : (std::is_same<T, uint16_t>::value ? 65535 : -1);
-    if (i32 && p <= 2 && top > 0 && nn * top < ((int64_t)1 << 24)) {  // exact integer sums: cell_mean_row_kernel
+    if (i32 && p <= 3) {  // cell_mean_row_kernel: exact integer sums when they are, else in-order floats
+      const bool exact = top > 0 && nn * top < ((int64_t)1 << 24);
       const int64_t ext_q[3] = {cf.ext[0], cf.ext[1], ceil_div(cf.ext[2], (int64_t)kMeanR)};
       const Flat Fq = make_flat(ext_q, C);
       const int64_t nq = B * ext_q[0] * ext_q[1] * ext_q[2] * C;
       auto go = [&](auto nsp_c, auto kk_c) {
-        cell_mean_row_kernel<T, decltype(nsp_c)::value, decltype(kk_c)::value>
-            <<<ggrid(nq), kGThreads, 0, stream>>>(src, s, g, C, p, cf, Fq, cells, nq);
+        constexpr int NSP = decltype(nsp_c)::value, KK = decltype(kk_c)::value;
+        if (exact) cell_mean_row_kernel<T, NSP, KK, true><<<ggrid(nq), kGThreads, 0, stream>>>(src, s, g, C, p, cf, Fq, cells, nq);
+        else cell_mean_row_kernel<T, NSP, KK, false><<<ggrid(nq), kGThreads, 0, stream>>>(src, s, g, C, p, cf, Fq, cells, nq);
       };
       auto with_kk = [&](auto nsp_c) {
         if (p == 0) go(nsp_c, std::integral_constant<int, 2>{});
         else if (p == 1) go(nsp_c, std::integral_constant<int, 4>{});
-        else go(nsp_c, std::integral_constant<int, 6>{});
+        else if (p == 2) go(nsp_c, std::integral_constant<int, 6>{});
+        else go(nsp_c, std::integral_constant<int, 8>{});
       };
       if (nsp == 3) with_kk(std::integral_constant<int, 3>{});
       else with_kk(std::integral_constant<int, 2>{});

@@ -734,3 +734,35 @@ def test_encode_store_policy_is_output_neutral(kom, case, cached, kmp_opt):
     for i, (a, b) in enumerate(zip(maps, want_maps)):
         assert np.array_equal(a, b), (knob, cached, i)
     assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
+
+
+@pytest.mark.parametrize('ndim,shape,dtype,p,top', [
+    # u16 at p = 3 takes the in-order float kernel; values < 2^14 keep its sums exact, because past
+    # 2^24 the sum's order matters and the reference does not pin it (XLA's reduce; the oracle's
+    # np.mean) -- see oracle/predictors.py mean_predictions_fn
+    (3, (2, 21, 18, 23, 1), np.uint16, 3, 1 << 14),
+    (3, (1, 30, 26, 34, 1), np.uint8, 3, None),    # exact integer sums
+    (3, (2, 19, 27, 33, 1), np.uint16, 2, None),
+    (3, (2, 17, 15, 31, 2), np.uint16, 1, None),   # two channels
+    (2, (3, 45, 38, 1), np.uint16, 3, None),
+    (2, (2, 61, 77, 3), np.uint8, 2, None),        # RGB
+])
+def test_generic_mean_cells_match_oracle(kom, ndim, shape, dtype, p, top):
+    """The generic path's cell means (kmp_codec_generic.hip cell_mean_row_kernel: 4 cells of a row
+    per thread, exact integer sums or the reference's in-order float sum) on shapes the one-pass
+    kernels do not take, paddings up to 3, against the oracle, encode and decode."""
+    import oracle
+    from oracle import predictors as OP
+    ns, ons = (kom.volume, oracle.volume) if ndim == 3 else (kom.image, oracle.image)
+    enc, dec, oenc = (ns.encode_values_uint16, ns.decode_values_uint16, ons.encode_values_uint16) \
+        if dtype == np.uint16 else (ns.encode_values_uint8, ns.decode_values_uint8, ons.encode_values_uint8)
+    x = np.random.default_rng(21).integers(0, top or np.iinfo(dtype).max + 1, size=shape, dtype=np.int64).astype(dtype)
+    want_lo, (want_maps, want_dims) = ons.encode(OP.mean_predictions_fn(p, ndim), oenc, x, padding=p)
+    pred = kom.MeanPredictor(p, ndim)
+    lo, (maps, dims) = ns.encode(pred, enc, x, padding=p)
+    assert _last_launch(kom) == 'encode_generic'
+    assert tuple(dims) == tuple(want_dims) and np.array_equal(lo, want_lo)
+    for i, (a, b) in enumerate(zip(maps, want_maps)):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f'map {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}'
+    assert np.array_equal(ns.decode(pred, dec, lo, (maps, dims), padding=p), x)
