@@ -370,64 +370,46 @@ typedef uint32_t g32a1 __attribute__((aligned(1)));
 typedef uint8_t g8x4 __attribute__((ext_vector_type(4)));
 typedef uint8_t g8x4a1 __attribute__((ext_vector_type(4), aligned(1)));
 
-template <typename T>
-__device__ __forceinline__ void g_load8(const T* p, uint32_t (&v)[8]) {  // 8 consecutive samples
-  if constexpr (sizeof(T) == 1) {
-    const g32x2a1 w = *(const g32x2a1*)p;
+// N consecutive samples (N x sizeof(T) a multiple of 4 bytes) as unaligned dword vector accesses
+template <typename T, int N>
+__device__ __forceinline__ void g_loadn(const T* p, uint32_t (&v)[N]) {
+  constexpr int NW = N * (int)sizeof(T) / 4;
+  static_assert(N * sizeof(T) % 4 == 0, "g_loadn: whole dwords");
+  uint32_t w[NW];
+  const char* c = (const char*)p;
+  constexpr int N4 = NW / 4 * 4;  // dwordx4 pieces, then one x2 and / or one x1
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
-  } else if constexpr (sizeof(T) == 2) {
-    const g32x4a1 w = *(const g32x4a1*)p;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-  } else {
-    const g32x4a1 a = *(const g32x4a1*)p, b = *(const g32x4a1*)(p + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+  for (int i = 0; i < N4; i += 4) {
+    const g32x4a1 t = *(const g32x4a1*)(c + 4 * i);
+    w[i] = t[0]; w[i + 1] = t[1]; w[i + 2] = t[2]; w[i + 3] = t[3];
   }
+  if constexpr (NW - N4 >= 2) {
+    const g32x2a1 t = *(const g32x2a1*)(c + 4 * N4);
+    w[N4] = t[0]; w[N4 + 1] = t[1];
+  }
+  if constexpr ((NW - N4) % 2) w[NW - 1] = *(const g32a1*)(c + 4 * (NW - 1));
+  constexpr int PER = 4 / (int)(sizeof(T) < 4 ? sizeof(T) : 4);
+  constexpr uint32_t MASK = sizeof(T) == 1 ? 0xffu : (sizeof(T) == 2 ? 0xffffu : 0xffffffffu);
+#pragma unroll
+  for (int e = 0; e < N; ++e) v[e] = (w[e / PER] >> (8 * sizeof(T) * (e % PER))) & MASK;
 }
-template <typename T>
-__device__ __forceinline__ void g_store8(T* p, const uint32_t (&v)[8]) {
-  if constexpr (sizeof(T) == 1) {
-    uint32_t w[2] = {0u, 0u};
+template <typename T, int N>
+__device__ __forceinline__ void g_storen(T* p, const uint32_t (&v)[N]) {
+  constexpr int NW = N * (int)sizeof(T) / 4;
+  static_assert(N * sizeof(T) % 4 == 0, "g_storen: whole dwords");
+  constexpr int PER = 4 / (int)(sizeof(T) < 4 ? sizeof(T) : 4);
+  constexpr uint32_t MASK = sizeof(T) == 1 ? 0xffu : (sizeof(T) == 2 ? 0xffffu : 0xffffffffu);
+  uint32_t w[NW];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) w[e >> 2] |= (v[e] & 0xffu) << (8 * (e & 3));
-    *(g32x2a1*)p = g32x2a1{w[0], w[1]};
-  } else if constexpr (sizeof(T) == 2) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+  for (int i = 0; i < NW; ++i) w[i] = 0u;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) w[e >> 1] |= (v[e] & 0xffffu) << (16 * (e & 1));
-    *(g32x4a1*)p = g32x4a1{w[0], w[1], w[2], w[3]};
-  } else {
-    *(g32x4a1*)p = g32x4a1{v[0], v[1], v[2], v[3]};
-    *(g32x4a1*)(p + 4) = g32x4a1{v[4], v[5], v[6], v[7]};
-  }
-}
-template <typename T>
-__device__ __forceinline__ void g_store4(T* p, const uint32_t (&v)[4]) {  // 4 consecutive values
-  if constexpr (sizeof(T) == 1) {
-    *(g8x4a1*)p = g8x4{(uint8_t)v[0], (uint8_t)v[1], (uint8_t)v[2], (uint8_t)v[3]};
-  } else if constexpr (sizeof(T) == 2) {
-    *(g32x2a1*)p = g32x2a1{(v[0] & 0xffffu) | (v[1] << 16), (v[2] & 0xffffu) | (v[3] << 16)};
-  } else {
-    *(g32x4a1*)p = g32x4a1{v[0], v[1], v[2], v[3]};
-  }
-}
-template <typename T>
-__device__ __forceinline__ void g_load4(const T* p, uint32_t (&v)[4]) {
-  if constexpr (sizeof(T) == 1) {
-    const uint32_t w = *(const g32a1*)p;
+  for (int e = 0; e < N; ++e) w[e / PER] |= (v[e] & MASK) << (8 * sizeof(T) * (e % PER));
+  char* c = (char*)p;
+  constexpr int N4 = NW / 4 * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (w >> (8 * e)) & 0xffu;
-  } else if constexpr (sizeof(T) == 2) {
-    const g32x2a1 w = *(const g32x2a1*)p;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-  } else {
-    const g32x4a1 w = *(const g32x4a1*)p;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = w[e];
-  }
+  for (int i = 0; i < N4; i += 4) *(g32x4a1*)(c + 4 * i) = g32x4a1{w[i], w[i + 1], w[i + 2], w[i + 3]};
+  if constexpr (NW - N4 >= 2) *(g32x2a1*)(c + 4 * N4) = g32x2a1{w[N4], w[N4 + 1]};
+  if constexpr ((NW - N4) % 2) *(g32a1*)(c + 4 * (NW - 1)) = w[NW - 1];
 }
 
 // (b, oz, oy, xq) of a flat thread index over B x ext0 x ext1 x nxq (xq: a group of 4 columns)
@@ -435,17 +417,21 @@ struct Row4 {
   FDiv dq, d1, d0;
 };
 
-template <typename T, int CODER, bool PERCH, int NSP, typename I, bool DEC>
+// CC channels (1..4, interleaved): a thread owns 4 output positions x CC channels of a row, so
+// its highres rows are 8 x CC consecutive samples, its lowres / map values 4 x CC, its cells 5 x CC
+template <typename T, int CODER, bool PERCH, int NSP, int CC, bool DEC>
 __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restrict__ src, CMapPtrs imaps, Geo g,
                                                              const T* __restrict__ cells, int64_t B, T* __restrict__ dst,
                                                              MapPtrs omaps, Frame f, Row4 R, int64_t nxq,
                                                              int64_t total) {
+  using I = int32_t;
   using TO = typename coder_out<CODER>::type;
   constexpr int NM = NSP == 3 ? 7 : 3;
   constexpr int NZ = NSP == 3 ? 2 : 1;
-  const I hy = (I)g.n[2], hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
-  const I ly = (I)g.E[2], lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
-  const I cy = (I)g.Lc[2], cz = (I)g.Lc[1] * cy, cb = (I)g.Lc[0] * cz;
+  constexpr int NH = 8 * CC, NO = 4 * CC;  // samples of a highres row segment / of an output group
+  const I hy = (I)g.n[2] * CC, hz = (I)g.n[1] * hy, hb = (I)g.n[0] * hz;
+  const I ly = (I)g.E[2] * CC, lz = (I)g.E[1] * ly, lb = (I)g.E[0] * lz;
+  const I cy = (I)g.Lc[2] * CC, cz = (I)g.Lc[1] * cy, cb = (I)g.Lc[0] * cz;
   const I kp = (I)B * cb;  // LinearPredictor: channel plane stride (planar cells)
   const I end2 = (I)(f.begin[2] + f.ext[2]);
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -461,9 +447,9 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
     const I ox0 = (I)f.begin[2] + 4 * xq;
     const int nout = (int)(end2 - ox0 < 4 ? end2 - ox0 : 4);
     // ---- the cells around the 4 outputs: (oz - dz, oy - dy, ox0 - 1 + j), j = 0..4 ----
-    const I cbase = b * cb + oz * cz + oy * cy + ox0;  // cell (oz, oy, ox0)
+    const I cbase = b * cb + oz * cz + oy * cy + ox0 * CC;  // cell (oz, oy, ox0), channel 0
     bool cv[2][2][5];
-    T cm[2][2][5];
+    T cm[2][2][5][CC];
 #pragma unroll
     for (int dz = 0; dz < 2; ++dz)
 #pragma unroll
@@ -474,24 +460,27 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         for (int j = 0; j < 5; ++j) {
           const I x = ox0 - 1 + j;
           cv[dz][dy][j] = rowok && x >= 0 && x < (I)g.Lc[2];
-          if (!PERCH) cm[dz][dy][j] = cv[dz][dy][j] ? cells[cbase - dz * cz - dy * cy + (j - 1)] : T(0);
+#pragma unroll
+          for (int ch = 0; ch < CC; ++ch)
+            if (!PERCH) cm[dz][dy][j][ch] = cv[dz][dy][j] ? cells[cbase - dz * cz - dy * cy + (j - 1) * CC + ch] : T(0);
         }
       }
-    auto cell = [&](int i, int dz, int dy, int dx, int ch) -> T {
-      if constexpr (PERCH) return cells[cbase - dz * cz - dy * cy + (i - dx) + (I)ch * kp];
-      else return cm[dz][dy][i + 1 - dx];
+    // map k's contribution channel kch of the cell (oz - dz, oy - dy, ox0 + i - dx), sample channel ch
+    auto cell = [&](int i, int dz, int dy, int dx, int kch, int ch) -> T {
+      if constexpr (PERCH) return cells[cbase - dz * cz - dy * cy + (i - dx) * CC + ch + (I)kch * kp];
+      else return cm[dz][dy][i + 1 - dx][ch];
     };
-    auto pred = [&](int k, int i) -> uint32_t {
+    auto pred = [&](int k, int i, int ch) -> uint32_t {
       Contrib c[4];
       const int nc = map_contribs(NSP, k, c);
-      if (k == center_map(NSP)) return (uint32_t)to_i32(cell(i, 0, 0, 0, c[0].ch));
+      if (k == center_map(NSP)) return (uint32_t)to_i32(cell(i, 0, 0, 0, c[0].ch, ch));
       float sacc = 0.0f;
       int cnt = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (q >= nc) break;
         if (cv[c[q].dz][c[q].dy][i + 1 - c[q].dx]) {
-          sacc += (float)cell(i, c[q].dz, c[q].dy, c[q].dx, c[q].ch);
+          sacc += (float)cell(i, c[q].dz, c[q].dy, c[q].dx, c[q].ch, ch);
           ++cnt;
         }
       }
@@ -500,33 +489,35 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
       return (uint32_t)to_i32(gcast<T>(sacc));
     };
     if constexpr (!DEC) {
-      // ---- encode: the 8 samples of each of the 2^d highres rows, then lowres + maps ----
-      uint32_t hv[NZ][2][8];
+      // ---- encode: the 8 x CC samples of each of the 2^d highres rows, then lowres + maps ----
+      uint32_t hv[NZ][2][NH];
 #pragma unroll
       for (int pz = 0; pz < NZ; ++pz)
 #pragma unroll
         for (int py = 0; py < 2; ++py) {
           const I hz_ = 2 * oz + pz, hy_ = 2 * oy + py;
           const bool rowok = hz_ < (I)g.n[0] && hy_ < (I)g.n[1];
-          const T* rp = src + b * hb + hz_ * hz + hy_ * hy + 2 * ox0;
+          const T* rp = src + b * hb + hz_ * hz + hy_ * hy + 2 * ox0 * CC;
           if (rowok && 2 * ox0 + 8 <= (I)g.n[2]) {
-            g_load8<T>(rp, hv[pz][py]);
+            g_loadn<T, NH>(rp, hv[pz][py]);
           } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) hv[pz][py][e] = (rowok && 2 * ox0 + e < (I)g.n[2]) ? (uint32_t)rp[e] : 0u;
+            for (int e = 0; e < NH; ++e) hv[pz][py][e] = (rowok && 2 * ox0 + e / CC < (I)g.n[2]) ? (uint32_t)rp[e] : 0u;
           }
         }
       if (oz < (I)g.E[0] && oy < (I)g.E[1]) {
-        uint32_t lv[4];
+        uint32_t lv[NO];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lv[i] = hv[0][0][2 * i];
-        T* lp = dst + b * lb + oz * lz + oy * ly + ox0;
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int ch = 0; ch < CC; ++ch) lv[i * CC + ch] = hv[0][0][2 * i * CC + ch];
+        T* lp = dst + b * lb + oz * lz + oy * ly + ox0 * CC;
         const int n = (int)((I)g.E[2] - ox0 < nout ? (I)g.E[2] - ox0 : nout);
-        if (n == 4) g_store4<T>(lp, lv);
+        if (n == 4) g_storen<T, NO>(lp, lv);
         else
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (i < n) lp[i] = (T)lv[i];
+          for (int e = 0; e < NO; ++e)
+            if (e / CC < n) lp[e] = (T)lv[e];
       }
 #pragma unroll
       for (int k = 0; k < NM; ++k) {
@@ -535,20 +526,23 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         if (oz >= e0 || oy >= e1) continue;
         const int n = (int)(e2 - ox0 < nout ? e2 - ox0 : nout);
         if (n <= 0) continue;
-        uint32_t ov[4];
+        uint32_t ov[NO];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          ov[i] = (uint32_t)code_encode<CODER>((int32_t)pred(k, i), to_i32((T)hv[NSP == 3 ? p0 : 0][p1][2 * i + p2]));
-        TO* mp = (TO*)omaps.p[k] + ((b * e0 + oz) * e1 + oy) * e2 + ox0;
-        if (n == 4) g_store4<TO>(mp, ov);
+#pragma unroll
+          for (int ch = 0; ch < CC; ++ch)
+            ov[i * CC + ch] = (uint32_t)code_encode<CODER>((int32_t)pred(k, i, ch),
+                                                           to_i32((T)hv[NSP == 3 ? p0 : 0][p1][(2 * i + p2) * CC + ch]));
+        TO* mp = (TO*)omaps.p[k] + (((b * e0 + oz) * e1 + oy) * e2 + ox0) * CC;
+        if (n == 4) g_storen<TO, NO>(mp, ov);
         else
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (i < n) mp[i] = (TO)ov[i];
+          for (int e = 0; e < NO; ++e)
+            if (e / CC < n) mp[e] = (TO)ov[e];
       }
     } else {
-      // ---- decode: lowres + maps into the 8 samples of each highres row ----
-      uint32_t hv[NZ][2][8];
+      // ---- decode: lowres + maps into the 8 x CC samples of each highres row ----
+      uint32_t hv[NZ][2][8][CC];
       bool hok[NZ][2][8];
 #pragma unroll
       for (int pz = 0; pz < NZ; ++pz)
@@ -556,20 +550,22 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         for (int py = 0; py < 2; ++py)
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            hv[pz][py][e] = 0u;
+#pragma unroll
+            for (int ch = 0; ch < CC; ++ch) hv[pz][py][e][ch] = 0u;
             hok[pz][py][e] = false;
           }
       if (oz < (I)g.E[0] && oy < (I)g.E[1]) {
-        const T* lp = src + b * lb + oz * lz + oy * ly + ox0;
+        const T* lp = src + b * lb + oz * lz + oy * ly + ox0 * CC;
         const int n = (int)((I)g.E[2] - ox0 < nout ? (I)g.E[2] - ox0 : nout);
-        uint32_t lv[4];
-        if (n == 4) g_load4<T>(lp, lv);
+        uint32_t lv[NO];
+        if (n == 4) g_loadn<T, NO>(lp, lv);
         else
 #pragma unroll
-          for (int i = 0; i < 4; ++i) lv[i] = i < n ? (uint32_t)lp[i] : 0u;
+          for (int e = 0; e < NO; ++e) lv[e] = e / CC < n ? (uint32_t)lp[e] : 0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          hv[0][0][2 * i] = lv[i];
+#pragma unroll
+          for (int ch = 0; ch < CC; ++ch) hv[0][0][2 * i][ch] = lv[i * CC + ch];
           hok[0][0][2 * i] = i < n;
         }
       }
@@ -580,15 +576,18 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         if (oz >= e0 || oy >= e1) continue;
         const int n = (int)(e2 - ox0 < nout ? e2 - ox0 : nout);
         if (n <= 0) continue;
-        const TO* mp = (const TO*)imaps.p[k] + ((b * e0 + oz) * e1 + oy) * e2 + ox0;
-        uint32_t mv[4];
-        if (n == 4) g_load4<TO>(mp, mv);
+        const TO* mp = (const TO*)imaps.p[k] + (((b * e0 + oz) * e1 + oy) * e2 + ox0) * CC;
+        uint32_t mv[NO];
+        if (n == 4) g_loadn<TO, NO>(mp, mv);
         else
 #pragma unroll
-          for (int i = 0; i < 4; ++i) mv[i] = i < n ? (uint32_t)mp[i] : 0u;
+          for (int e = 0; e < NO; ++e) mv[e] = e / CC < n ? (uint32_t)mp[e] : 0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          hv[NSP == 3 ? p0 : 0][p1][2 * i + p2] = (uint32_t)(T)code_decode<CODER>((int32_t)pred(k, i), (int32_t)(TO)mv[i]);
+#pragma unroll
+          for (int ch = 0; ch < CC; ++ch)
+            hv[NSP == 3 ? p0 : 0][p1][2 * i + p2][ch] =
+                (uint32_t)(T)code_decode<CODER>((int32_t)pred(k, i, ch), (int32_t)(TO)mv[i * CC + ch]);
           hok[NSP == 3 ? p0 : 0][p1][2 * i + p2] = i < n;
         }
       }
@@ -598,15 +597,20 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         for (int py = 0; py < 2; ++py) {
           const I hz_ = 2 * oz + pz, hy_ = 2 * oy + py;
           if (hz_ >= (I)g.n[0] || hy_ >= (I)g.n[1]) continue;
-          T* rp = dst + b * hb + hz_ * hz + hy_ * hy + 2 * ox0;
+          T* rp = dst + b * hb + hz_ * hz + hy_ * hy + 2 * ox0 * CC;
           bool all = true;
 #pragma unroll
           for (int e = 0; e < 8; ++e) all = all && hok[pz][py][e];
-          if (all) g_store8<T>(rp, hv[pz][py]);
+          uint32_t row[NH];
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int ch = 0; ch < CC; ++ch) row[e * CC + ch] = hv[pz][py][e][ch];
+          if (all) g_storen<T, NH>(rp, row);
           else
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (hok[pz][py][e]) rp[e] = (T)hv[pz][py][e];
+            for (int e = 0; e < NH; ++e)
+              if (hok[pz][py][e / CC]) rp[e] = (T)row[e];
         }
     }
   }
@@ -722,6 +726,16 @@ static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int6
   return linear_cells<T>(src, s.S, s.mult, g, nsp, B, C, pred, cbeg, cext, cells, stream);
 }
 
+// the row kernel's compile-time channel count (1..4; 3D takes 1..2 -- with 3-4 channels its
+// 7 maps' values outgrow the registers and spill)
+template <typename F>
+static void with_cc(int64_t C, F&& f) {
+  if (C == 1) f(std::integral_constant<int, 1>{});
+  else if (C == 2) f(std::integral_constant<int, 2>{});
+  else if (C == 3) f(std::integral_constant<int, 3>{});
+  else f(std::integral_constant<int, 4>{});
+}
+
 // the encode / decode kernel of (NSP, PERCH, I) for this call
 template <bool DEC, typename T, int CODER, typename Launch>
 static void gen_dispatch(int nsp, bool perch, bool i32, Launch&& launch) {
@@ -757,12 +771,16 @@ static int encode_generic_t(const T* hi, const Geo& g, int nsp, int64_t B, int64
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
-  if (C == 1 && fits32(g, B, C, K)) {  // one channel: 4 output columns a thread
+  if (C <= (nsp == 3 ? 2 : 4) && fits32(g, B, C, K)) {  // 4 output positions (x C) a thread
     const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
     const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
     gen_dispatch<false, T, CODER>(nsp, perch, true, [&](auto nsp_c, auto perch_c, auto) {
-      codec_row4_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, int32_t, false>
-          <<<ggrid(n4), kGThreads, 0, stream>>>(hi, CMapPtrs{}, g, cells, B, lowres, maps, f, R, nxq, n4);
+      with_cc(C, [&](auto cc_c) {
+        constexpr int NSP = decltype(nsp_c)::value, CC = decltype(cc_c)::value;
+        if constexpr (NSP == 2 || CC <= 2)  // (3D with 3-4 channels: the per-element kernel, see above)
+          codec_row4_kernel<T, CODER, decltype(perch_c)::value, NSP, CC, false>
+              <<<ggrid(n4), kGThreads, 0, stream>>>(hi, CMapPtrs{}, g, cells, B, lowres, maps, f, R, nxq, n4);
+      });
     });
     return check_launch("encode_generic");
   }
@@ -789,12 +807,16 @@ static int decode_generic_t(const T* lowres, const CMapPtrs& maps, const Geo& g,
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
-  if (C == 1 && fits32(g, B, C, K)) {  // one channel: 4 output columns a thread
+  if (C <= (nsp == 3 ? 2 : 4) && fits32(g, B, C, K)) {  // 4 output positions (x C) a thread
     const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
     const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
     gen_dispatch<true, T, CODER>(nsp, perch, true, [&](auto nsp_c, auto perch_c, auto) {
-      codec_row4_kernel<T, CODER, decltype(perch_c)::value, decltype(nsp_c)::value, int32_t, true>
-          <<<ggrid(n4), kGThreads, 0, stream>>>(lowres, maps, g, cells, B, hi, MapPtrs{}, f, R, nxq, n4);
+      with_cc(C, [&](auto cc_c) {
+        constexpr int NSP = decltype(nsp_c)::value, CC = decltype(cc_c)::value;
+        if constexpr (NSP == 2 || CC <= 2)
+          codec_row4_kernel<T, CODER, decltype(perch_c)::value, NSP, CC, true>
+              <<<ggrid(n4), kGThreads, 0, stream>>>(lowres, maps, g, cells, B, hi, MapPtrs{}, f, R, nxq, n4);
+      });
     });
     return check_launch("decode_generic");
   }
