@@ -86,6 +86,14 @@ __device__ __forceinline__ T gcast(float v) {
   else return cast_f32<T>(v);
 }
 
+// astype(T) of an f32 LinearPredictor value (kmp_linear.hip lin_cast: the clamp-then-convert form
+// of the saturating conversion for 8- / 16-bit samples, cast_f32 otherwise)
+template <typename T>
+__device__ __forceinline__ T lin_cast_t(float v) {
+  if constexpr (sizeof(T) <= 2) return (T)wv::cvt_sat_mfma<T>(v);
+  else return cast_f32<T>(v);
+}
+
 // the 7 (3) maps' lattice parities (z, y, x) and contributions at compile time (kmp_aggregate.h)
 template <int NSP>
 __device__ __forceinline__ constexpr int gpar(int k, int a) {
@@ -419,11 +427,24 @@ struct Row4 {
 
 // CC channels (1..4, interleaved): a thread owns 4 output positions x CC channels of a row, so
 // its highres rows are 8 x CC consecutive samples, its lowres / map values 4 x CC, its cells 5 x CC
-template <typename T, int CODER, bool PERCH, int NSP, int CC, bool DEC>
+// FK > 0 (images, one channel, f32 LinearPredictor with KK = FK = 2p + 2 <= 4): no cells array --
+// the thread computes the 2 x 5 cells around its outputs itself, from a (FK + 1) x (FK + 4) patch
+// of lowres nodes, with the reference's fma chain (linear_valu_kernel's arithmetic: same bits).
+// Each cell is computed by ~2.5 threads; the cells pass (a write and a re-read of 5 predictions a
+// cell) is gone.
+template <typename T, int CODER, bool PERCH, int NSP, int CC, bool DEC, int FK = 0>
 __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restrict__ src, CMapPtrs imaps, Geo g,
                                                              const T* __restrict__ cells, int64_t B, T* __restrict__ dst,
                                                              MapPtrs omaps, Frame f, Row4 R, int64_t nxq,
-                                                             int64_t total) {
+                                                             int64_t total, Src ns = Src{}, const float* W = nullptr,
+                                                             const float* bias = nullptr, int p = 0) {
+  static_assert(FK == 0 || (NSP == 2 && CC == 1 && PERCH), "fused cells: images, one channel, LinearPredictor");
+  constexpr int FKO = 5, FN = FK * FK;  // outputs / features of a 2D cell
+  __shared__ float wl[FK > 0 ? FN * FKO + FKO : 1];
+  if constexpr (FK > 0) {
+    for (int i = threadIdx.x; i < FN * FKO + FKO; i += blockDim.x) wl[i] = i < FN * FKO ? W[i] : bias[i - FN * FKO];
+    __syncthreads();
+  }
   using I = int32_t;
   using TO = typename coder_out<CODER>::type;
   constexpr int NM = NSP == 3 ? 7 : 3;
@@ -466,8 +487,44 @@ __global__ void __launch_bounds__(kGThreads) codec_row4_kernel(const T* __restri
         }
       }
     // map k's contribution channel kch of the cell (oz - dz, oy - dy, ox0 + i - dx), sample channel ch
+    // FK > 0: the cells (oy - dy, ox0 - 1 + j), channels kch, computed here
+    T pc[FK > 0 ? 2 : 1][FK > 0 ? 5 : 1][FKO];
+    if constexpr (FK > 0) {
+      constexpr int NRW = FK + 1, NCL = FK + 4;  // node patch: rows oy - 1 - p .., cols ox0 - 1 - p ..
+      const I sr = DEC ? (I)g.E[2] : (I)g.n[2];
+      const I sb = DEC ? (I)(g.E[0] * g.E[1] * g.E[2]) : (I)(g.n[0] * g.n[1] * g.n[2]);
+      I col[NCL];
+#pragma unroll
+      for (int c2 = 0; c2 < NCL; ++c2) col[c2] = (I)node_src((int64_t)ox0 - 1 - p + c2, g.L[2], g.E[2], ns.mult);
+      float nd[NRW][NCL];
+#pragma unroll
+      for (int r2 = 0; r2 < NRW; ++r2) {
+        const I rb = b * sb + (I)node_src((int64_t)oy - 1 - p + r2, g.L[1], g.E[1], ns.mult) * sr;
+#pragma unroll
+        for (int c2 = 0; c2 < NCL; ++c2) nd[r2][c2] = (float)src[rb + col[c2]];
+      }
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          float acc[FKO];
+#pragma unroll
+          for (int k = 0; k < FKO; ++k) acc[k] = wl[FN * FKO + k];
+#pragma unroll
+          for (int fy = 0; fy < FK; ++fy)
+#pragma unroll
+            for (int fx = 0; fx < FK; ++fx) {
+              const float fv = nd[1 - dy + fy][j + fx];
+#pragma unroll
+              for (int k = 0; k < FKO; ++k) acc[k] = __builtin_fmaf(fv, wl[(fy * FK + fx) * FKO + k], acc[k]);
+            }
+#pragma unroll
+          for (int k = 0; k < FKO; ++k) pc[dy][j][k] = lin_cast_t<T>(acc[k]);
+        }
+    }
     auto cell = [&](int i, int dz, int dy, int dx, int kch, int ch) -> T {
-      if constexpr (PERCH) return cells[cbase - dz * cz - dy * cy + (i - dx) * CC + ch + (I)kch * kp];
+      if constexpr (FK > 0) return pc[dy][i + 1 - dx][kch];
+      else if constexpr (PERCH) return cells[cbase - dz * cz - dy * cy + (i - dx) * CC + ch + (I)kch * kp];
       else return cm[dz][dy][i + 1 - dx][ch];
     };
     auto pred = [&](int k, int i, int ch) -> uint32_t {
@@ -726,6 +783,19 @@ static int run_predictor(const T* src, const Src& s, const Geo& g, int nsp, int6
   return linear_cells<T>(src, s.S, s.mult, g, nsp, B, C, pred, cbeg, cext, cells, stream);
 }
 
+// Images with one channel and the f32 LinearPredictor at p <= 1: the row kernel computes its cells
+// itself (codec_row4_kernel FK > 0; at p = 2 the 7 x 10 node patch and 36 x 5 weights outgrow the
+// registers); KMP_DISABLE_LINEAR_FUSED=1 keeps the two-pass path
+static bool fuse_lin2d(int nsp, int64_t C, const Geo& g, int64_t B, const kmp_predictor* pred) {
+  return nsp == 2 && C == 1 && pred->kind == KMP_PRED_LINEAR && pred->padding <= 1 && pred->weights && pred->bias &&
+         fits32(g, B, C, 5) && !opt(OPT_DISABLE_LINEAR_FUSED, 0);
+}
+template <typename F>
+static void with_fk(int p, F&& f) {
+  if (p == 0) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 4>{});
+}
+
 // the row kernel's compile-time channel count (1..4; 3D takes 1..2 -- with 3-4 channels its
 // 7 maps' values outgrow the registers and spill)
 template <typename F>
@@ -766,8 +836,18 @@ static int encode_generic_t(const T* hi, const Geo& g, int nsp, int64_t B, int64
   Src s{{g.n[0], g.n[1], g.n[2]}, 2};
   T* cells = (T*)ws;
   Frame f = make_frame(nsp, g, region);
-  if (int st = run_predictor<T>(hi, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   const int64_t total = B * f.ext[0] * f.ext[1] * f.ext[2] * C;
+  if (fuse_lin2d(nsp, C, g, B, pred)) {  // images, f32 LinearPredictor: the cells computed in the row kernel
+    if (total == 0) return KMP_OK;
+    const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
+    const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
+    with_fk(pred->padding, [&](auto fk_c) {
+      codec_row4_kernel<T, CODER, true, 2, 1, false, decltype(fk_c)::value><<<ggrid(n4), kGThreads, 0, stream>>>(
+          hi, CMapPtrs{}, g, nullptr, B, lowres, maps, f, R, nxq, n4, s, pred->weights, pred->bias, pred->padding);
+    });
+    return check_launch("encode_generic");
+  }
+  if (int st = run_predictor<T>(hi, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
@@ -802,8 +882,18 @@ static int decode_generic_t(const T* lowres, const CMapPtrs& maps, const Geo& g,
   Src s{{g.E[0], g.E[1], g.E[2]}, 1};
   T* cells = (T*)ws;
   Frame f = make_frame(nsp, g, region);
-  if (int st = run_predictor<T>(lowres, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   const int64_t total = B * f.ext[0] * f.ext[1] * f.ext[2] * C;
+  if (fuse_lin2d(nsp, C, g, B, pred)) {
+    if (total == 0) return KMP_OK;
+    const int64_t nxq = ceil_div(f.ext[2], 4), n4 = B * f.ext[0] * f.ext[1] * nxq;
+    const Row4 R{fdiv(nxq), fdiv(f.ext[1]), fdiv(f.ext[0])};
+    with_fk(pred->padding, [&](auto fk_c) {
+      codec_row4_kernel<T, CODER, true, 2, 1, true, decltype(fk_c)::value><<<ggrid(n4), kGThreads, 0, stream>>>(
+          lowres, maps, g, nullptr, B, hi, MapPtrs{}, f, R, nxq, n4, s, pred->weights, pred->bias, pred->padding);
+    });
+    return check_launch("decode_generic");
+  }
+  if (int st = run_predictor<T>(lowres, s, g, nsp, B, C, pred, f, cells, stream)) return st;
   if (total == 0) return KMP_OK;
   const bool perch = pred->kind != KMP_PRED_MEAN;
   const int K = perch ? (nsp == 3 ? 19 : 5) : 1;
